@@ -1,0 +1,150 @@
+/*
+ * wos.h -- C ABI of the MI355X walk-on-stars pressure-projection engine.
+ *
+ * This is the drop-in boundary for the one hot path of
+ * Pranav-Jain/Neural-Monte-Carlo-Fluid-Simulation: the zombie / zombie3d WoSt
+ * estimator behind the pybind11 module `zombie_bindings`
+ * (bindings/zombie/demo/demo.cpp:393-401, bindings/zombie3d/demo/demo.cpp:119-125).
+ * Plain pointers and sizes only; no torch / STL types cross this boundary.
+ *
+ * Every function returns WOS_OK (0) or a negative WOS_E* status; the message of
+ * the last failure on the calling thread is available from wos_last_error()
+ * (the reference aborts the interpreter instead: config.h:8-11, scene.h:106-109).
+ */
+#ifndef WOS_H
+#define WOS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WOS_ABI_VERSION 1
+
+enum {
+    WOS_OK = 0,
+    WOS_E_INVALID = -1,     /* bad argument / config value            */
+    WOS_E_IO = -2,          /* file missing / unreadable               */
+    WOS_E_DEVICE = -3,      /* HIP runtime error                       */
+    WOS_E_CAPACITY = -4,    /* scene too large for the LDS-staged path */
+    WOS_E_NOMEM = -5
+};
+
+/* flags for wos_solve */
+#define WOS_PTRS_DEVICE 0x1u   /* pts/p/grad/n_est/steps are device pointers on the scene's device */
+#define WOS_ASYNC       0x2u   /* enqueue on `stream` and return; stats are not filled */
+
+/* A boundary mesh: 2D line segments (dim=2) or 3D triangles (dim=3). */
+typedef struct wos_mesh {
+    int32_t dim;
+    int32_t n_vertices;
+    int32_t n_prims;
+    float *vertices;          /* n_vertices * dim */
+    int32_t *prims;           /* n_prims * dim (0-based vertex indices) */
+} wos_mesh;
+
+/* Replaces Scene::loadOBJ (bindings/zombie/demo/scene.h:104-145, 2D `v`/`l`
+ * lines, flipOrientation swaps segment ends, normalizeDomain recentres) and
+ * zombie::loadSurfaceMesh<3> (include/zombie/utils/fcpw_scene_loader.h:47-73).
+ * Arrays are malloc'd; release with wos_mesh_free. */
+int wos_load_obj(const char *path, int32_t dim, int32_t flip_orientation,
+                 int32_t normalize, wos_mesh *out);
+void wos_mesh_free(wos_mesh *mesh);
+
+typedef struct wos_scene_desc {
+    int32_t dim;                     /* 2 or 3 */
+    const float *vertices;           /* Neumann boundary (the reference's OBJ "boundary") */
+    const int32_t *prims;
+    int32_t n_vertices, n_prims;
+    const float *dvertices;          /* optional Dirichlet boundary (empty in the reference) */
+    const int32_t *dprims;
+    int32_t n_dvertices, n_dprims;
+    float dirichlet_value;           /* constant g on the Dirichlet boundary */
+    float absorption;                /* scene.absorptionCoeff (lambda) */
+    int32_t is_watertight;           /* scene.isWatertight */
+    int32_t is_double_sided;         /* scene.isDoubleSided */
+    const float *source;             /* -div(u) grid: 2D [H][W] (rows ~ y); 3D [X][Y][Z] */
+    int32_t source_dims[3];
+    int32_t source_on_device;        /* source is a device pointer (copied d2d) */
+} wos_scene_desc;
+
+typedef struct wos_scene wos_scene;
+
+/* Replaces Scene::Scene(json, mat) (scene.h:54-77) / Scene(json, mat3d)
+ * (scene_3d.h:22-40): normals, silhouettes (fcpw.inl:224-353, sbvh.inl:313-436),
+ * padded bbox, then uploads geometry + source to `device`. */
+int wos_scene_create(const wos_scene_desc *desc, int32_t device, wos_scene **out);
+int wos_scene_destroy(wos_scene *scene);
+
+typedef struct wos_scene_info {
+    int32_t dim, n_prims, n_silhouettes, n_dprims, device;
+    float bbox_min[3], bbox_max[3];
+} wos_scene_info;
+int wos_scene_get_info(const wos_scene *scene, wos_scene_info *info);
+
+/* Solver / output settings: the keys runWalkOnStars_sampled reads
+ * (demo.cpp:121-137) plus output.boundaryDistanceMask (grid.h:159) and the
+ * counter-based RNG key that replaces the clock seeds. */
+typedef struct wos_solver_params {
+    int32_t n_walks;                        /* nWalks (128) */
+    int32_t max_walk_length;                /* maxWalkLength (1024) */
+    int32_t steps_before_tikhonov;          /* setpsBeforeApplyingTikhonov (maxWalkLength) */
+    int32_t steps_before_maximal_spheres;   /* setpsBeforeUsingMaximalSpheres (maxWalkLength) */
+    float epsilon_shell;                    /* epsilonShell (1e-3) */
+    float min_star_radius;                  /* minStarRadius (1e-3) */
+    float silhouette_precision;             /* silhouettePrecision (1e-3) */
+    float russian_roulette_threshold;       /* russianRouletteThreshold (0) */
+    float boundary_distance_mask;           /* output.boundaryDistanceMask (0) */
+    int32_t disable_gradient_control_variates;
+    int32_t disable_gradient_antithetic_variates;
+    int32_t use_cosine_sampling;            /* useCosineSamplingForDirectionalDerivatives */
+    int32_t ignore_dirichlet;
+    int32_t ignore_neumann;
+    int32_t ignore_source;
+    uint64_t seed;                          /* RNG key */
+} wos_solver_params;
+
+void wos_default_params(wos_solver_params *p);
+
+typedef struct wos_stats {
+    uint64_t walk_steps;        /* ball steps of recorded walks (first ball + walk() iterations) */
+    uint64_t wasted_steps;      /* ball steps of dropped walks (escaped / over max length) */
+    uint64_t walks_recorded;
+    uint64_t walks_escaped;
+    uint64_t walks_max_length;
+    uint64_t walks_rr;
+    uint64_t walks_dirichlet;
+    uint64_t points_estimated;
+    uint64_t rejection_iters;
+    double kernel_ms;           /* device time of the solve kernel (HIP events) */
+} wos_stats;
+
+/* Replaces runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d
+ * (zombie3d/demo/demo.cpp:15-116) for n query points pts[n*dim]:
+ *   p[n]          masked pressure    (grid.h:155-179)
+ *   grad[n*dim]   masked gradient    (grid.h:207-237)
+ *   n_est[n]      recorded walks per point (optional, may be NULL)
+ *   steps[n]      ball steps per point incl. wasted (optional, may be NULL)
+ * The RNG of point i is keyed by the global index index_base + i*index_stride,
+ * so sharding the points across GPUs does not change any result.
+ * `stream` is a hipStream_t (NULL = the device's null stream). */
+int wos_solve(wos_scene *scene, const wos_solver_params *params,
+              const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
+              float *p, float *grad, int32_t *n_est, int32_t *steps,
+              wos_stats *stats, void *stream, uint32_t flags);
+
+/* Device self-test of the deterministic math used by the kernel (for the
+ * GPU-vs-oracle parity tests): which = 0 exp, 1 log, 2 sin, 3 cos, 4 atan,
+ * 5 sqrt, 6 bessi0, 7 bessi1, 8 bessk0, 9 bessk1 (double); 10 expf, 11 logf,
+ * 12 sinf, 13 cosf, 14 cbrtf (float in, float out widened to double). */
+int wos_selftest_math(int32_t which, const double *x, double *out, int64_t n, int32_t device);
+
+const char *wos_last_error(void);
+int32_t wos_abi_version(void);
+int32_t wos_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WOS_H */

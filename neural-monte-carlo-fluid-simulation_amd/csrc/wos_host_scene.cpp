@@ -1,0 +1,320 @@
+// wos_host_scene.cpp -- host-side scene preparation (no GPU work here).
+//
+// Replaces what zombie/fcpw do at Scene construction time:
+//   OBJ parsing        scene.h:104-145 (2D `v`/`l`), fcpw scene_loader.inl:29-150 (3D `f`)
+//   bounding box       fcpw_scene_loader.h:75-93 + bounding_volumes.h:38-49 (FLT_EPSILON pad)
+//   vertex/edge normals fcpw.inl:200-221,298-353
+//   silhouettes        fcpw.inl:224-293, vertex_silhouettes.inl, edge_silhouettes.inl,
+//                      ignore rule sbvh.inl:313-436 + scene.h:84-90
+// and packs everything into the flat records described in wos_scene.h.
+#include "wos_host_scene.h"
+
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+
+#include "wos_detmath.h"
+
+namespace wos {
+
+namespace {
+
+struct V3 { float x[3] = {0.0f, 0.0f, 0.0f}; };
+
+inline float dot3(const V3& a, const V3& b) { return a.x[0] * b.x[0] + a.x[1] * b.x[1] + a.x[2] * b.x[2]; }
+inline V3 sub(const V3& a, const V3& b) { V3 r; for (int k = 0; k < 3; k++) r.x[k] = a.x[k] - b.x[k]; return r; }
+inline V3 cross(const V3& a, const V3& b) {
+  V3 r;
+  r.x[0] = a.x[1] * b.x[2] - a.x[2] * b.x[1];
+  r.x[1] = a.x[2] * b.x[0] - a.x[0] * b.x[2];
+  r.x[2] = a.x[0] * b.x[1] - a.x[1] * b.x[0];
+  return r;
+}
+inline void normalize(V3& v) {  // Eigen normalized()
+  float z = dot3(v, v);
+  if (z > 0.0f) { float s = std::sqrt(z); for (int k = 0; k < 3; k++) v.x[k] = v.x[k] / s; }
+}
+inline V3 seg_normal(const V3& pa, const V3& pb) {  // LineSegment::normal (line_segments.inl:46-55)
+  V3 s = sub(pb, pa), n;
+  n.x[0] = s.x[1]; n.x[1] = -s.x[0]; n.x[2] = 0.0f;
+  return n;
+}
+inline V3 tri_normal(const V3& pa, const V3& pb, const V3& pc) {  // Triangle::normal
+  return cross(sub(pb, pa), sub(pc, pa));
+}
+
+struct Geom {
+  int dim = 0;
+  std::vector<V3> v;
+  std::vector<std::array<int, 3>> ix;
+  std::vector<V3> vn, en;
+  std::vector<std::array<int, 3>> pe;  // 3D edge ids per triangle
+};
+
+bool build_geom(Geom& g, int dim, int nv, int np, const float* v, const int32_t* ix, std::string& err) {
+  g.dim = dim;
+  g.v.resize(nv);
+  g.ix.resize(np);
+  for (int i = 0; i < nv; i++)
+    for (int k = 0; k < dim; k++) g.v[i].x[k] = v[i * dim + k];
+  for (int p = 0; p < np; p++) {
+    g.ix[p] = {0, 0, 0};
+    for (int k = 0; k < dim; k++) {
+      int q = ix[p * dim + k];
+      if (q < 0 || q >= nv) { err = "primitive " + std::to_string(p) + " references vertex out of range"; return false; }
+      g.ix[p][k] = q;
+    }
+  }
+  g.vn.assign(nv, V3());
+  if (dim == 2) {
+    for (int p = 0; p < np; p++) {
+      V3 n = seg_normal(g.v[g.ix[p][0]], g.v[g.ix[p][1]]);
+      normalize(n);
+      for (int k = 0; k < 2; k++)
+        for (int c = 0; c < 3; c++) g.vn[g.ix[p][k]].x[c] += 1.0f * n.x[c];
+    }
+    for (auto& n : g.vn) normalize(n);
+  } else {
+    std::map<std::pair<int, int>, int> emap;
+    g.pe.resize(np);
+    for (int p = 0; p < np; p++)
+      for (int j = 0; j < 3; j++) {
+        int I = g.ix[p][j], J = g.ix[p][(j + 1) % 3];
+        if (I > J) std::swap(I, J);
+        auto key = std::make_pair(I, J);
+        auto it = emap.find(key);
+        int e;
+        if (it == emap.end()) { e = (int)emap.size(); emap[key] = e; } else e = it->second;
+        g.pe[p][j] = e;
+      }
+    g.en.assign(emap.size(), V3());
+    for (int p = 0; p < np; p++) {
+      V3 n = tri_normal(g.v[g.ix[p][0]], g.v[g.ix[p][1]], g.v[g.ix[p][2]]);
+      V3 nu = n;
+      normalize(nu);
+      V3 raw = n;
+      float area = 0.5f * std::sqrt(dot3(raw, raw));
+      for (int j = 0; j < 3; j++) {
+        for (int c = 0; c < 3; c++) g.vn[g.ix[p][j]].x[c] += 1.0f * nu.x[c];
+        for (int c = 0; c < 3; c++) g.en[g.pe[p][j]].x[c] += area * nu.x[c];
+      }
+    }
+    for (auto& n : g.vn) normalize(n);
+    for (auto& n : g.en) normalize(n);
+  }
+  return true;
+}
+
+void pack_prims(const Geom& g, std::vector<float>& prim, std::vector<float>& aux) {
+  const int dim = g.dim, np = (int)g.ix.size();
+  prim.clear(); aux.clear();
+  for (int p = 0; p < np; p++) {
+    for (int k = 0; k < dim; k++)
+      for (int c = 0; c < dim; c++) prim.push_back(g.v[g.ix[p][k]].x[c]);
+    if (dim == 2) {
+      V3 ns = seg_normal(g.v[g.ix[p][0]], g.v[g.ix[p][1]]);
+      normalize(ns);
+      const V3* src[3] = {&g.vn[g.ix[p][0]], &g.vn[g.ix[p][1]], &ns};
+      for (auto* s : src) { aux.push_back(s->x[0]); aux.push_back(s->x[1]); }
+    } else {
+      V3 nf = tri_normal(g.v[g.ix[p][0]], g.v[g.ix[p][1]], g.v[g.ix[p][2]]);
+      normalize(nf);
+      for (int j = 0; j < 3; j++) for (int c = 0; c < 3; c++) aux.push_back(g.vn[g.ix[p][j]].x[c]);
+      for (int j = 0; j < 3; j++) for (int c = 0; c < 3; c++) aux.push_back(g.en[g.pe[p][j]].x[c]);
+      for (int c = 0; c < 3; c++) aux.push_back(nf.x[c]);
+    }
+  }
+}
+
+bool ignore_candidate(float angle, bool double_sided) { return double_sided ? false : angle < 1e-3f; }
+
+// silhouette candidates, in order of first appearance over primitives
+void build_silhouettes(const Geom& g, bool double_sided, std::vector<float>& sil, int& ns) {
+  sil.clear(); ns = 0;
+  const int nv = (int)g.v.size(), np = (int)g.ix.size();
+  if (g.dim == 2) {
+    std::vector<int> prev(nv, -1), next(nv, -1);
+    for (int p = 0; p < np; p++) { next[g.ix[p][0]] = g.ix[p][1]; prev[g.ix[p][1]] = g.ix[p][0]; }
+    std::vector<char> seen(nv, 0);
+    for (int p = 0; p < np; p++)
+      for (int k = 0; k < 2; k++) {
+        int vi = g.ix[p][k];
+        if (seen[vi]) continue;
+        seen[vi] = 1;
+        bool has0 = next[vi] != -1, has1 = prev[vi] != -1;
+        V3 n0, n1;
+        if (has0) { n0 = seg_normal(g.v[vi], g.v[next[vi]]); normalize(n0); }
+        if (has1) { n1 = seg_normal(g.v[prev[vi]], g.v[vi]); normalize(n1); }
+        if (has0 && has1) {
+          float det = n0.x[0] * n1.x[1] - n1.x[0] * n0.x[1];
+          if (ignore_candidate(det, double_sided)) continue;
+        }
+        const float rec[kSilStride2] = {g.v[vi].x[0], g.v[vi].x[1], n0.x[0], n0.x[1], n1.x[0], n1.x[1],
+                                        (has0 && has1) ? 0.0f : 1.0f, 0.0f};
+        sil.insert(sil.end(), rec, rec + kSilStride2);
+        ns++;
+      }
+  } else {
+    const int ne = (int)g.en.size();
+    std::vector<std::array<int, 4>> sidx(ne, {-1, -1, -1, -1});
+    for (int p = 0; p < np; p++)
+      for (int j = 0; j < 3; j++) {
+        int I = j - 1 < 0 ? 2 : j - 1, J = j, K = j + 1 > 2 ? 0 : j + 1;
+        int e = g.pe[p][j];
+        float orientation = 1.0f;
+        if (g.ix[p][J] > g.ix[p][K]) { std::swap(J, K); orientation = -1.0f; }
+        sidx[e][orientation == 1.0f ? 0 : 3] = g.ix[p][I];
+        sidx[e][1] = g.ix[p][J];
+        sidx[e][2] = g.ix[p][K];
+      }
+    std::vector<char> seen(ne, 0);
+    for (int p = 0; p < np; p++)
+      for (int k = 0; k < 3; k++) {
+        int e = g.pe[p][k];
+        if (seen[e]) continue;
+        seen[e] = 1;
+        bool has0 = sidx[e][3] != -1, has1 = sidx[e][0] != -1;
+        V3 n0, n1;
+        const V3 &pa = g.v[sidx[e][1]], &pb = g.v[sidx[e][2]];
+        if (has0) { n0 = cross(sub(pb, pa), sub(g.v[sidx[e][3]], pa)); normalize(n0); }
+        if (has1) { n1 = cross(sub(pa, pb), sub(g.v[sidx[e][0]], pb)); normalize(n1); }
+        if (has0 && has1) {
+          V3 ed = sub(pb, pa);
+          normalize(ed);
+          float ang = fatan2(dot3(ed, cross(n0, n1)), dot3(n0, n1));
+          if (ignore_candidate(ang, double_sided)) continue;
+        }
+        float rec[kSilStride3] = {pa.x[0], pa.x[1], pa.x[2], pb.x[0], pb.x[1], pb.x[2], n0.x[0], n0.x[1],
+                                  n0.x[2], n1.x[0], n1.x[1], n1.x[2], (has0 && has1) ? 0.0f : 1.0f, 0.0f,
+                                  0.0f, 0.0f};
+        sil.insert(sil.end(), rec, rec + kSilStride3);
+        ns++;
+      }
+  }
+}
+
+}  // namespace
+
+bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
+  if (in.dim != 2 && in.dim != 3) { err = "dim must be 2 or 3"; return false; }
+  if (in.n_vertices < 0 || in.n_prims < 0 || in.n_dvertices < 0 || in.n_dprims < 0) {
+    err = "negative mesh size"; return false;
+  }
+  if ((in.n_prims > 0 && (!in.vertices || !in.prims)) || (in.n_dprims > 0 && (!in.dvertices || !in.dprims))) {
+    err = "missing mesh arrays"; return false;
+  }
+  if (in.n_prims == 0 && in.n_dprims == 0) { err = "scene has no boundary primitives"; return false; }
+  out = HostScene();
+  out.dim = in.dim;
+  Geom neu, dir;
+  if (in.n_prims > 0 && !build_geom(neu, in.dim, in.n_vertices, in.n_prims, in.vertices, in.prims, err)) return false;
+  if (in.n_dprims > 0 && !build_geom(dir, in.dim, in.n_dvertices, in.n_dprims, in.dvertices, in.dprims, err))
+    return false;
+  pack_prims(neu, out.prim, out.paux);
+  pack_prims(dir, out.dprim, out.dpaux);
+  out.n_prims = (int)neu.ix.size();
+  out.n_dprims = (int)dir.ix.size();
+  build_silhouettes(neu, in.is_double_sided != 0, out.sil, out.n_sil);
+  // bounding box over all boundary vertices, padded by FLT_EPSILON per vertex
+  for (int k = 0; k < 3; k++) { out.pmin[k] = kFltMax; out.pmax[k] = -kFltMax; }
+  const Geom* gs[2] = {&neu, &dir};
+  for (const Geom* g : gs)
+    for (const V3& v : g->v)
+      for (int k = 0; k < in.dim; k++) {
+        out.pmin[k] = smin(out.pmin[k], v.x[k] - kFltEps);
+        out.pmax[k] = smax(out.pmax[k], v.x[k] + kFltEps);
+      }
+  if (in.dim == 2) { out.pmin[2] = out.pmax[2] = 0.0f; }
+  for (int k = 0; k < 3; k++) out.ext[k] = out.pmax[k] - out.pmin[k];
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// OBJ parsing
+// ---------------------------------------------------------------------------
+static int parse_face_index(const std::string& token) {  // scene_loader.inl:29-44
+  std::stringstream in(token);
+  std::string s;
+  int idx[3] = {1, 1, 1};
+  int i = 0;
+  while (std::getline(in, s, '/')) {
+    if (s != "\\") {
+      std::stringstream ss(s);
+      if (i < 3) ss >> idx[i++];
+    }
+  }
+  return idx[0] - 1;
+}
+
+bool load_obj(const std::string& path, int dim, bool flip, bool normalize_domain, std::vector<float>& verts,
+              std::vector<int32_t>& prims, std::string& err) {
+  std::ifstream obj(path);
+  if (!obj) { err = "Error opening file: " + path; return false; }
+  verts.clear(); prims.clear();
+  std::string line;
+  if (dim == 2) {
+    // scene.h:104-145
+    while (std::getline(obj, line)) {
+      std::istringstream ss(line);
+      std::string token;
+      ss >> token;
+      if (token == "v") {
+        float x = 0.0f, y = 0.0f;
+        ss >> x >> y;
+        verts.push_back(x); verts.push_back(y);
+      } else if (token == "l") {
+        size_t i = 0, j = 0;
+        ss >> i >> j;
+        if (flip) { prims.push_back((int32_t)(j - 1)); prims.push_back((int32_t)(i - 1)); }
+        else { prims.push_back((int32_t)(i - 1)); prims.push_back((int32_t)(j - 1)); }
+      }
+    }
+  } else {
+    // fcpw loadTriangleSoupFromOBJFile (scene_loader.inl:100-150)
+    while (std::getline(obj, line)) {
+      std::stringstream ss(line);
+      std::string token;
+      ss >> token;
+      if (token == "v") {
+        float x = 0.0f, y = 0.0f, z = 0.0f;
+        ss >> x >> y >> z;
+        verts.push_back(x); verts.push_back(y); verts.push_back(z);
+      } else if (token == "f") {
+        while (ss >> token) {
+          int pos = parse_face_index(token);
+          if (pos < 0) {
+            if (!std::getline(obj, line)) break;
+            size_t i = line.find_first_not_of("\t\n\v\f\r ");
+            if (i == std::string::npos) continue;
+            pos = parse_face_index(line.substr(i));
+          }
+          prims.push_back(pos);
+        }
+      }
+    }
+    if (prims.size() % 3 != 0) { err = "OBJ face index count is not a multiple of 3 (triangles only)"; return false; }
+    if (flip)
+      for (size_t t = 0; t < prims.size(); t += 3) std::swap(prims[t + 1], prims[t + 2]);
+  }
+  const int nv = (int)(verts.size() / dim);
+  for (int32_t q : prims)
+    if (q < 0 || q >= nv) { err = "OBJ index out of range in " + path; return false; }
+  if (normalize_domain && nv > 0) {
+    // scene.h:132-142
+    float cm[3] = {0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < nv; i++) for (int k = 0; k < dim; k++) cm[k] += verts[i * dim + k];
+    for (int k = 0; k < dim; k++) cm[k] /= (float)nv;
+    float radius = 0.0f;
+    for (int i = 0; i < nv; i++) {
+      float s = 0.0f;
+      for (int k = 0; k < dim; k++) { verts[i * dim + k] -= cm[k]; s += verts[i * dim + k] * verts[i * dim + k]; }
+      radius = smax(radius, std::sqrt(s));
+    }
+    for (int i = 0; i < nv; i++) for (int k = 0; k < dim; k++) verts[i * dim + k] /= radius;
+  }
+  return true;
+}
+
+}  // namespace wos

@@ -1,0 +1,1153 @@
+// wos_kernel.hip -- gfx950 walk-on-stars solve kernel.
+//
+// One wavefront (64 lanes) owns one query point at a time; lane l runs
+// antithetic pair l of that point (both members, sharing the pair's walk
+// stream, walk_on_stars.h:494-616).  Neumann segments/triangles and the
+// silhouette candidates are staged in LDS once per workgroup and scanned
+// brute-force (every lane reads the same LDS word: broadcast, no conflicts).
+// The per-point statistics (Welford means with sequential control variates,
+// walk_on_stars.h:500-506,744-877) are folded in walk order by lanes 0..DIM
+// in lockstep so the result is bit-identical to the sequential CPU oracle.
+// Points are handed out by a device-scope atomic work counter (one returning
+// atomicAdd per point), so uneven per-point cost (near-wall points run longer
+// walks) does not leave waves idle at the tail.
+//
+// Numerics follow the reference operation by operation: float state, double
+// Bessel evaluations rounded to float members (distributions.h:573-696), double
+// 2*pi divisors, Eigen's float-scalar conversions -- see the oracle restatement
+// (oracle/wos_oracle.c) which is the parity checker for this file.
+
+#include "wos_detmath.h"
+#include "wos_scene.h"
+
+namespace wos {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kChunkPairs = kWave;        // pairs per statistics chunk
+
+enum { WC_DIRICHLET = 0, WC_RR = 1, WC_MAXLEN = 2, WC_ESCAPED = 3 };
+
+// counters[] slots
+enum { C_STEPS = 0, C_WASTED, C_REC, C_ESC, C_MAXL, C_RR, C_DIR, C_PTS, C_ITERS, C_NUM };
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int DIM>
+__device__ __forceinline__ float dotv(const float* a, const float* b) {
+  float s = a[0] * b[0] + a[1] * b[1];
+  if constexpr (DIM == 3) s = s + a[2] * b[2];
+  return s;
+}
+template <int DIM>
+__device__ __forceinline__ float normv(const float* a) { return __builtin_sqrtf(dotv<DIM>(a, a)); }
+
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  r[0] = x; r[1] = y; r[2] = z;
+}
+
+// Eigen normalized(): v / sqrt(|v|^2) when |v|^2 > 0
+template <int DIM>
+__device__ __forceinline__ void normalize_div(float* v) {
+  float z = dotv<DIM>(v, v);
+  if (z > 0.0f) { float s = __builtin_sqrtf(z); for (int k = 0; k < DIM; k++) v[k] = v[k] / s; }
+}
+// enoki::normalize restated: v * (1/sqrt(|v|^2))
+template <int DIM>
+__device__ __forceinline__ void normalize_rcp(float* v) {
+  float inv = 1.0f / __builtin_sqrtf(dotv<DIM>(v, v));
+  for (int k = 0; k < DIM; k++) v[k] = v[k] * inv;
+}
+
+// ---------------------------------------------------------------------------
+// geometry queries (brute force over LDS / global arrays)
+// ---------------------------------------------------------------------------
+
+// wide closest point on a segment (wide_query_operations.h:121-141)
+template <int DIM>
+__device__ __forceinline__ float cp_segment(const float* pa, const float* pb, const float* x, float* pt, float* t) {
+  float u[DIM], v[DIM];
+  for (int k = 0; k < DIM; k++) { u[k] = pb[k] - pa[k]; v[k] = x[k] - pa[k]; }
+  float c1 = dotv<DIM>(u, v), c2 = dotv<DIM>(u, u);
+  float tt = c1 * (1.0f / c2);
+  if (c1 <= 0.0f) tt = 0.0f;
+  if (c2 <= c1) tt = 1.0f;
+  float d[DIM];
+  for (int k = 0; k < DIM; k++) { pt[k] = pa[k] + u[k] * tt; d[k] = x[k] - pt[k]; }
+  *t = tt;
+  return normv<DIM>(d);
+}
+
+// wide closest point on a triangle (wide_query_operations.h:144-235)
+__device__ __forceinline__ float cp_triangle(const float* pa, const float* pb, const float* pc, const float* x,
+                                             float* pt, float* t0, float* t1) {
+  float ab[3], ac[3], ax[3], d[3];
+  for (int k = 0; k < 3; k++) { ab[k] = pb[k] - pa[k]; ac[k] = pc[k] - pa[k]; ax[k] = x[k] - pa[k]; }
+  float d1 = dotv<3>(ab, ax), d2 = dotv<3>(ac, ax);
+  if (d1 <= 0.0f && d2 <= 0.0f) {
+    for (int k = 0; k < 3; k++) { pt[k] = pa[k]; d[k] = x[k] - pt[k]; }
+    *t0 = 1.0f; *t1 = 0.0f; return normv<3>(d);
+  }
+  float bx[3]; for (int k = 0; k < 3; k++) bx[k] = x[k] - pb[k];
+  float d3 = dotv<3>(ab, bx), d4 = dotv<3>(ac, bx);
+  if (d3 >= 0.0f && d4 <= d3) {
+    for (int k = 0; k < 3; k++) { pt[k] = pb[k]; d[k] = x[k] - pt[k]; }
+    *t0 = 0.0f; *t1 = 1.0f; return normv<3>(d);
+  }
+  float cx[3]; for (int k = 0; k < 3; k++) cx[k] = x[k] - pc[k];
+  float d5 = dotv<3>(ab, cx), d6 = dotv<3>(ac, cx);
+  if (d6 >= 0.0f && d5 <= d6) {
+    for (int k = 0; k < 3; k++) { pt[k] = pc[k]; d[k] = x[k] - pt[k]; }
+    *t0 = 0.0f; *t1 = 0.0f; return normv<3>(d);
+  }
+  float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0f && d1 >= 0.0f && d3 <= 0.0f) {
+    float v = d1 * (1.0f / (d1 - d3));
+    for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ab[k] * v; d[k] = x[k] - pt[k]; }
+    *t0 = 1.0f - v; *t1 = v; return normv<3>(d);
+  }
+  float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) {
+    float w = d2 * (1.0f / (d2 - d6));
+    for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ac[k] * w; d[k] = x[k] - pt[k]; }
+    *t0 = 1.0f - w; *t1 = 0.0f; return normv<3>(d);
+  }
+  float va = d3 * d6 - d5 * d4;
+  if (va <= 0.0f && (d4 - d3) >= 0.0f && (d5 - d6) >= 0.0f) {
+    float w = (d4 - d3) * (1.0f / ((d4 - d3) + (d5 - d6)));
+    for (int k = 0; k < 3; k++) { pt[k] = pb[k] + (pc[k] - pb[k]) * w; d[k] = x[k] - pt[k]; }
+    *t0 = 0.0f; *t1 = 1.0f - w; return normv<3>(d);
+  }
+  float denom = 1.0f / (va + vb + vc);
+  float v = vb * denom, w = vc * denom;
+  for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ab[k] * v + ac[k] * w; d[k] = x[k] - pt[k]; }
+  *t0 = 1.0f - v - w; *t1 = v;
+  return normv<3>(d);
+}
+
+template <int DIM>
+__device__ __forceinline__ float cp_prim(const float* P, const float* x, float* pt, float* t0, float* t1) {
+  if constexpr (DIM == 2) { *t1 = 0.0f; return cp_segment<2>(P, P + 2, x, pt, t0); }
+  else return cp_triangle(P, P + 3, P + 6, x, pt, t0, t1);
+}
+
+struct Closest { float d; float p[3]; float t0, t1; int prim; };
+
+// Wave-cooperative closest point over `np` primitives (key fl(d*d), last index
+// wins ties, mbvh.inl:1297-1351); the result is uniform across the wave.
+template <int DIM>
+__device__ Closest closest_wave(const float* prims, int np, const float* x, int lane) {
+  constexpr int PS = Layout<DIM>::prim;
+  float bk = kFltMax; int bi = -1;
+  for (int p = lane; p < np; p += kWave) {
+    float pt[DIM], t0, t1;
+    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+    float d2 = d * d;
+    if (d2 <= bk) { bk = d2; bi = p; }
+  }
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    float ok = __shfl_xor(bk, off);
+    int oi = __shfl_xor(bi, off);
+    if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
+  }
+  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
+  c.p[0] = c.p[1] = c.p[2] = 0.0f;
+  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
+  return c;
+}
+
+// Interaction::computeNormal via normal(uv) (line_segments.inl:57-73, triangles.inl:61-89)
+template <int DIM>
+__device__ __forceinline__ void closest_normal(const float* aux, const Closest& c, float* n) {
+  constexpr int AS = Layout<DIM>::aux;
+  const float* A = aux + c.prim * AS;
+  if constexpr (DIM == 2) {
+    const float* src = (c.t0 <= kFltEps) ? A : (c.t0 >= 1.0f - kFltEps) ? A + 2 : A + 4;
+    n[0] = src[0]; n[1] = src[1];
+  } else {
+    float u0 = c.t0, u1 = c.t1;
+    int vI = -1, eI = -1;
+    if (u0 >= 1.0f - kFltEps && u1 <= kFltEps) vI = 0;
+    else if (u0 <= kFltEps && u1 >= 1.0f - kFltEps) vI = 1;
+    else if (u0 <= kFltEps && u1 <= kFltEps) vI = 2;
+    if (vI == -1) {
+      if (u0 <= kFltEps) eI = 1;
+      else if (u1 <= kFltEps) eI = 2;
+      else if (u0 + u1 >= 1.0f - kFltEps) eI = 0;
+    }
+    const float* src = vI >= 0 ? A + 3 * vI : eI >= 0 ? A + 9 + 3 * eI : A + 18;
+    n[0] = src[0]; n[1] = src[1]; n[2] = src[2];
+  }
+}
+
+template <int DIM>
+__device__ __forceinline__ float signed_dist(const float* aux, const Closest& c, const float* x) {
+  float n[DIM], d[DIM];
+  closest_normal<DIM>(aux, c, n);
+  for (int k = 0; k < DIM; k++) d[k] = x[k] - c.p[k];
+  return (dotv<DIM>(d, n) > 0.0f ? 1.0f : -1.0f) * c.d;
+}
+
+// computeDistToDirichlet without Dirichlet geometry: far bbox corner
+// (fcpw_scene_loader.h:312-314, bounding_volumes.h:64-69)
+template <int DIM>
+__device__ __forceinline__ float bbox_far_dist(const DevScene& sc, const float* x) {
+  float m[DIM];
+  for (int k = 0; k < DIM; k++) m[k] = smin(sc.pmin[k] - x[k], x[k] - sc.pmax[k]);
+  return __builtin_sqrtf(dotv<DIM>(m, m));
+}
+
+// per-lane (non-cooperative) closest distance to the Dirichlet boundary
+template <int DIM>
+__device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
+  if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
+  constexpr int PS = Layout<DIM>::prim;
+  float sr2 = kFltMax, best = kFltMax;
+  for (int p = 0; p < sc.n_dprims; p++) {
+    float pt[DIM], t0, t1;
+    float d = cp_prim<DIM>(sc.dprim + p * PS, x, pt, &t0, &t1);
+    float d2 = d * d;
+    if (d2 <= sr2) { sr2 = d2; best = d; }
+  }
+  return best;
+}
+
+struct Hit { float p[3], n[3], d; };
+
+// first ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92)
+template <int DIM>
+__device__ __forceinline__ bool ray_hit(const float* prims, int np, const float* o, const float* dir,
+                                        float tmax, Hit* h) {
+  constexpr int PS = Layout<DIM>::prim;
+  bool found = false;
+  float rt = tmax;
+  for (int p = 0; p < np; p++) {
+    const float* P = prims + p * PS;
+    if constexpr (DIM == 2) {
+      float u0 = P[0] - o[0], u1 = P[1] - o[1];
+      float v0 = P[2] - P[0], v1 = P[3] - P[1];
+      float dv = dir[0] * v1 - dir[1] * v0;
+      if (!(__builtin_fabsf(dv) > kFltEps)) continue;
+      float inv = 1.0f / dv;
+      float t = (u0 * dir[1] - u1 * dir[0]) * inv;
+      if (!(t >= 0.0f && t <= 1.0f)) continue;
+      float d = (u0 * v1 - u1 * v0) * inv;
+      if (!(d >= 0.0f && d <= rt)) continue;
+      rt = d; found = true;
+      h->d = d;
+      h->p[0] = P[0] + t * v0; h->p[1] = P[1] + t * v1;
+      h->n[0] = v1; h->n[1] = -v0;
+    } else {
+      float v1[3], v2[3], pp[3], s[3], q[3];
+      for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; s[k] = o[k] - P[k]; }
+      cross3(pp, dir, v2);
+      float det = dotv<3>(v1, pp);
+      if (!(__builtin_fabsf(det) > kFltEps)) continue;
+      float inv = 1.0f / det;
+      float v = dotv<3>(s, pp) * inv;
+      if (!(v >= 0.0f && v <= 1.0f)) continue;
+      cross3(q, s, v1);
+      float w = dotv<3>(dir, q) * inv;
+      if (!(w >= 0.0f && v + w <= 1.0f)) continue;
+      float d = dotv<3>(v2, q) * inv;
+      if (!(d >= 0.0f && d <= rt)) continue;
+      rt = d; found = true;
+      h->d = d;
+      for (int k = 0; k < 3; k++) h->p[k] = P[k] + v1[k] * v + v2[k] * w;
+      cross3(h->n, v1, v2);
+    }
+  }
+  if (found) normalize_rcp<DIM>(h->n);
+  return found;
+}
+
+// occlusion-only ray test (hasLineOfSight, primitive.h:225-235)
+template <int DIM>
+__device__ bool ray_occluded(const float* prims, int np, const float* o, const float* dir, float tmax) {
+  Hit h;
+  return ray_hit<DIM>(prims, np, o, dir, tmax, &h);
+}
+
+// isWideSilhouetteVertex / isWideSilhouetteEdge (wide_query_operations.h:328-395)
+template <int DIM>
+__device__ __forceinline__ bool is_silhouette(const float* S, const float* view, float d, bool flip, float prec) {
+  float sign = flip ? 1.0f : -1.0f;
+  const float* n0 = DIM == 2 ? S + 2 : S + 6;
+  const float* n1 = DIM == 2 ? S + 4 : S + 9;
+  if (!(d > prec)) {
+    if constexpr (DIM == 2) {
+      float det = n0[0] * n1[1] - n0[1] * n1[0];
+      return sign * det > prec;
+    } else {
+      float ed[3], c[3];
+      for (int k = 0; k < 3; k++) ed[k] = S[3 + k] - S[k];
+      normalize_rcp<3>(ed);
+      cross3(c, n0, n1);
+      float ang = fatan2(dotv<3>(ed, c), dotv<3>(n0, n1));
+      return sign * ang > prec;
+    }
+  }
+  float inv = 1.0f / d;
+  float u[DIM];
+  for (int k = 0; k < DIM; k++) u[k] = view[k] * inv;
+  float dot0 = dotv<DIM>(u, n0), dot1 = dotv<DIM>(u, n1);
+  if (__builtin_fabsf(dot0) <= prec) return sign * dot1 > prec;
+  if (__builtin_fabsf(dot1) <= prec) return sign * dot0 > prec;
+  return dot0 * dot1 < 0.0f;
+}
+
+// computeStarRadius (fcpw_scene_loader.h:621-641), brute-force closest silhouette
+template <int DIM>
+__device__ __forceinline__ float star_radius(const float* sil, int ns, int np, const float* x, float minR,
+                                             float maxR, float prec, bool flipOrient) {
+  constexpr int SS = Layout<DIM>::sil;
+  if (minR > maxR) return maxR;
+  if (np > 0) {
+    bool flip = !flipOrient;
+    float r2 = maxR < kFltMax ? maxR * maxR : kFltMax;
+    float minR2 = minR * minR;
+    bool found = false;
+    float best = 0.0f;
+    if (!(minR2 >= r2)) {
+      for (int s = 0; s < ns; s++) {
+        const float* S = sil + s * SS;
+        float view[DIM], d;
+        if constexpr (DIM == 2) {
+          view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
+          d = normv<2>(view);
+        } else {
+          float pt[3], t;
+          d = cp_segment<3>(S, S + 3, x, pt, &t);
+          for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
+        }
+        float d2 = d * d;
+        if (d2 > r2) continue;
+        const float miss = DIM == 2 ? S[6] : S[12];
+        bool sil_ok = miss != 0.0f ? true : is_silhouette<DIM>(S, view, d, flip, prec);
+        if (sil_ok && d2 <= r2) {
+          r2 = d2; best = d; found = true;
+          if (minR2 >= r2) break;
+        }
+      }
+    }
+    if (found) return smax(best, minR);
+  }
+  return smax(maxR, minR);
+}
+
+// offsetPointAlongDirection (fcpw_scene_loader.h:258-290)
+template <int DIM>
+__device__ __forceinline__ void offset_point(const float* p, const float* n, float* out) {
+  const float origin = 1.0f / 32.0f, floatScale = 1.0f / 65536.0f, intScale = 256.0f;
+  for (int k = 0; k < DIM; k++) {
+    int no = cvt_trunc(n[k] * intScale);
+    float po = bits_to_float((uint32_t)((int32_t)float_to_bits(p[k]) + (p[k] < 0 ? -no : no)));
+    out[k] = __builtin_fabsf(p[k]) < origin ? p[k] + floatScale * n[k] : po;
+  }
+}
+
+// PDE source lookup: scene.h:194-198 + image.h:53-58 (2D), scene_3d.h:120-126 (3D)
+template <int DIM>
+__device__ __forceinline__ float source_value(const DevScene& sc, const float* x) {
+  if (sc.source == nullptr) return 0.0f;
+  if constexpr (DIM == 2) {
+    float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
+    float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
+    int h = sc.sdims[0], w = sc.sdims[1];
+    int i = sclamp(cvt_trunc(uy * (float)h), 0, h - 1);
+    int j = sclamp(cvt_trunc(ux * (float)w), 0, w - 1);
+    return sc.source[(size_t)i * w + j];
+  } else {
+    int X = sc.sdims[0], Y = sc.sdims[1], Z = sc.sdims[2];
+    float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
+    float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
+    float uz = (x[2] - sc.pmin[2]) / sc.ext[2];
+    int i = sclamp(cvt_trunc(ux * (float)X), 0, X - 1);
+    int j = sclamp(cvt_trunc(uy * (float)Y), 0, Y - 1);
+    int k = sclamp(cvt_trunc(uz * (float)Z), 0, Z - 1);
+    return sc.source[((size_t)i * Y + j) * Z + k];
+  }
+}
+
+template <int DIM>
+__device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x) {
+  for (int k = 0; k < DIM; k++)
+    if (!(x[k] >= sc.pmin[k] && x[k] <= sc.pmax[k])) return true;
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// Green's functions on balls (distributions.h:273-832)
+// ---------------------------------------------------------------------------
+template <int DIM>
+struct Gfn {
+  bool yukawa;
+  float c[DIM], yVol[DIM], ySurf[DIM];
+  float R, r;
+  float lambda, sqrtLambda;
+  float muR, A0, A1, B0, B1;   // 2D: K0muR I0muR K1muR I1muR ; 3D: expmuR sinhmuR K32muR I32muR
+  static constexpr float rClamp = 1e-4f;
+
+  __device__ __forceinline__ void init(bool yuk, float lam) {
+    yukawa = yuk; lambda = lam; sqrtLambda = __builtin_sqrtf(lam);
+  }
+
+  __device__ __forceinline__ void update_ball(const float* cc, float RR) {
+    for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
+    R = RR; r = 0.0f;
+    if (!yukawa) return;
+    muR = R * sqrtLambda;
+    if constexpr (DIM == 2) {
+      A0 = (float)bessk0((double)muR);
+      A1 = (float)bessi0((double)muR);
+      B0 = (float)bessk1((double)muR);
+      B1 = (float)bessi1((double)muR);
+    } else {
+      float expmuR = fexp(-muR);
+      float exp2muR = expmuR * expmuR;
+      float coshmuR = (1.0f + exp2muR) / (2.0f * expmuR);
+      float sinhmuR = (1.0f - exp2muR) / (2.0f * expmuR);
+      A0 = expmuR; A1 = sinhmuR;
+      B0 = expmuR * (1.0f + 1.0f / muR);
+      B1 = coshmuR - sinhmuR / muR;
+    }
+  }
+
+  // G(r) for the current r (evaluate())
+  __device__ __forceinline__ float evaluate() const {
+    if (!yukawa) {
+      if constexpr (DIM == 2) return (float)((double)flog(R / r) / kTwoPi);
+      else return (float)((double)(1.0f / r - 1.0f / R) / kFourPi);
+    }
+    float mur = r * sqrtLambda;
+    if constexpr (DIM == 2) {
+      float K0mur = (float)bessk0((double)mur);
+      float I0mur = (float)bessi0((double)mur);
+      return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
+    } else {
+      float expmur = fexp(-mur);
+      float sinhmur = (1.0f - expmur * expmur) / (2.0f * expmur);
+      return (float)((double)(expmur - A0 * sinhmur / A1) / (kFourPi * (double)r));
+    }
+  }
+
+  __device__ __forceinline__ float poisson_kernel() const {
+    if (!yukawa) return DIM == 2 ? (float)(1.0 / kTwoPi) : (float)(1.0 / kFourPi);
+    if constexpr (DIM == 2) return (float)(1.0 / (kTwoPi * (double)A1));
+    else return (float)((double)muR / (kFourPi * (double)A1));
+  }
+
+  __device__ __forceinline__ float norm() const {
+    if (!yukawa) return DIM == 2 ? R * R / 4.0f : R * R / 6.0f;
+    double pk = (double)poisson_kernel();
+    return (float)((1.0 - (DIM == 2 ? kTwoPi : kFourPi) * pk) / (double)lambda);
+  }
+
+  __device__ __forceinline__ float gradient_norm() const {
+    if (!yukawa) {
+      if constexpr (DIM == 2) { float r2 = r * r; return (float)((double)(1.0f / r2 - 1.0f / (R * R)) / kTwoPi); }
+      else { float r3 = r * r * r; return (float)((double)(1.0f / r3 - 1.0f / (R * R * R)) / kFourPi); }
+    }
+    float mur = r * sqrtLambda;
+    if constexpr (DIM == 2) {
+      float K1mur = (float)bessk1((double)mur);
+      float I1mur = (float)bessi1((double)mur);
+      float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
+      return (float)((double)Qr / (kTwoPi * (double)r));
+    } else {
+      float r2 = r * r;
+      float expmur = fexp(-mur);
+      float exp2mur = expmur * expmur;
+      float coshmur = (1.0f + exp2mur) / (2.0f * expmur);
+      float sinhmur = (1.0f - exp2mur) / (2.0f * expmur);
+      float K32mur = expmur * (1.0f + 1.0f / mur);
+      float I32mur = coshmur - sinhmur / mur;
+      float Qr = sqrtLambda * (K32mur - I32mur * B0 / B1);
+      return (float)((double)Qr / (kFourPi * (double)r2));
+    }
+  }
+
+  __device__ __forceinline__ void gradient(float* out) const {
+    float gn = gradient_norm();
+    for (int k = 0; k < DIM; k++) out[k] = (yVol[k] - c[k]) * gn;
+  }
+
+  __device__ __forceinline__ void poisson_kernel_gradient(float* out) const {
+    float d[DIM];
+    for (int k = 0; k < DIM; k++) d[k] = ySurf[k] - c[k];
+    if (!yukawa) {
+      if constexpr (DIM == 2) {
+        float s = (float)((kTwoPi * (double)R) * (double)R);
+        for (int k = 0; k < 2; k++) out[k] = (2.0f * d[k]) / s;
+      } else {
+        float s = (float)((kFourPi * (double)R) * (double)R);
+        for (int k = 0; k < 3; k++) out[k] = (3.0f * d[k]) / s;
+      }
+      return;
+    }
+    if constexpr (DIM == 2) {
+      float QR = sqrtLambda / (R * B1);
+      for (int k = 0; k < 2; k++) out[k] = (d[k] * QR) / (float)kTwoPi;
+    } else {
+      float QR = lambda / B1;
+      for (int k = 0; k < 3; k++) out[k] = (d[k] * QR) / (float)kFourPi;
+    }
+  }
+
+  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y) const {
+    if (!yukawa) return 1.0f;
+    float d[DIM];
+    for (int k = 0; k < DIM; k++) d[k] = y[k] - c[k];
+    float rr = smax(rClamp, normv<DIM>(d));
+    float mur = rr * sqrtLambda;
+    if constexpr (DIM == 2) {
+      float K1mur = (float)bessk1((double)mur);
+      float I1mur = (float)bessi1((double)mur);
+      float Q = K1mur + I1mur * A0 / A1;
+      return mur * Q;
+    } else {
+      float expmur = fexp(-mur);
+      float exp2mur = expmur * expmur;
+      float coshmur = (1.0f + exp2mur) / (2.0f * expmur);
+      float sinhmur = (1.0f - exp2mur) / (2.0f * expmur);
+      float K32mur = expmur * (1.0f + 1.0f / mur);
+      float I32mur = coshmur - sinhmur / mur;
+      float Q = K32mur + I32mur * A0 / A1;
+      return mur * Q;
+    }
+  }
+
+  // off-centred G(x,y): only reached in the non-finite (NaN-propagation) regime
+  __device__ float evaluate_xy(const float* x, const float* y) const {
+    float yx[DIM], xc[DIM], yc[DIM];
+    for (int k = 0; k < DIM; k++) { yx[k] = y[k] - x[k]; xc[k] = x[k] - c[k]; yc[k] = y[k] - c[k]; }
+    if (!yukawa) {
+      float rr = smax(rClamp, normv<DIM>(yx));
+      if constexpr (DIM == 2) return (float)((double)(flog(R * R - dotv<2>(xc, yc)) - flog(R * rr)) / kTwoPi);
+      else return (float)((double)(1.0f / rr - R / (R * R - dotv<3>(xc, yc))) / kFourPi);
+    }
+    float r1 = smax(rClamp, normv<DIM>(yx));
+    float r2 = (R * R - dotv<DIM>(xc, yc)) / R;
+    float mur1 = r1 * sqrtLambda, mur2 = r2 * sqrtLambda;
+    if constexpr (DIM == 2) {
+      float K0mur1 = (float)bessk0((double)mur1), K0mur2 = (float)bessk0((double)mur2);
+      float I0mur1 = (float)bessi0((double)mur1), I0mur2 = (float)bessi0((double)mur2);
+      float Q1 = K0mur1 - I0mur1 * A0 / A1;
+      float Q2 = K0mur2 - I0mur2 * A0 / A1;
+      return (float)((double)(Q1 - Q2) / kTwoPi);
+    } else {
+      float e1 = fexp(-mur1), e2 = fexp(-mur2);
+      float s1 = (1.0f - e1 * e1) / (2.0f * e1), s2 = (1.0f - e2 * e2) / (2.0f * e2);
+      float Q1 = (e1 - A0 * s1 / A1) / r1;
+      float Q2 = (e2 - A0 * s2 / A1) / r2;
+      return (float)((double)(Q1 - Q2) / kFourPi);
+    }
+  }
+};
+
+template <int DIM>
+__device__ __forceinline__ float pdf_sphere_uniform(float r) {
+  if constexpr (DIM == 2) return (float)(1.0 / (kTwoPi * (double)r));
+  else return (float)(1.0 / ((kFourPi * (double)r) * (double)r));
+}
+
+template <int DIM>
+__device__ __forceinline__ void sample_unit_sphere(const float* u, float* out) {
+  if constexpr (DIM == 2) {
+    float phi = (float)(kTwoPi * (double)u[0]);
+    fsincos(phi, &out[1], &out[0]);
+  } else {
+    float z = 1.0f - 2.0f * u[0];
+    float r = __builtin_sqrtf(smax(0.0f, 1.0f - z * z));
+    float phi = (float)(kTwoPi * (double)u[1]);
+    float s, c;
+    fsincos(phi, &s, &c);
+    out[0] = r * c; out[1] = r * s; out[2] = z;
+  }
+}
+
+// sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720)
+template <int DIM>
+__device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg32& s, float* pdf, float* out,
+                                              uint32_t* iters) {
+  const float R = g.R;
+  if (DIM == 3 && !g.yukawa) {
+    float u1 = s.nextf(), u2 = s.nextf();
+    float phi = (float)(kTwoPi * (double)u2);
+    float r = (1.0f + __builtin_sqrtf(1.0f - fcbrt(u1 * u1)) * fcos(phi)) * R / 2.0f;
+    r = smax(Gfn<DIM>::rClamp, r);
+    if (r > R) r = R / 2.0f;
+    g.r = r;
+    for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + r * dir[k]; out[k] = g.yVol[k]; }
+    *pdf = g.evaluate() / g.norm();
+    return;
+  }
+  float bound;
+  if (!g.yukawa) {
+    bound = 1.5f / R;
+  } else {
+    const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
+    const float lam = g.lambda, sl = g.sqrtLambda;
+    bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
+                     : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
+  }
+  // norm() depends only on the ball: hoisted out of the loop (same value every iteration)
+  const float nrm = g.norm();
+  int iter = 0;
+  float p = 0.0f;
+  do {
+    float u = s.nextf();
+    g.r = s.nextf() * R;
+    p = g.evaluate() / nrm;
+    float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
+    iter++;
+    if (u < pdfRadius / bound) break;
+  } while (iter < 1000);
+  *pdf = p;
+  *iters += (uint32_t)iter;
+  g.r = smax(Gfn<DIM>::rClamp, g.r);
+  if (g.r > R) g.r = R / 2.0f;
+  for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
+}
+
+// ---------------------------------------------------------------------------
+// walk (walk_on_stars.h:135-329)
+// ---------------------------------------------------------------------------
+template <int DIM>
+struct WalkState {
+  float pt[DIM], n[DIM], prevDir[DIM];
+  float prevDist, throughput;
+  bool onNeumann;
+  int walkLength;
+  float totalNeumann, totalSource, firstSource;
+  float sdir[DIM], bdir[DIM];
+};
+
+template <int DIM>
+__device__ __forceinline__ float prim_area(const float* P) {
+  if constexpr (DIM == 2) {
+    float s[2] = {P[2] - P[0], P[3] - P[1]};
+    return normv<2>(s);
+  } else {
+    float v1[3], v2[3], n[3];
+    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; }
+    cross3(n, v1, v2);
+    return 0.5f * normv<3>(n);
+  }
+}
+
+// Neumann boundary sample (walk_on_stars.h:212-260).  With the reference's h == 0
+// (scene.h:176-181) the term is exactly +0 unless G or the throughput is
+// non-finite; only then the brute-force stochastic sample is evaluated.
+template <int DIM>
+__device__ __noinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM>& g,
+                                          WalkState<DIM>& st, float R, const float* rn) {
+  constexpr int PS = Layout<DIM>::prim;
+  const int np = sc.n_prims;
+  const float* x = st.pt;
+  float total = 0.0f;
+  for (int p = 0; p < np; p++) {
+    float pt[DIM], t0, t1;
+    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+    if (d * d <= R * R) {
+      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
+      total += prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
+    }
+  }
+  if (!(total > 0.0f)) return;
+  float target = rn[0] * total, acc = 0.0f, selw = 0.0f;
+  int sel = -1;
+  for (int p = 0; p < np; p++) {
+    float pt[DIM], t0, t1;
+    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+    if (d * d <= R * R) {
+      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
+      float w = prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
+      acc += w; sel = p; selw = w;
+      if (target < acc) break;
+    }
+  }
+  if (sel < 0) return;
+  const float* P = prims + sel * PS;
+  float sp[DIM], sn[DIM], pdf;
+  if constexpr (DIM == 2) {
+    float s0 = P[2] - P[0], s1 = P[3] - P[1];
+    float sv[2] = {s0, s1};
+    float area = normv<2>(sv), u = rn[1];
+    sp[0] = P[0] + u * s0; sp[1] = P[1] + u * s1;
+    sn[0] = s1 / area; sn[1] = -s0 / area;
+    pdf = 1.0f / area;
+  } else {
+    float v1[3], v2[3];
+    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; }
+    cross3(sn, v1, v2);
+    float area = normv<3>(sn);
+    float u1 = __builtin_sqrtf(rn[1]), u2 = rn[2], u = 1.0f - u1, v = u2 * u1, w = 1.0f - u - v;
+    for (int k = 0; k < 3; k++) { sp[k] = P[k] * u + P[3 + k] * v + P[6 + k] * w; sn[k] /= area; }
+    pdf = 2.0f / area;
+  }
+  pdf *= selw / total;
+  float dts[DIM];
+  for (int k = 0; k < DIM; k++) dts[k] = sp[k] - x[k];
+  float distToSample = normv<DIM>(dts);
+  float alpha = st.onNeumann ? 2.0f : 1.0f;
+  if (pdf > 0.0f && distToSample < R) {
+    float p1[DIM], p2[DIM], mn[DIM];
+    for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
+    if (st.onNeumann) offset_point<DIM>(x, mn, p1); else for (int k = 0; k < DIM; k++) p1[k] = x[k];
+    for (int k = 0; k < DIM; k++) mn[k] = -sn[k];
+    offset_point<DIM>(sp, mn, p2);
+    float dd[DIM];
+    for (int k = 0; k < DIM; k++) dd[k] = p2[k] - p1[k];
+    float dn = normv<DIM>(dd);
+    for (int k = 0; k < DIM; k++) dd[k] /= dn;
+    if (!ray_occluded<DIM>(prims, np, p1, dd, dn)) {
+      float G = g.evaluate_xy(x, sp);
+      float hval = 0.0f;
+      st.totalNeumann += st.throughput * alpha * G * hval / pdf;
+    }
+  }
+}
+
+template <int DIM>
+__device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, const float* prims,
+                                    const float* sil, float dirichletDist, Pcg32& smp, Gfn<DIM>& g,
+                                    WalkState<DIM>& st, uint32_t* steps, uint32_t* iters) {
+  const int np = sc.n_prims, ns = sc.n_sil;
+  while (dirichletDist > prm.epsilon_shell) {
+    float starRadius;
+    bool flip = false;
+    if (sc.double_sided && st.onNeumann) {
+      if (st.prevDist > 0.0f && dotv<DIM>(st.prevDir, st.n) < 0.0f) {
+        for (int k = 0; k < DIM; k++) st.n[k] *= -1.0f;
+        flip = true;
+      }
+    }
+    if (prm.steps_before_maximal_spheres <= st.walkLength) {
+      starRadius = dirichletDist;
+    } else {
+      starRadius = star_radius<DIM>(sil, ns, np, st.pt, prm.min_star_radius, dirichletDist,
+                                    prm.silhouette_precision, flip);
+      if (prm.min_star_radius <= dirichletDist)
+        starRadius = smax(0.99f * starRadius, prm.min_star_radius);
+    }
+    g.update_ball(st.pt, starRadius);
+    (*steps)++;
+    float u[2];
+    u[0] = smp.nextf();
+    if constexpr (DIM == 3) u[1] = smp.nextf();
+    float dir[DIM];
+    sample_unit_sphere<DIM>(u, dir);
+    if (st.onNeumann && dotv<DIM>(st.n, dir) > 0.0f)
+      for (int k = 0; k < DIM; k++) dir[k] *= -1.0f;
+
+    float org[DIM];
+    if (st.onNeumann) {
+      float mn[DIM];
+      for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
+      offset_point<DIM>(st.pt, mn, org);
+    } else {
+      for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
+    }
+    Hit ip;
+    bool hit = np > 0 && ray_hit<DIM>(prims, np, org, dir, starRadius, &ip);
+    if (!hit) {
+      for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
+      ip.d = starRadius;
+    }
+    if (!prm.ignore_neumann) {
+      float rn[3] = {0.0f, 0.0f, 0.0f};
+      for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
+      bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
+      if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
+    }
+    if (!prm.ignore_source) {
+      float pdf, sp[DIM];
+      sample_volume<DIM>(g, dir, smp, &pdf, sp, iters);
+      if (g.r <= ip.d) {
+        float contrib = g.norm() * source_value<DIM>(sc, sp);
+        st.totalSource += st.throughput * contrib;
+      }
+    }
+    if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
+    st.prevDist = ip.d;
+    for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
+    st.onNeumann = hit;
+    st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
+    if (st.throughput < prm.rr_threshold) {
+      float survival = st.throughput / prm.rr_threshold;
+      if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
+      st.throughput = prm.rr_threshold;
+    }
+    st.walkLength++;
+    if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
+    if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
+    dirichletDist = dirichlet_dist_lane<DIM>(sc, st.pt);
+  }
+  return WC_DIRICHLET;
+}
+
+// ---------------------------------------------------------------------------
+// the solve kernel
+// ---------------------------------------------------------------------------
+// Per-wave LDS scratch: stratified samples [2*n_pairs*(DIM-1)] then the walk
+// records of one chunk (SoA, 2*kChunkPairs entries each):
+//   total | first | bdir[DIM] | sdir[DIM] | code
+template <int DIM>
+struct RecLayout {
+  static constexpr int kRec = 2 * kChunkPairs;
+  static constexpr int total = 0, first = kRec, bdir = 2 * kRec, sdir = (2 + DIM) * kRec,
+                       code = (2 + 2 * DIM) * kRec, size = (3 + 2 * DIM) * kRec;
+};
+
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void wos_solve_kernel(
+    const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base,
+    int64_t stride, float* __restrict__ p_out, float* __restrict__ g_out, int32_t* __restrict__ nest_out,
+    int32_t* __restrict__ steps_out, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work,
+    int geom_floats, int lhs_floats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+
+  // stage Neumann primitives + silhouette candidates (every workgroup once)
+  const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
+  const int primAl = (primN + 3) & ~3;
+  for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
+  for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
+  __syncthreads();
+  const float* Lprim = smem;
+  const float* Lsil = smem + primAl;
+  float* wbase = smem + geom_floats + wave * (lhs_floats + RecLayout<DIM>::size);
+  float* strat = wbase;
+  float* rec = wbase + lhs_floats;
+
+  uint32_t c_steps = 0, c_wasted = 0, c_rec = 0, c_esc = 0, c_maxl = 0, c_rr = 0, c_dir = 0, c_pts = 0, c_iters = 0;
+
+  const int sd = DIM - 1;
+  const int npairs = prm.n_pairs;
+  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
+
+  for (;;) {
+    unsigned int idx = 0;
+    if (lane == 0) idx = atomicAdd(work, 1u);
+    idx = __shfl(idx, 0);
+    if ((int64_t)idx >= n) break;
+    const int64_t gidx = base + (int64_t)idx * stride;
+
+    float x[DIM];
+    for (int k = 0; k < DIM; k++) x[k] = pts[(int64_t)idx * DIM + k];
+
+    // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
+    float nDist = kFltMax, nSigned = kFltMax;
+    if (sc.n_prims > 0) {
+      Closest c = closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
+      nDist = c.d;
+      nSigned = signed_dist<DIM>(sc.paux, c, x);
+    }
+    float dDist, dSigned;
+    if (sc.n_dprims > 0) {
+      Closest c = closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
+      dDist = c.d;
+      dSigned = signed_dist<DIM>(sc.dpaux, c, x);
+    } else {
+      dDist = dSigned = bbox_far_dist<DIM>(sc, x);
+    }
+    bool inside = !sc.watertight ? true
+                  : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
+    const bool estimate = inside || sc.double_sided;
+
+    // statistics registers: lane 0 = solution chain, lanes 1..DIM = gradient components
+    float sMean = 0.0f, sM2 = 0.0f, sFirst = 0.0f;
+    int sN = 0;
+    uint32_t pt_steps = 0;
+
+    if (estimate) {
+      c_pts++;
+      // ---- stratified samples (sampling.h:435-457), per-point stream
+      const int nstrat = 2 * npairs;
+      if (lane == 0) {
+        Pcg32 ps;
+        ps.seed(seed32(prm.seed, (uint64_t)gidx, 0, 0), 1u);
+        const float ome = 1.0f - kFltEps;
+        const float inv = 1.0f / (float)nstrat;
+        for (int i = 0; i < nstrat; ++i)
+          for (int j = 0; j < sd; ++j) {
+            float sj = ((float)i + ps.nextf()) * inv;
+            strat[sd * i + j] = smin(sj, ome);
+          }
+        for (int i = 0; i < sd; ++i)
+          for (int j = 0; j < nstrat; ++j) {
+            int other = j + (int)ps.bounded((uint32_t)(nstrat - j));
+            float t = strat[sd * j + i];
+            strat[sd * j + i] = strat[sd * other + i];
+            strat[sd * other + i] = t;
+          }
+      }
+      wave_sync();
+
+      const float boundaryDist = smin(dDist, nDist);
+      const float firstR = 0.99f * boundaryDist;
+
+      for (int c0 = 0; c0 < npairs; c0 += kChunkPairs) {
+        const int w = c0 + lane;
+        if (w < npairs) {
+          float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
+          for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
+          Pcg32 fs;
+          fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1), 1u);
+          const uint32_t wseed = seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 2);
+          for (int a = 0; a < prm.n_anti; a++) {
+            Gfn<DIM> g;
+            g.init(yuk0, sc.absorption);
+            WalkState<DIM> st;
+            for (int k = 0; k < DIM; k++) {
+              st.pt[k] = x[k]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; st.sdir[k] = 0.0f; st.bdir[k] = 0.0f;
+            }
+            st.prevDist = 0.0f; st.throughput = 1.0f; st.onNeumann = false; st.walkLength = 0;
+            st.totalNeumann = 0.0f; st.totalSource = 0.0f; st.firstSource = 0.0f;
+            g.update_ball(st.pt, firstR);
+            uint32_t wsteps = 1, witers = 0;
+            if (!prm.ignore_source) {
+              if (a == 0) {
+                float dir[DIM];
+                sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
+                sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, &witers);
+              } else {
+                float sdv[DIM];
+                for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - st.pt[k];
+                for (int k = 0; k < DIM; k++) g.yVol[k] = st.pt[k] - sdv[k];
+                g.r = normv<DIM>(sdv);
+              }
+              float gnorm = g.norm();
+              float contrib = gnorm * source_value<DIM>(sc, g.yVol);
+              st.totalSource += st.throughput * contrib;
+              st.firstSource = contrib;
+              float gr[DIM];
+              g.gradient(gr);
+              float den = sourcePdf * gnorm;
+              for (int k = 0; k < DIM; k++) st.sdir[k] = gr[k] / den;
+            }
+            if (a == 0) {
+              const float* u = &strat[sd * (2 * w + 1)];
+              float bd[DIM];
+              if (prm.use_cosine) {
+                if constexpr (DIM == 2) {
+                  float u1 = 2.0f * u[0] - 1.0f;
+                  bd[0] = u1; bd[1] = __builtin_sqrtf(smax(0.0f, 1.0f - u1 * u1));
+                } else {
+                  float u1 = 2.0f * u[0] - 1.0f, u2 = 2.0f * u[1] - 1.0f, dx = 0.0f, dy = 0.0f;
+                  if (!(u1 == 0 && u2 == 0)) {
+                    float theta, r;
+                    if (__builtin_fabsf(u1) > __builtin_fabsf(u2)) { r = u1; theta = (float)(0.25 * kPi * (double)(u2 / u1)); }
+                    else { r = u2; theta = (float)(0.5 * kPi * (double)(1.0f - 0.5f * (u1 / u2))); }
+                    float sn, cs;
+                    fsincos(theta, &sn, &cs);
+                    dx = r * cs; dy = r * sn;
+                  }
+                  bd[0] = dx; bd[1] = dy; bd[2] = __builtin_sqrtf(smax(0.0f, 1.0f - (dx * dx + dy * dy)));
+                }
+                if (fs.nextf() < 0.5f) bd[DIM - 1] *= -1.0f;
+                float ct = __builtin_fabsf(bd[DIM - 1]);
+                float pdfc = DIM == 2 ? ct / 2.0f : (float)((double)ct / kPi);
+                boundaryPdf = 0.5f * pdfc;
+                // transformCoordinates (sampling.h:176-203) with n = (1,0[,0])
+                if constexpr (DIM == 2) {
+                  const float n0 = 1.0f, n1 = 0.0f;
+                  float s0 = n1, s1 = -n0;
+                  float t0 = bd[0] * s0 + bd[1] * n0, t1 = bd[0] * s1 + bd[1] * n1;
+                  bd[0] = t0; bd[1] = t1;
+                } else {
+                  const float n[3] = {1.0f, 0.0f, 0.0f};
+                  float sign = __builtin_copysignf(1.0f, n[2]);
+                  const float aa = -1.0f / (sign + n[2]);
+                  const float b = n[0] * n[1] * aa;
+                  float b1[3] = {1.0f + sign * n[0] * n[0] * aa, sign * b, -sign * n[0]};
+                  float b2[3] = {b, sign + n[1] * n[1] * aa, -n[1]};
+                  float t[3];
+                  for (int k = 0; k < 3; k++) t[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
+                  for (int k = 0; k < 3; k++) bd[k] = t[k];
+                }
+              } else {
+                sample_unit_sphere<DIM>(u, bd);
+                boundaryPdf = pdf_sphere_uniform<DIM>(1.0f);
+              }
+              for (int k = 0; k < DIM; k++) { g.ySurf[k] = g.c[k] + g.R * bd[k]; boundaryPt[k] = g.ySurf[k]; }
+            } else {
+              float bd[DIM];
+              for (int k = 0; k < DIM; k++) bd[k] = boundaryPt[k] - st.pt[k];
+              for (int k = 0; k < DIM; k++) g.ySurf[k] = st.pt[k] - bd[k];
+            }
+            st.prevDist = g.R;
+            for (int k = 0; k < DIM; k++) st.prevDir[k] = (g.ySurf[k] - st.pt[k]) / g.R;
+            for (int k = 0; k < DIM; k++) st.pt[k] = g.ySurf[k];
+            st.throughput *= g.poisson_kernel() / boundaryPdf;
+            {
+              float pg[DIM];
+              g.poisson_kernel_gradient(pg);
+              float den = boundaryPdf * st.throughput;
+              for (int k = 0; k < DIM; k++) st.bdir[k] = pg[k] / den;
+            }
+            const float dd = dirichlet_dist_lane<DIM>(sc, st.pt);
+            Pcg32 ws;
+            ws.seed(wseed, 1u);
+            const int code = walk<DIM>(sc, prm, Lprim, Lsil, dd, ws, g, st, &wsteps, &witers);
+            c_iters += witers;
+            pt_steps += wsteps;
+            const int r = lane * prm.n_anti + a;
+            const bool recorded = code == WC_DIRICHLET || code == WC_RR;
+            if (recorded) {
+              const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
+              rec[RecLayout<DIM>::total + r] = st.throughput * term + st.totalNeumann + st.totalSource;
+              c_steps += wsteps; c_rec++;
+              if (code == WC_RR) c_rr++; else c_dir++;
+            } else {
+              c_wasted += wsteps;
+              if (code == WC_ESCAPED) c_esc++; else c_maxl++;
+            }
+            rec[RecLayout<DIM>::first + r] = st.firstSource;
+            for (int k = 0; k < DIM; k++) {
+              rec[RecLayout<DIM>::bdir + k * RecLayout<DIM>::kRec + r] = st.bdir[k];
+              rec[RecLayout<DIM>::sdir + k * RecLayout<DIM>::kRec + r] = st.sdir[k];
+            }
+            rec[RecLayout<DIM>::code + r] = recorded ? 1.0f : 0.0f;
+          }
+        }
+        wave_sync();
+        // ---- statistics in walk order (walk_on_stars.h:500-506,583-614)
+        const int cnt = (npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs;
+        for (int j = 0; j < cnt; ++j) {
+          float cvb = __shfl(sMean, 0);
+          float cvs = __shfl(sFirst / (float)(sN > 1 ? sN : 1), 0);
+          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
+          for (int a = 0; a < prm.n_anti; a++) {
+            const int r = j * prm.n_anti + a;
+            if (rec[RecLayout<DIM>::code + r] == 0.0f) continue;
+            const float total = rec[RecLayout<DIM>::total + r];
+            const float first = rec[RecLayout<DIM>::first + r];
+            if (lane == 0) {
+              sN += 1;
+              float delta = total - sMean;
+              sMean += delta / (float)sN;
+              float delta2 = total - sMean;
+              sM2 += delta * delta2;
+              sFirst += first;
+            } else if (lane <= DIM) {
+              const int k = lane - 1;
+              const float bc = total - first;
+              const float be = (bc - cvb) * rec[RecLayout<DIM>::bdir + k * RecLayout<DIM>::kRec + r];
+              const float se = (first - cvs) * rec[RecLayout<DIM>::sdir + k * RecLayout<DIM>::kRec + r];
+              const float ge = be + se;
+              sN += 1;
+              float delta = ge - sMean;
+              sMean += delta / (float)sN;
+              float delta2 = ge - sMean;
+              sM2 += delta * delta2;
+            }
+          }
+        }
+        wave_sync();
+      }
+    }
+
+    // ---- masked outputs (grid.h:155-179, 207-237)
+    const float mask = prm.boundary_distance_mask;
+    const bool maskP = __builtin_fabsf(nDist) < mask;
+    const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
+    float val = estimate ? sMean : 0.0f;
+    if (lane == 0) {
+      p_out[idx] = maskP ? 0.0f : val;
+      if (nest_out) nest_out[idx] = sN;
+    } else if (lane <= DIM) {
+      g_out[(int64_t)idx * DIM + (lane - 1)] = maskG ? 0.0f : val;
+    }
+    if (steps_out) {
+      uint32_t s = pt_steps;
+      for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      if (lane == 0) steps_out[idx] = (int32_t)s;
+    }
+  }
+
+  // ---- counters: wave reduction + one atomic per wave
+  uint32_t vals[C_NUM] = {c_steps, c_wasted, c_rec, c_esc, c_maxl, c_rr, c_dir, c_pts, c_iters};
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) {
+    unsigned long long v = vals[i];
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0 && v) atomicAdd(&counters[i], v);
+  }
+}
+
+template __global__ void wos_solve_kernel<2>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                             int64_t, float*, float*, int32_t*, int32_t*, unsigned long long*,
+                                             unsigned int*, int, int);
+template __global__ void wos_solve_kernel<3>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                             int64_t, float*, float*, int32_t*, int32_t*, unsigned long long*,
+                                             unsigned int*, int, int);
+
+// math self-test kernel (parity of the deterministic math with the CPU oracle)
+__global__ void wos_math_selftest_kernel(int which, const double* x, double* out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double v = x[i], r = 0.0;
+  switch (which) {
+    case 0: r = dexp(v); break;
+    case 1: r = dlog(v); break;
+    case 2: { double s, c; dsincos(v, &s, &c); r = s; } break;
+    case 3: { double s, c; dsincos(v, &s, &c); r = c; } break;
+    case 4: r = datan(v); break;
+    case 5: r = __builtin_sqrt(v); break;
+    case 6: r = bessi0(v); break;
+    case 7: r = bessi1(v); break;
+    case 8: r = bessk0(v); break;
+    case 9: r = bessk1(v); break;
+    case 10: r = (double)fexp((float)v); break;
+    case 11: r = (double)flog((float)v); break;
+    case 12: r = (double)fsin((float)v); break;
+    case 13: r = (double)fcos((float)v); break;
+    case 14: r = (double)fcbrt((float)v); break;
+    case 15: r = (double)__builtin_sqrtf((float)v); break;
+    default: r = __builtin_nan("");
+  }
+  out[i] = r;
+}
+
+
+// ---------------------------------------------------------------------------
+// host-side launchers (called from wos_capi.hip)
+// ---------------------------------------------------------------------------
+int rec_floats(int dim) { return dim == 2 ? RecLayout<2>::size : RecLayout<3>::size; }
+
+hipError_t launch_solve(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                        int64_t base, int64_t stride, float* p, float* g, int32_t* nest, int32_t* steps,
+                        unsigned long long* counters, unsigned int* work, int grid, size_t shmem,
+                        int geom_floats, int lhs_floats, hipStream_t s) {
+  if (dim == 2)
+    hipLaunchKernelGGL(wos_solve_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, p,
+                       g, nest, steps, counters, work, geom_floats, lhs_floats);
+  else
+    hipLaunchKernelGGL(wos_solve_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, p,
+                       g, nest, steps, counters, work, geom_floats, lhs_floats);
+  return hipGetLastError();
+}
+
+hipError_t occupancy_blocks_per_cu(int dim, size_t shmem, int* blocks) {
+  if (dim == 2)
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_solve_kernel<2>, kBlock, shmem);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_solve_kernel<3>, kBlock, shmem);
+}
+
+hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s) {
+  int grid = (int)((n + 255) / 256);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(wos_math_selftest_kernel, dim3(grid), dim3(256), 0, s, which, x, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace wos

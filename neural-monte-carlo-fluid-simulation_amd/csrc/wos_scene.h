@@ -1,0 +1,72 @@
+// wos_scene.h -- scene and solver-parameter layouts shared by the host-side scene
+// preparation (wos_scene.cpp) and the gfx950 kernels (wos_kernel.hip).
+//
+// HBM layout (all float32, structure-of-records, 16-byte aligned):
+//   prim  : Neumann primitives, packed per primitive
+//           2D  [pa.x pa.y pb.x pb.y]                          (4 floats)
+//           3D  [pa.xyz pb.xyz pc.xyz]                         (9 floats)
+//   paux  : per-primitive normals used only by signed-distance queries
+//           2D  [na.xy nb.xy nseg.xy]  (vertex normals at the ends + segment normal)
+//           3D  [na nb nc | e0 e1 e2 | nface]  (vertex, edge, face normals; 21 floats)
+//   sil   : silhouette candidates (vertices in 2D, edges in 3D)
+//           2D  [p.xy n0.xy n1.xy miss pad]                    (8 floats)
+//           3D  [pa.xyz pb.xyz n0.xyz n1.xyz miss pad pad pad] (16 floats)
+//   dprim/dpaux : same as prim/paux for the (optional) Dirichlet boundary
+//   source: the -div(u) grid, row-major; 2D (H rows ~ y, W cols ~ x), 3D (X,Y,Z)
+//
+// The Neumann prim + sil arrays are staged into LDS by every workgroup.
+#pragma once
+#include <stdint.h>
+
+namespace wos {
+
+constexpr int kPrimStride2 = 4, kPrimStride3 = 9;
+constexpr int kAuxStride2 = 6, kAuxStride3 = 21;
+constexpr int kSilStride2 = 8, kSilStride3 = 16;
+
+template <int DIM> struct Layout;
+template <> struct Layout<2> {
+  static constexpr int prim = kPrimStride2, aux = kAuxStride2, sil = kSilStride2;
+};
+template <> struct Layout<3> {
+  static constexpr int prim = kPrimStride3, aux = kAuxStride3, sil = kSilStride3;
+};
+
+struct DevScene {
+  int32_t dim;
+  int32_t n_prims, n_sil, n_dprims;
+  const float* prim;
+  const float* paux;
+  const float* sil;
+  const float* dprim;
+  const float* dpaux;
+  const float* source;
+  int32_t sdims[3];
+  float pmin[3], pmax[3], ext[3];
+  float absorption;
+  float g_dirichlet;
+  int32_t watertight;
+  int32_t double_sided;
+};
+
+struct DevParams {
+  int32_t n_walks;          // as configured (nWalks)
+  int32_t n_pairs;          // walks per antithetic iteration set (nWalks/2 or nWalks)
+  int32_t n_anti;           // 2 with antithetic variates, else 1
+  int32_t max_walk_length;
+  int32_t steps_before_tikhonov;
+  int32_t steps_before_maximal_spheres;
+  float epsilon_shell;
+  float min_star_radius;
+  float silhouette_precision;
+  float rr_threshold;
+  float boundary_distance_mask;
+  int32_t use_cv;
+  int32_t use_cosine;
+  int32_t ignore_dirichlet;
+  int32_t ignore_neumann;
+  int32_t ignore_source;
+  uint64_t seed;
+};
+
+}  // namespace wos

@@ -1,0 +1,200 @@
+"""Host-side API of the MI355X walk-on-stars engine (thin layer over include/wos.h).
+
+Mirrors the reference's operator interface for the pressure solve:
+  Scene(config, source)   <-> bindings/zombie/demo/scene.h:54-77 (2D),
+                              bindings/zombie3d/demo/scene_3d.h:22-40 (3D)
+  solve(points)           <-> runWalkOnStars_sampled, demo.cpp:119-205 /
+                              runWalkOnStars_3d, zombie3d/demo/demo.cpp:15-116
+Inputs may be numpy arrays (host) or torch tensors already on the GPU (zero-copy:
+device pointers are handed to the C ABI and the kernel runs on torch's current
+stream).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import SceneDesc, SceneInfo, SolverParams, Stats, WosError, check
+
+_DEFAULT_SEED = 0x5EED0001
+
+
+def load_obj(path, dim, flip_orientation=False, normalize=False):
+    """OBJ -> (vertices [V,dim] f32, prims [P,dim] i32) with the reference's parsing rules."""
+    L = _lib.load()
+    m = _lib.Mesh()
+    check(L.wos_load_obj(os.fsencode(path), dim, int(flip_orientation), int(normalize), C.byref(m)),
+          f"wos_load_obj({path})")
+    try:
+        v = np.ctypeslib.as_array(m.vertices, shape=(m.n_vertices * dim,)).copy().reshape(-1, dim)
+        ix = np.ctypeslib.as_array(m.prims, shape=(m.n_prims * dim,)).copy().reshape(-1, dim)
+    finally:
+        L.wos_mesh_free(C.byref(m))
+    return v.astype(np.float32), ix.astype(np.int32)
+
+
+def _get_opt(d, key, default, typ):
+    v = d.get(key, default) if d is not None else default
+    return typ(v)
+
+
+def solver_params(solver=None, output=None, seed=None):
+    """Parse the reference's wost.json "solver" / "output" sections (demo.cpp:121-137,
+    grid.h:159), same keys (including the misspelled `setps...`) and defaults."""
+    s = dict(solver or {})
+    o = dict(output or {})
+    p = SolverParams()
+    _lib.load().wos_default_params(C.byref(p))
+    p.n_walks = _get_opt(s, "nWalks", 128, int)
+    p.max_walk_length = _get_opt(s, "maxWalkLength", 1024, int)
+    p.steps_before_tikhonov = _get_opt(s, "setpsBeforeApplyingTikhonov", p.max_walk_length, int)
+    p.steps_before_maximal_spheres = _get_opt(s, "setpsBeforeUsingMaximalSpheres", p.max_walk_length, int)
+    p.epsilon_shell = _get_opt(s, "epsilonShell", 1e-3, float)
+    p.min_star_radius = _get_opt(s, "minStarRadius", 1e-3, float)
+    p.silhouette_precision = _get_opt(s, "silhouettePrecision", 1e-3, float)
+    p.russian_roulette_threshold = _get_opt(s, "russianRouletteThreshold", 0.0, float)
+    p.boundary_distance_mask = _get_opt(o, "boundaryDistanceMask", 0.0, float)
+    p.disable_gradient_control_variates = int(bool(s.get("disableGradientControlVariates", False)))
+    p.disable_gradient_antithetic_variates = int(bool(s.get("disableGradientAntitheticVariates", False)))
+    p.use_cosine_sampling = int(bool(s.get("useCosineSamplingForDirectionalDerivatives", False)))
+    p.ignore_dirichlet = int(bool(s.get("ignoreDirichlet", False)))
+    p.ignore_neumann = int(bool(s.get("ignoreNeumann", False)))
+    p.ignore_source = int(bool(s.get("ignoreSource", False)))
+    p.seed = int(seed if seed is not None else s.get("seed", _DEFAULT_SEED)) & 0xFFFFFFFFFFFFFFFF
+    return p
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+class WosScene:
+    """Geometry + source field resident on one GPU."""
+
+    def __init__(self, vertices, prims, source=None, absorption=0.0, *, dvertices=None, dprims=None,
+                 dirichlet_value=0.0, watertight=True, double_sided=False, device=0):
+        L = _lib.load()
+        v = np.ascontiguousarray(vertices, dtype=np.float32)
+        ix = np.ascontiguousarray(prims, dtype=np.int32)
+        self.dim = int(v.shape[1])
+        if self.dim not in (2, 3) or ix.ndim != 2 or ix.shape[1] != self.dim:
+            raise WosError("vertices must be [V,2|3] and prims [P,dim]")
+        d = SceneDesc()
+        d.dim = self.dim
+        d.vertices = v.ctypes.data_as(C.POINTER(C.c_float))
+        d.prims = ix.ctypes.data_as(C.POINTER(C.c_int32))
+        d.n_vertices, d.n_prims = v.shape[0], ix.shape[0]
+        keep = [v, ix]
+        if dprims is not None and len(dprims):
+            dv = np.ascontiguousarray(dvertices, dtype=np.float32)
+            dix = np.ascontiguousarray(dprims, dtype=np.int32)
+            d.dvertices = dv.ctypes.data_as(C.POINTER(C.c_float))
+            d.dprims = dix.ctypes.data_as(C.POINTER(C.c_int32))
+            d.n_dvertices, d.n_dprims = dv.shape[0], dix.shape[0]
+            keep += [dv, dix]
+        d.dirichlet_value = float(dirichlet_value)
+        d.absorption = float(absorption)
+        d.is_watertight = int(bool(watertight))
+        d.is_double_sided = int(bool(double_sided))
+        self.source_shape = None
+        if source is not None:
+            if _is_torch(source) and source.is_cuda:
+                src = source.detach().to(dtype=__import__("torch").float32).contiguous()
+                d.source = src.data_ptr()
+                d.source_on_device = 1
+                keep.append(src)
+                shape = tuple(src.shape)
+            else:
+                if _is_torch(source):
+                    source = source.detach().cpu().numpy()
+                src = np.ascontiguousarray(source, dtype=np.float32)
+                d.source = src.ctypes.data
+                keep.append(src)
+                shape = src.shape
+            if len(shape) != self.dim:
+                raise WosError(f"source grid must be {self.dim}-D, got shape {shape}")
+            for k in range(3):
+                d.source_dims[k] = shape[k] if k < len(shape) else 0
+            self.source_shape = tuple(int(s) for s in shape)
+        self.device = int(device)
+        h = C.c_void_p()
+        check(L.wos_scene_create(C.byref(d), self.device, C.byref(h)), "wos_scene_create")
+        self._h = h
+        del keep
+
+    @classmethod
+    def from_obj(cls, path, dim, source=None, absorption=0.0, flip_orientation=False, normalize=False, **kw):
+        v, ix = load_obj(path, dim, flip_orientation, normalize)
+        return cls(v, ix, source, absorption, **kw)
+
+    def info(self):
+        i = SceneInfo()
+        check(_lib.load().wos_scene_get_info(self._h, C.byref(i)), "wos_scene_get_info")
+        return {"dim": i.dim, "n_prims": i.n_prims, "n_silhouettes": i.n_silhouettes,
+                "n_dprims": i.n_dprims, "device": i.device,
+                "bbox_min": list(i.bbox_min)[:i.dim], "bbox_max": list(i.bbox_max)[:i.dim]}
+
+    def solve(self, pts, params=None, *, index_base=0, index_stride=1, counts=False, stream=None,
+              sync=True):
+        """Solve at query points.  Returns (p [N], grad [N,dim], stats dict[, n_est, steps])
+        as numpy arrays for host input, torch tensors for GPU tensor input."""
+        L = _lib.load()
+        params = params if params is not None else solver_params()
+        st = Stats()
+        if _is_torch(pts) and pts.is_cuda:
+            import torch
+            x = pts.detach().to(torch.float32).contiguous()
+            n = x.shape[0]
+            if x.ndim != 2 or x.shape[1] != self.dim:
+                raise WosError(f"points must be [N,{self.dim}]")
+            p = torch.empty(n, dtype=torch.float32, device=x.device)
+            g = torch.empty(n, self.dim, dtype=torch.float32, device=x.device)
+            ne = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
+            sp = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
+            s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+            flags = _lib.WOS_PTRS_DEVICE | (0 if sync else _lib.WOS_ASYNC)
+            check(L.wos_solve(self._h, C.byref(params), x.data_ptr(), n, index_base, index_stride,
+                              p.data_ptr(), g.data_ptr(), ne.data_ptr() if counts else None,
+                              sp.data_ptr() if counts else None, C.byref(st), s, flags), "wos_solve")
+        else:
+            if _is_torch(pts):
+                pts = pts.detach().cpu().numpy()
+            x = np.ascontiguousarray(pts, dtype=np.float32)
+            if x.ndim != 2 or x.shape[1] != self.dim:
+                raise WosError(f"points must be [N,{self.dim}]")
+            n = x.shape[0]
+            p = np.empty(n, np.float32)
+            g = np.empty((n, self.dim), np.float32)
+            ne = np.empty(n, np.int32) if counts else None
+            sp = np.empty(n, np.int32) if counts else None
+            check(L.wos_solve(self._h, C.byref(params), x.ctypes.data, n, index_base, index_stride,
+                              p.ctypes.data, g.ctypes.data, ne.ctypes.data if counts else None,
+                              sp.ctypes.data if counts else None, C.byref(st), stream, 0), "wos_solve")
+        out = (p, g, st.as_dict())
+        if counts:
+            out = out + (ne, sp)
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().wos_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def selftest_math(which, x, device=0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    check(_lib.load().wos_selftest_math(which, x.ctypes.data, out.ctypes.data, x.size, device),
+          "wos_selftest_math")
+    return out
+
+
+def device_count():
+    return int(_lib.load().wos_device_count())

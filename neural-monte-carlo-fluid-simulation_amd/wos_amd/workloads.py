@@ -1,0 +1,176 @@
+"""Synthetic workloads of BASELINE.json's configs.
+
+Inputs mirror what the reference's caller hands to zombie_bindings:
+  * query points: src/2d/models/base.py:226-251 (sample_random_2D(res^2) over the
+    OBJ's vertex bbox, karman points inside the cylinder removed, base.py:239-241)
+    or cell-centred grids (src/2d/utils/model_utils.py:3-20);
+  * source grid: -div(u) sampled on sample_uniform_2D(1000, with_boundary=True)
+    (model_split.py:230-243): shape (res_y+2, res_x+2), rows ~ y ('xy' meshgrid).
+    The SIREN divergence is replaced by a smooth analytic field (no checkpoints).
+"""
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SCENES = os.path.join(REPO, "scenes")
+
+KARMAN_OBJ = os.path.join(SCENES, "geometry_1cyl_long_open.obj")
+SQUARE_OBJ = os.path.join(SCENES, "square.obj")
+CUBE_OBJ = os.path.join(SCENES, "cube.obj")
+
+# examples/*/wost.json "solver" section (shared by all examples) with the
+# BASELINE walk counts substituted per config.
+SOLVER_BASE = {
+    "maxWalkLength": 10000, "epsilonShell": 1e-3, "minStarShapedRadius": 1e-3,
+    "ignoreDirichlet": True, "ignoreNeumann": False, "ignoreSource": False,
+    "russianRouletteThreshold": 0.99, "setpsBeforeApplyingTikhonov": 0,
+}
+OUTPUT_BASE = {"gridRes": 300, "boundaryDistanceMask": 1e-3}
+SCENE_BASE = {"absorptionCoeff": 350, "normalizeDomain": False, "flipOrientation": False,
+              "isDoubleSided": False, "isWatertight": True}
+
+
+def read_obj_vertices(path, dim):
+    vs = []
+    with open(path) as f:
+        for line in f:
+            t = line.split()
+            if t and t[0] == "v":
+                vs.append([float(c) for c in t[1:1 + dim]])
+    return np.asarray(vs, np.float64)
+
+
+def scene_size(path, dim=2):
+    """[min_x, max_x, min_y, max_y(, min_z, max_z)] as src/2d/main.py:36-44 computes it."""
+    v = read_obj_vertices(path, dim)
+    out = []
+    for k in range(dim):
+        out += [float(v[:, k].min()), float(v[:, k].max())]
+    return out
+
+
+def uniform_grid_2d(resolution, size, with_boundary=True):
+    """sample_uniform_2D (src/2d/utils/model_utils.py:3-20), meshgrid 'xy' -> [res_y(+2), res_x(+2), 2]."""
+    if (size[1] - size[0]) > (size[3] - size[2]):
+        res_x, res_y = resolution, int(resolution * (size[3] - size[2]) / (size[1] - size[0]))
+    else:
+        res_x, res_y = int(resolution * (size[1] - size[0]) / (size[3] - size[2])), resolution
+    x = np.linspace(0.5, res_x - 0.5, res_x, dtype=np.float32)
+    y = np.linspace(0.5, res_y - 0.5, res_y, dtype=np.float32)
+    if with_boundary:
+        x = np.concatenate([[0.0], x, [res_x * 1.0]]).astype(np.float32)
+        y = np.concatenate([[0.0], y, [res_y * 1.0]]).astype(np.float32)
+    X, Y = np.meshgrid(x, y, indexing="xy")
+    X = X / res_x * (size[1] - size[0]) + size[0]
+    Y = Y / res_y * (size[3] - size[2]) + size[2]
+    return np.stack([X, Y], -1).astype(np.float32)
+
+
+def karman_source(grid):
+    x, y = grid[..., 0].astype(np.float64), grid[..., 1].astype(np.float64)
+    return (np.sin(3 * x) * np.cos(2 * y) + 0.5 * np.cos(5 * x + 1)).astype(np.float32)
+
+
+def karman_obstacle(size):
+    """Cylinder centre/radius as src/2d/main.py:94-96 derives them (vertices strictly inside the bbox)."""
+    v = read_obj_vertices(KARMAN_OBJ, 2)
+    inside = (v[:, 0] > size[0]) & (v[:, 0] < size[1]) & (v[:, 1] > size[2]) & (v[:, 1] < size[3])
+    ov = v[inside]
+    c = ov.mean(0)
+    r = np.mean(np.linalg.norm(ov - c, axis=1)) + OUTPUT_BASE["boundaryDistanceMask"]
+    return c, r
+
+
+def karman_points(n=65536, seed=1234):
+    """sample_random_2D(256^2) over the scene bbox minus points in the cylinder (base.py:230-241)."""
+    size = scene_size(KARMAN_OBJ)
+    rng = np.random.default_rng(seed)
+    u = rng.random((n, 2), dtype=np.float32)
+    pts = np.empty_like(u)
+    pts[:, 0] = u[:, 0] * (size[1] - size[0]) + size[0]
+    pts[:, 1] = u[:, 1] * (size[3] - size[2]) + size[2]
+    c, r = karman_obstacle(size)
+    d = np.sqrt((pts[:, 0] - c[0]) ** 2 + (pts[:, 1] - c[1]) ** 2) - r
+    return np.ascontiguousarray(pts[d > 0], dtype=np.float32)
+
+
+def karman_grid_points(nx=256, ny=128):
+    size = scene_size(KARMAN_OBJ)
+    x = (np.arange(nx, dtype=np.float64) + 0.5) / nx * (size[1] - size[0]) + size[0]
+    y = (np.arange(ny, dtype=np.float64) + 0.5) / ny * (size[3] - size[2]) + size[2]
+    X, Y = np.meshgrid(x, y, indexing="xy")
+    return np.stack([X.ravel(), Y.ravel()], -1).astype(np.float32)
+
+
+def karman_config(n_walks=128, n_points=65536, seed=1234, grid_points=False):
+    """Config B: karman 2D (geometry_1cyl_long_open.obj, lambda=350, 128 walks)."""
+    size = scene_size(KARMAN_OBJ)
+    grid = uniform_grid_2d(1000, size, with_boundary=True)
+    src = karman_source(grid)
+    pts = karman_grid_points() if grid_points else karman_points(n_points, seed)
+    solver = dict(SOLVER_BASE, nWalks=n_walks)
+    scene = dict(SCENE_BASE, boundary=KARMAN_OBJ)
+    return {"name": "karman2d", "dim": 2, "scene": scene, "solver": solver, "output": dict(OUTPUT_BASE),
+            "source": src, "points": pts, "obj": KARMAN_OBJ}
+
+
+def taylorgreen_config(n_walks=32, res=32):
+    """Config A: taylorgreen 2D on square.obj, 32x32 cell-centred points, 32 walks."""
+    size = scene_size(SQUARE_OBJ)
+    L = size[1] - size[0]
+    grid = uniform_grid_2d(1000, size, with_boundary=True)
+    x, y = grid[..., 0].astype(np.float64), grid[..., 1].astype(np.float64)
+    src = (np.cos(2 * np.pi * (x - size[0]) / L) * np.cos(np.pi * (y - size[2]) / L)).astype(np.float32)
+    xs = (np.arange(res) + 0.5) / res * (size[1] - size[0]) + size[0]
+    ys = (np.arange(res) + 0.5) / res * (size[3] - size[2]) + size[2]
+    X, Y = np.meshgrid(xs, ys, indexing="xy")
+    pts = np.stack([X.ravel(), Y.ravel()], -1).astype(np.float32)
+    solver = dict(SOLVER_BASE, nWalks=n_walks)
+    return {"name": "taylorgreen2d", "dim": 2, "scene": dict(SCENE_BASE, boundary=SQUARE_OBJ), "solver": solver,
+            "output": dict(OUTPUT_BASE), "source": src, "points": pts, "obj": SQUARE_OBJ}
+
+
+def box_2d(L=1.0):
+    """Unit box, counter-clockwise so segment normals (s.y,-s.x) point outward."""
+    v = np.array([[0, 0], [L, 0], [L, L], [0, L]], np.float32)
+    ix = np.array([[0, 1], [1, 2], [2, 3], [3, 0]], np.int32)
+    return v, ix
+
+
+def circle_2d(c, r, n=64):
+    """Clockwise circle: normals point into the disk (out of the fluid)."""
+    t = -np.arange(n) / n * 2 * np.pi
+    v = np.stack([c[0] + r * np.cos(t), c[1] + r * np.sin(t)], -1).astype(np.float32)
+    ix = np.stack([np.arange(n), (np.arange(n) + 1) % n], -1).astype(np.int32)
+    return v, ix
+
+
+def dirichlet_obstacle_config(n_walks=256, res=512, src_res=514):
+    """Config C (synthetic, no reference analogue): unit-square Neumann box with an
+    interior Dirichlet disk g=0 at (0.5,0.35), r=0.1; 512^2 cell-centred points."""
+    v, ix = box_2d(1.0)
+    dv, dix = circle_2d((0.5, 0.35), 0.1, 64)
+    xs = (np.arange(src_res) + 0.5) / src_res
+    X, Y = np.meshgrid(xs, xs, indexing="xy")
+    src = (np.cos(np.pi * X) * np.cos(np.pi * Y)).astype(np.float32)
+    g = (np.arange(res) + 0.5) / res
+    PX, PY = np.meshgrid(g, g, indexing="xy")
+    pts = np.stack([PX.ravel(), PY.ravel()], -1).astype(np.float32)
+    solver = dict(SOLVER_BASE, nWalks=n_walks, ignoreDirichlet=False)
+    return {"name": "box_dirichlet2d", "dim": 2, "vertices": v, "prims": ix, "dvertices": dv, "dprims": dix,
+            "dirichlet_value": 0.0, "absorption": 350.0, "solver": solver, "output": dict(OUTPUT_BASE),
+            "source": src, "points": pts}
+
+
+def cube_config(res=128, n_walks=64, src_res=82):
+    """Config D/E: cube.obj ([-1,1]^3), res^3 cell-centred points, 82^3 source grid."""
+    xs = (np.arange(src_res) + 0.5) / src_res * 2 - 1
+    X, Y, Z = np.meshgrid(xs, xs, xs, indexing="ij")
+    src = (np.cos(np.pi * X / 2) * np.cos(np.pi * Y / 2) * np.cos(np.pi * Z / 2)).astype(np.float32)
+    g = ((np.arange(res) + 0.5) / res * 2 - 1).astype(np.float32)
+    PX, PY, PZ = np.meshgrid(g, g, g, indexing="ij")
+    pts = np.stack([PX.ravel(), PY.ravel(), PZ.ravel()], -1).astype(np.float32)
+    solver = dict(SOLVER_BASE, nWalks=n_walks)
+    return {"name": f"cube3d_{res}", "dim": 3, "scene": dict(SCENE_BASE, boundary=CUBE_OBJ), "solver": solver,
+            "output": dict(OUTPUT_BASE, gridRes=100), "source": src, "points": pts, "obj": CUBE_OBJ}

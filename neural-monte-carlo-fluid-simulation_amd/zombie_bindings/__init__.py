@@ -1,0 +1,114 @@
+"""Drop-in replacement for the reference's pybind11 module `zombie_bindings`.
+
+Same names, argument meaning and return structure as
+  bindings/zombie/demo/demo.cpp:393-401      (2D: Scene(dict), Scene(dict, mat), wost, bvc)
+  bindings/zombie3d/demo/demo.cpp:119-125    (3D: Scene(dict, mat3d), wost)
+so src/2d/models/model_split.py:185-228 and src/3d/models/model_split.py:190-230
+run unchanged with this directory on sys.path.  The solve runs in the HIP kernel
+of ../lib/libwos_hip.so (there is no CPU path).
+
+Differences, all deliberate (DESIGN.md "Boundary"):
+  * missing required keys raise KeyError instead of abort() (config.h:8-11);
+  * RNG seeds are counter-based (solver key "seed", default 0x5EED0001) instead of
+    std::chrono::system_clock, so results are reproducible;
+  * 3D wost solves at the query points it is given (the reference's 3D binding
+    ignores them and solves on a gridRes^3 lattice, zombie3d/demo/grid.h:105-146).
+Extensions: numpy / torch inputs are accepted without nested-list conversion, a
+torch CUDA tensor of points stays on the GPU; optional scene key
+"dirichletBoundary" (OBJ) + "dirichletValue" adds Dirichlet geometry.
+"""
+import os
+
+import numpy as np
+
+from wos_amd import engine as _engine
+
+__all__ = ["Scene", "wost", "bvc"]
+
+
+def _required(d, key):
+    if key not in d:
+        raise KeyError(f"Missing required setting: {key}")
+    return d[key]
+
+
+def _read_pfm(path):
+    with open(path, "rb") as f:
+        header = f.readline().decode().strip()
+        if header not in ("Pf", "PF"):
+            raise ValueError(f"{path}: not a PFM file")
+        w, h = map(int, f.readline().decode().split())
+        scale = float(f.readline().decode().strip())
+        ch = 1 if header == "Pf" else 3
+        data = np.frombuffer(f.read(), dtype="<f4" if scale < 0 else ">f4").astype(np.float32)
+    img = data.reshape(h, w, ch)[::-1]  # PFM rows are bottom-to-top
+    if ch == 3:  # Image<1>::setFromRGB grayscale (image.h:72-76)
+        img = 0.299 * img[..., 0] + 0.587 * img[..., 1] + 0.114 * img[..., 2]
+    else:
+        img = img[..., 0]
+    return np.ascontiguousarray(img, dtype=np.float32)
+
+
+class Scene:
+    """Scene(config) / Scene(config, sourceValue) as in scene.h:22-77 / scene_3d.h:22-40."""
+
+    def __init__(self, config, source=None, device=None):
+        config = dict(config)
+        boundary = _required(config, "boundary")
+        if source is None:
+            # Scene(const json&) reads the source image named by "sourceValue" (scene.h:22-52)
+            src = _read_pfm(_required(config, "sourceValue"))
+            watertight_default, flip_default = True, True
+        else:
+            src = source
+            watertight_default, flip_default = False, False
+        if not hasattr(src, "shape"):
+            src = np.asarray(src, dtype=np.float32)
+        dim = len(src.shape)
+        if dim not in (2, 3):
+            raise ValueError(f"source must be a 2D (H,W) or 3D (X,Y,Z) grid, got shape {tuple(src.shape)}")
+        self.dim = dim
+        self.is_watertight = bool(config.get("isWatertight", watertight_default))
+        self.is_double_sided = bool(config.get("isDoubleSided", False))
+        absorption = float(config.get("absorptionCoeff", 0.0))
+        if dim == 2:
+            flip = bool(config.get("flipOrientation", flip_default))
+            normalize = bool(config.get("normalizeDomain", False))
+        else:  # scene_3d.h reads flipOrientation/normalizeDomain but never applies them
+            flip, normalize = False, False
+        v, ix = _engine.load_obj(boundary, dim, flip, normalize)
+        dv = dix = None
+        if config.get("dirichletBoundary"):
+            dv, dix = _engine.load_obj(config["dirichletBoundary"], dim, flip, normalize)
+        if device is None:
+            device = int(os.environ.get("WOS_DEVICE", os.environ.get("LOCAL_RANK", 0)))
+        self._scene = _engine.WosScene(v, ix, src, absorption, dvertices=dv, dprims=dix,
+                                       dirichlet_value=float(config.get("dirichletValue", 0.0)),
+                                       watertight=self.is_watertight, double_sided=self.is_double_sided,
+                                       device=device)
+        self.bbox = self._scene.info()
+        self.last_stats = None
+
+
+def wost(scene, solverConfig, outputConfig, pts, return_numpy=False):
+    """runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d: returns
+    (points, p, grad) as nested lists (numpy arrays if return_numpy; torch
+    tensors when pts is a CUDA tensor)."""
+    _required(outputConfig, "gridRes")  # required even by the sampled path (demo.cpp:132)
+    params = _engine.solver_params(solverConfig, outputConfig)
+    if _engine._is_torch(pts) and pts.is_cuda:
+        p, g, stats = scene._scene.solve(pts, params)
+        scene.last_stats = stats
+        return pts, p, g
+    x = np.ascontiguousarray(np.asarray(pts, dtype=np.float32).reshape(-1, scene.dim))
+    p, g, stats = scene._scene.solve(x, params)
+    scene.last_stats = stats
+    if return_numpy:
+        return x, p, g
+    return x.tolist(), p.tolist(), g.tolist()
+
+
+def bvc(scene, solverConfig, outputConfig):
+    """Boundary value caching (demo.cpp:265-363) is exported by the reference but never
+    called by the time-stepper; it is out of scope for this engine."""
+    raise NotImplementedError("bvc is not provided by the MI355X engine (unused by src/2d, src/3d)")

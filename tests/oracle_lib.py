@@ -1,0 +1,181 @@
+"""ctypes bindings to the CPU oracle (oracle/build/libwos_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.  The product path never loads this library.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "libwos_oracle.so")
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int32), ("n_vertices", C.c_int32), ("n_prims", C.c_int32),
+        ("vertices", C.POINTER(C.c_float)), ("prims", C.POINTER(C.c_int32)),
+        ("n_dvertices", C.c_int32), ("n_dprims", C.c_int32),
+        ("dvertices", C.POINTER(C.c_float)), ("dprims", C.POINTER(C.c_int32)),
+        ("dirichlet_value", C.c_float), ("absorption", C.c_float),
+        ("is_watertight", C.c_int32), ("is_double_sided", C.c_int32),
+        ("source", C.POINTER(C.c_float)), ("source_dims", C.c_int32 * 3),
+    ]
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("n_walks", C.c_int32), ("max_walk_length", C.c_int32),
+        ("steps_before_tikhonov", C.c_int32), ("steps_before_maximal_spheres", C.c_int32),
+        ("epsilon_shell", C.c_float), ("min_star_radius", C.c_float),
+        ("silhouette_precision", C.c_float), ("russian_roulette_threshold", C.c_float),
+        ("boundary_distance_mask", C.c_float),
+        ("disable_gradient_control_variates", C.c_int32),
+        ("disable_gradient_antithetic_variates", C.c_int32),
+        ("use_cosine_sampling", C.c_int32), ("ignore_dirichlet", C.c_int32),
+        ("ignore_neumann", C.c_int32), ("ignore_source", C.c_int32),
+        ("seed", C.c_uint64), ("math_mode", C.c_int32), ("n_threads", C.c_int32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped",
+        "walks_max_length", "walks_rr", "walks_dirichlet", "points_estimated",
+        "rejection_iters")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = C.CDLL(ORACLE_SO)
+        L.oracle_solve.restype = C.c_int
+        L.oracle_solve.argtypes = [C.POINTER(SceneDesc), C.POINTER(Params), C.c_void_p, C.c_int64,
+                                   C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.POINTER(Stats)]
+        L.oracle_point_info.restype = C.c_int
+        L.oracle_point_info.argtypes = [C.POINTER(SceneDesc), C.c_void_p] + [C.c_void_p] * 6
+        L.oracle_bessel.restype = C.c_double
+        L.oracle_bessel.argtypes = [C.c_int, C.c_double, C.c_int]
+        L.oracle_math.restype = C.c_double
+        L.oracle_math.argtypes = [C.c_int, C.c_double, C.c_int]
+        L.oracle_seed32.restype = C.c_uint32
+        L.oracle_seed32.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.oracle_lhs.restype = C.c_int
+        L.oracle_lhs.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float)) if a is not None else None
+
+
+def _iptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else None
+
+
+class OracleScene:
+    """Keeps numpy buffers alive for the SceneDesc pointers."""
+
+    def __init__(self, vertices, prims, source, absorption, *, dvertices=None, dprims=None,
+                 dirichlet_value=0.0, watertight=True, double_sided=False):
+        self.v = np.ascontiguousarray(vertices, dtype=np.float32)
+        self.ix = np.ascontiguousarray(prims, dtype=np.int32)
+        self.dim = int(self.v.shape[1])
+        self.dv = None if dvertices is None else np.ascontiguousarray(dvertices, dtype=np.float32)
+        self.dix = None if dprims is None else np.ascontiguousarray(dprims, dtype=np.int32)
+        self.src = np.ascontiguousarray(source, dtype=np.float32)
+        d = SceneDesc()
+        d.dim = self.dim
+        d.n_vertices, d.n_prims = self.v.shape[0], self.ix.shape[0]
+        d.vertices, d.prims = _fptr(self.v), _iptr(self.ix)
+        if self.dv is not None:
+            d.n_dvertices, d.n_dprims = self.dv.shape[0], self.dix.shape[0]
+            d.dvertices, d.dprims = _fptr(self.dv), _iptr(self.dix)
+        d.dirichlet_value = dirichlet_value
+        d.absorption = absorption
+        d.is_watertight = int(watertight)
+        d.is_double_sided = int(double_sided)
+        d.source = _fptr(self.src)
+        dims = list(self.src.shape) + [0] * (3 - self.src.ndim)
+        for k in range(3):
+            d.source_dims[k] = dims[k]
+        self.desc = d
+
+
+def make_params(solver=None, output=None, *, seed=0x5EED0001, math_mode=0, n_threads=None):
+    """Build oracle params from the reference's JSON dicts (demo.cpp:121-137, grid.h:159)."""
+    s = dict(solver or {})
+    o = dict(output or {})
+    p = Params()
+    p.n_walks = int(s.get("nWalks", 128))
+    p.max_walk_length = int(s.get("maxWalkLength", 1024))
+    p.steps_before_tikhonov = int(s.get("setpsBeforeApplyingTikhonov", p.max_walk_length))
+    p.steps_before_maximal_spheres = int(s.get("setpsBeforeUsingMaximalSpheres", p.max_walk_length))
+    p.epsilon_shell = float(s.get("epsilonShell", 1e-3))
+    p.min_star_radius = float(s.get("minStarRadius", 1e-3))
+    p.silhouette_precision = float(s.get("silhouettePrecision", 1e-3))
+    p.russian_roulette_threshold = float(s.get("russianRouletteThreshold", 0.0))
+    p.boundary_distance_mask = float(o.get("boundaryDistanceMask", 0.0))
+    p.disable_gradient_control_variates = int(bool(s.get("disableGradientControlVariates", False)))
+    p.disable_gradient_antithetic_variates = int(bool(s.get("disableGradientAntitheticVariates", False)))
+    p.use_cosine_sampling = int(bool(s.get("useCosineSamplingForDirectionalDerivatives", False)))
+    p.ignore_dirichlet = int(bool(s.get("ignoreDirichlet", False)))
+    p.ignore_neumann = int(bool(s.get("ignoreNeumann", False)))
+    p.ignore_source = int(bool(s.get("ignoreSource", False)))
+    p.seed = int(s.get("seed", seed))
+    p.math_mode = math_mode
+    p.n_threads = n_threads or (os.cpu_count() or 1)
+    return p
+
+
+def solve(scene: OracleScene, params: Params, pts, index_base=0, index_stride=1):
+    pts = np.ascontiguousarray(pts, dtype=np.float32)
+    n = pts.shape[0]
+    p = np.zeros(n, np.float32)
+    g = np.zeros((n, scene.dim), np.float32)
+    nest = np.zeros(n, np.int32)
+    steps = np.zeros(n, np.int32)
+    st = Stats()
+    rc = lib().oracle_solve(C.byref(scene.desc), C.byref(params), pts.ctypes.data, n,
+                            index_base, index_stride, p.ctypes.data, g.ctypes.data,
+                            nest.ctypes.data, steps.ctypes.data, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve failed rc={rc}")
+    return p, g, nest, steps, st.as_dict()
+
+
+def point_info(scene: OracleScene, pt):
+    pt = np.ascontiguousarray(pt, dtype=np.float32)
+    out = [C.c_float(), C.c_float(), C.c_float(), C.c_int32(), C.c_float(), C.c_int32()]
+    rc = lib().oracle_point_info(C.byref(scene.desc), pt.ctypes.data, *[C.addressof(o) for o in out])
+    if rc != 0:
+        raise RuntimeError("oracle_point_info failed")
+    keys = ["dirichlet_dist", "neumann_dist", "signed_neumann_dist", "inside", "star_radius", "n_silhouettes"]
+    return {k: o.value for k, o in zip(keys, out)}
+
+
+def lhs(seed, n, dims):
+    out = np.zeros(n * dims, np.float32)
+    lib().oracle_lhs(seed, n, dims, out.ctypes.data)
+    return out
+
+
+def seed32(key, idx, pair, tag):
+    return int(lib().oracle_seed32(key, idx, pair, tag))

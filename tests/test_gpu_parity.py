@@ -1,0 +1,177 @@
+"""GPU parity: the HIP kernel (through the C ABI) vs the CPU oracle restatement.
+
+Bar: bit-exact on fixed seeds.  Both sides run the same counter-based RNG layout
+and the same deterministic math (det mode), with -ffp-contract=off on both, so
+every rejection / roulette decision, every walk and every Welford update must
+agree exactly.  Full-size (64k point) runs are checked through properties that
+do not need the oracle (determinism, shard invariance, finiteness, agreement of
+aggregate statistics with an oracle subset).
+"""
+import numpy as np
+import pytest
+
+import objparse
+from wos_amd import WosScene, selftest_math, solver_params, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_math_mode_det(oracle, which, x):
+    return np.array([oracle.lib().oracle_math(which if which < 5 else which, float(v), 0) for v in x])
+
+
+@pytest.mark.parametrize("which,lo,hi", [(0, -745, 709), (1, 1e-300, 1e300), (2, -20, 20), (3, -20, 20),
+                                         (4, -50, 50), (5, 0, 1e6)])
+def test_math_double_bit_exact(gpu, oracle, which, lo, hi):
+    rng = np.random.default_rng(which)
+    if which == 1 or which == 5:
+        x = np.exp(rng.uniform(np.log(max(lo, 1e-300)), np.log(hi), 20000))
+    else:
+        x = rng.uniform(lo, hi, 20000)
+    got = selftest_math(which, x)
+    if which == 5:
+        ref = np.sqrt(x)
+    else:
+        ref = np.array([oracle.lib().oracle_math(which, float(v), 0) for v in x])
+    np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("which", [6, 7, 8, 9])
+def test_bessel_bit_exact(gpu, oracle, which):
+    rng = np.random.default_rng(which)
+    x = np.concatenate([rng.uniform(1e-4, 4.0, 5000), rng.uniform(3.7, 120.0, 5000), [2.0, 3.75, 1e-3]])
+    got = selftest_math(which, x)
+    ref = np.array([oracle.lib().oracle_bessel(which - 6, float(v), 0) for v in x])
+    np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("which", [10, 11, 12, 13, 14])
+def test_math_float_bit_exact(gpu, oracle, which):
+    rng = np.random.default_rng(which)
+    if which == 11:
+        x = np.exp(rng.uniform(-80, 80, 20000)).astype(np.float32).astype(np.float64)
+    elif which == 14:
+        x = rng.uniform(0, 1, 20000).astype(np.float32).astype(np.float64)
+    else:
+        x = rng.uniform(-20, 20, 20000).astype(np.float32).astype(np.float64)
+    got = selftest_math(which, x)
+    ref = np.array([oracle.lib().oracle_math(which, float(v), 0) for v in x])
+    np.testing.assert_array_equal(got, ref)
+
+
+def _pair(cfg, oracle, dim=2):
+    v, ix = objparse.load(cfg["obj"], dim)
+    lam = float(cfg["scene"]["absorptionCoeff"])
+    osc = oracle.OracleScene(v, ix, cfg["source"], lam, watertight=True)
+    sc = WosScene(v, ix, cfg["source"], lam, watertight=True)
+    return osc, sc
+
+
+def _compare(oracle, osc, sc, cfg, pts, seed=0x5EED0001):
+    prm_o = oracle.make_params(cfg["solver"], cfg["output"], seed=seed, math_mode=0)
+    p0, g0, ne0, st0, s0 = oracle.solve(osc, prm_o, pts)
+    prm = solver_params(cfg["solver"], cfg["output"], seed=seed)
+    p1, g1, s1, ne1, st1 = sc.solve(pts, prm, counts=True)
+    np.testing.assert_array_equal(ne1, ne0)
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(p1.view(np.uint32), p0.view(np.uint32))
+    np.testing.assert_array_equal(g1.view(np.uint32), g0.view(np.uint32))
+    for k in ("walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_rr",
+              "points_estimated", "rejection_iters"):
+        assert s1[k] == s0[k], k
+    return p1, g1, s1
+
+
+def test_karman_bit_exact(gpu, oracle):
+    cfg = workloads.karman_config(n_walks=128)
+    osc, sc = _pair(cfg, oracle)
+    pts = cfg["points"][:2048]
+    _compare(oracle, osc, sc, cfg, pts)
+
+
+def test_karman_grid_and_edges_bit_exact(gpu, oracle):
+    """256x128 grid subset + points outside the domain / on the open ends / near walls."""
+    cfg = workloads.karman_config(n_walks=128, grid_points=True)
+    osc, sc = _pair(cfg, oracle)
+    pts = cfg["points"][::16]
+    c, r = workloads.karman_obstacle(workloads.scene_size(workloads.KARMAN_OBJ))
+    extra = np.array([[c[0], c[1]], [c[0] + r * 0.5, c[1]], [-1.2, 0.0], [2.0, 0.0], [0.0, 0.5995],
+                      [0.0, -0.5980], [-1.1032, 0.1], [1.9067, -0.2], [0.0, 0.0]], np.float32)
+    _compare(oracle, osc, sc, cfg, np.concatenate([pts, extra]))
+
+
+@pytest.mark.parametrize("nw", [1, 2, 5, 32, 200])
+def test_walk_counts_bit_exact(gpu, oracle, nw):
+    """odd / tiny / >64-pair walk counts (multiple statistics chunks)."""
+    cfg = workloads.karman_config(n_walks=nw)
+    osc, sc = _pair(cfg, oracle)
+    _compare(oracle, osc, sc, cfg, cfg["points"][:256])
+
+
+@pytest.mark.parametrize("flag", ["disableGradientControlVariates", "disableGradientAntitheticVariates",
+                                  "useCosineSamplingForDirectionalDerivatives", "ignoreSource",
+                                  "ignoreNeumann"])
+def test_solver_flags_bit_exact(gpu, oracle, flag):
+    cfg = workloads.karman_config(n_walks=64)
+    cfg["solver"][flag] = True
+    osc, sc = _pair(cfg, oracle)
+    _compare(oracle, osc, sc, cfg, cfg["points"][:256])
+
+
+def test_harmonic_then_tikhonov_bit_exact(gpu, oracle):
+    cfg = workloads.karman_config(n_walks=64)
+    cfg["solver"]["setpsBeforeApplyingTikhonov"] = 2
+    cfg["solver"]["russianRouletteThreshold"] = 0.5
+    cfg["solver"]["maxWalkLength"] = 64
+    osc, sc = _pair(cfg, oracle)
+    _compare(oracle, osc, sc, cfg, cfg["points"][:256])
+
+
+def test_taylorgreen_bit_exact(gpu, oracle):
+    """Config A (square of side 2*pi): includes the float-overflow (NaN) regime of the
+    2D Yukawa kernel for large balls (SURVEY.md §7.2 hard part 4)."""
+    cfg = workloads.taylorgreen_config(n_walks=32, res=16)
+    cfg["solver"]["maxWalkLength"] = 200
+    osc, sc = _pair(cfg, oracle)
+    _compare(oracle, osc, sc, cfg, cfg["points"])
+
+
+def test_dirichlet_obstacle_bit_exact(gpu, oracle):
+    cfg = workloads.dirichlet_obstacle_config(n_walks=64, res=24)
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"],
+                             dvertices=cfg["dvertices"], dprims=cfg["dprims"],
+                             dirichlet_value=1.0, watertight=True)
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], dvertices=cfg["dvertices"],
+                  dprims=cfg["dprims"], dirichlet_value=1.0, watertight=True)
+    _compare(oracle, osc, sc, cfg, cfg["points"])
+
+
+def test_cube3d_bit_exact(gpu, oracle):
+    cfg = workloads.cube_config(res=10, n_walks=64)
+    osc, sc = _pair(cfg, oracle, dim=3)
+    _compare(oracle, osc, sc, cfg, cfg["points"])
+
+
+def test_karman_full_size_properties(gpu, oracle):
+    """64k points x 128 walks (BASELINE config B): determinism, shard invariance,
+    finiteness, and the oracle on a strided subset matches bit for bit."""
+    cfg = workloads.karman_config(n_walks=128)
+    osc, sc = _pair(cfg, oracle)
+    pts = cfg["points"]
+    prm = solver_params(cfg["solver"], cfg["output"])
+    p1, g1, s1 = sc.solve(pts, prm)
+    p2, g2, s2 = sc.solve(pts, prm)
+    np.testing.assert_array_equal(p1, p2)
+    np.testing.assert_array_equal(g1, g2)
+    assert np.isfinite(p1).all() and np.isfinite(g1).all()
+    # shard invariance: odd-indexed points solved alone with their global indices
+    pe, ge, _ = sc.solve(pts[1::2], prm, index_base=1, index_stride=2)
+    np.testing.assert_array_equal(pe, p1[1::2])
+    np.testing.assert_array_equal(ge, g1[1::2])
+    # oracle subset at global indices
+    sub = np.arange(0, pts.shape[0], 97)
+    prm_o = oracle.make_params(cfg["solver"], cfg["output"], math_mode=0)
+    po, go, _, _, _ = oracle.solve(osc, prm_o, pts[sub], index_base=0, index_stride=97)
+    np.testing.assert_array_equal(po, p1[sub])
+    np.testing.assert_array_equal(go, g1[sub])
+    assert s1["walks_recorded"] > 0.9 * 128 * pts.shape[0]

@@ -869,7 +869,7 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
     uint32_t pt_steps = 0;
 
     if (estimate) {
-      c_pts++;
+      if (lane == 0) c_pts++;
       // ---- stratified samples (sampling.h:435-457), per-point stream
       const int nstrat = 2 * npairs;
       if (lane == 0) {

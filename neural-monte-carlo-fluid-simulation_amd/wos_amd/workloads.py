@@ -115,8 +115,13 @@ def karman_config(n_walks=128, n_points=65536, seed=1234, grid_points=False):
             "source": src, "points": pts, "obj": KARMAN_OBJ}
 
 
-def taylorgreen_config(n_walks=32, res=32):
-    """Config A: taylorgreen 2D on square.obj, 32x32 cell-centred points, 32 walks."""
+def taylorgreen_config(n_walks=32, res=32, flip=False):
+    """Config A: taylorgreen 2D on square.obj, 32x32 cell-centred points, 32 walks.
+
+    As shipped (flipOrientation false) square.obj's segments run clockwise, so their
+    normals (s.y,-s.x) point INTO the square and the reference's insideDomain
+    (fcpw_scene_loader.h:642-648) classifies every interior point as outside: the
+    reference returns p = grad p = 0 there.  flip=True gives the meaningful problem."""
     size = scene_size(SQUARE_OBJ)
     L = size[1] - size[0]
     grid = uniform_grid_2d(1000, size, with_boundary=True)
@@ -127,8 +132,9 @@ def taylorgreen_config(n_walks=32, res=32):
     X, Y = np.meshgrid(xs, ys, indexing="xy")
     pts = np.stack([X.ravel(), Y.ravel()], -1).astype(np.float32)
     solver = dict(SOLVER_BASE, nWalks=n_walks)
-    return {"name": "taylorgreen2d", "dim": 2, "scene": dict(SCENE_BASE, boundary=SQUARE_OBJ), "solver": solver,
-            "output": dict(OUTPUT_BASE), "source": src, "points": pts, "obj": SQUARE_OBJ}
+    return {"name": "taylorgreen2d", "dim": 2, "scene": dict(SCENE_BASE, boundary=SQUARE_OBJ, flipOrientation=flip),
+            "solver": solver, "output": dict(OUTPUT_BASE), "source": src, "points": pts, "obj": SQUARE_OBJ,
+            "flip": flip}
 
 
 def box_2d(L=1.0):
@@ -138,9 +144,10 @@ def box_2d(L=1.0):
     return v, ix
 
 
-def circle_2d(c, r, n=64):
-    """Clockwise circle: normals point into the disk (out of the fluid)."""
-    t = -np.arange(n) / n * 2 * np.pi
+def circle_2d(c, r, n=64, clockwise=True):
+    """Polygonal circle.  Clockwise: normals (s.y,-s.x) point into the disk, i.e. out of
+    a fluid that surrounds it (obstacle); counter-clockwise: fluid inside the disk."""
+    t = (-1.0 if clockwise else 1.0) * np.arange(n) / n * 2 * np.pi
     v = np.stack([c[0] + r * np.cos(t), c[1] + r * np.sin(t)], -1).astype(np.float32)
     ix = np.stack([np.arange(n), (np.arange(n) + 1) % n], -1).astype(np.int32)
     return v, ix

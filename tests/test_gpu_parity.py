@@ -59,8 +59,16 @@ def test_math_float_bit_exact(gpu, oracle, which):
     np.testing.assert_array_equal(got, ref)
 
 
+def assert_bits_equal(a, b):
+    """Bitwise equality; NaNs must sit at the same places (their payload/sign bits are
+    platform-defined: x86 default NaN is negative, the GPU's positive)."""
+    na, nb = np.isnan(a), np.isnan(b)
+    np.testing.assert_array_equal(na, nb)
+    np.testing.assert_array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
 def _pair(cfg, oracle, dim=2):
-    v, ix = objparse.load(cfg["obj"], dim)
+    v, ix = objparse.load(cfg["obj"], dim, flip=cfg.get("flip", False))
     lam = float(cfg["scene"]["absorptionCoeff"])
     osc = oracle.OracleScene(v, ix, cfg["source"], lam, watertight=True)
     sc = WosScene(v, ix, cfg["source"], lam, watertight=True)
@@ -74,8 +82,8 @@ def _compare(oracle, osc, sc, cfg, pts, seed=0x5EED0001):
     p1, g1, s1, ne1, st1 = sc.solve(pts, prm, counts=True)
     np.testing.assert_array_equal(ne1, ne0)
     np.testing.assert_array_equal(st1, st0)
-    np.testing.assert_array_equal(p1.view(np.uint32), p0.view(np.uint32))
-    np.testing.assert_array_equal(g1.view(np.uint32), g0.view(np.uint32))
+    assert_bits_equal(p1, p0)
+    assert_bits_equal(g1, g0)
     for k in ("walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_rr",
               "points_estimated", "rejection_iters"):
         assert s1[k] == s0[k], k
@@ -127,10 +135,12 @@ def test_harmonic_then_tikhonov_bit_exact(gpu, oracle):
     _compare(oracle, osc, sc, cfg, cfg["points"][:256])
 
 
-def test_taylorgreen_bit_exact(gpu, oracle):
-    """Config A (square of side 2*pi): includes the float-overflow (NaN) regime of the
-    2D Yukawa kernel for large balls (SURVEY.md §7.2 hard part 4)."""
-    cfg = workloads.taylorgreen_config(n_walks=32, res=16)
+@pytest.mark.parametrize("flip", [False, True])
+def test_taylorgreen_bit_exact(gpu, oracle, flip):
+    """Config A (square of side 2*pi).  As shipped every point is classified outside
+    (zero output, like the reference); flipped, it exercises the float-overflow (NaN)
+    regime of the 2D Yukawa kernel for large balls (SURVEY.md §7.2 hard part 4)."""
+    cfg = workloads.taylorgreen_config(n_walks=32, res=16, flip=flip)
     cfg["solver"]["maxWalkLength"] = 200
     osc, sc = _pair(cfg, oracle)
     _compare(oracle, osc, sc, cfg, cfg["points"])
@@ -175,3 +185,13 @@ def test_karman_full_size_properties(gpu, oracle):
     np.testing.assert_array_equal(po, p1[sub])
     np.testing.assert_array_equal(go, g1[sub])
     assert s1["walks_recorded"] > 0.9 * 128 * pts.shape[0]
+
+
+@pytest.mark.parametrize("name", ["karman_small", "taylorgreen_small", "box_dirichlet_small", "cube_small"])
+def test_gpu_matches_golden_fixture(gpu, name):
+    import os
+    import make_golden_cases as cases
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name}.npz"))
+    p, g = cases.run_case_gpu(name)
+    assert_bits_equal(p, ref["p"])
+    assert_bits_equal(g, ref["grad"])

@@ -111,8 +111,16 @@ void pack_prims(const Geom& g, std::vector<float>& prim, std::vector<float>& aux
   const int dim = g.dim, np = (int)g.ix.size();
   prim.clear(); aux.clear();
   for (int p = 0; p < np; p++) {
-    for (int k = 0; k < dim; k++)
-      for (int c = 0; c < dim; c++) prim.push_back(g.v[g.ix[p][k]].x[c]);
+    if (dim == 2) {
+      // 2D record [pa | v = pb - pa]: the edge vector every query (closest point,
+      // ray, area, sampling) uses, precomputed with the same float rounding
+      const V3 &pa = g.v[g.ix[p][0]], &pb = g.v[g.ix[p][1]];
+      prim.push_back(pa.x[0]); prim.push_back(pa.x[1]);
+      prim.push_back(pb.x[0] - pa.x[0]); prim.push_back(pb.x[1] - pa.x[1]);
+    } else {
+      for (int k = 0; k < dim; k++)
+        for (int c = 0; c < dim; c++) prim.push_back(g.v[g.ix[p][k]].x[c]);
+    }
     if (dim == 2) {
       V3 ns = seg_normal(g.v[g.ix[p][0]], g.v[g.ix[p][1]]);
       normalize(ns);

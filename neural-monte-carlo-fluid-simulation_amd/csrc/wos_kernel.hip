@@ -22,6 +22,22 @@
 
 namespace wos {
 
+#ifndef WOS_ABL_NO_SIL
+#define WOS_ABL_NO_SIL 0
+#endif
+#ifndef WOS_ABL_NO_RAY
+#define WOS_ABL_NO_RAY 0
+#endif
+#ifndef WOS_ABL_ONE_REJ
+#define WOS_ABL_ONE_REJ 0
+#endif
+#ifndef WOS_NO_FASTREJ
+#define WOS_NO_FASTREJ 0
+#endif
+#ifndef WOS_ABL_NO_STATS
+#define WOS_ABL_NO_STATS 0
+#endif
+
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
@@ -130,9 +146,23 @@ __device__ __forceinline__ float cp_triangle(const float* pa, const float* pb, c
   return normv<3>(d);
 }
 
+// closest point on a 2D segment record [pa | u = pb - pa] (same arithmetic as cp_segment)
+__device__ __forceinline__ float cp_segment_rec(const float* P, const float* x, float* pt, float* t) {
+  float u0 = P[2], u1 = P[3];
+  float v0 = x[0] - P[0], v1 = x[1] - P[1];
+  float c1 = u0 * v0 + u1 * v1, c2 = u0 * u0 + u1 * u1;
+  float tt = c1 * (1.0f / c2);
+  if (c1 <= 0.0f) tt = 0.0f;
+  if (c2 <= c1) tt = 1.0f;
+  pt[0] = P[0] + u0 * tt; pt[1] = P[1] + u1 * tt;
+  float d0 = x[0] - pt[0], d1 = x[1] - pt[1];
+  *t = tt;
+  return __builtin_sqrtf(d0 * d0 + d1 * d1);
+}
+
 template <int DIM>
 __device__ __forceinline__ float cp_prim(const float* P, const float* x, float* pt, float* t0, float* t1) {
-  if constexpr (DIM == 2) { *t1 = 0.0f; return cp_segment<2>(P, P + 2, x, pt, t0); }
+  if constexpr (DIM == 2) { *t1 = 0.0f; return cp_segment_rec(P, x, pt, t0); }
   else return cp_triangle(P, P + 3, P + 6, x, pt, t0, t1);
 }
 
@@ -219,7 +249,12 @@ __device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
 
 struct Hit { float p[3], n[3], d; };
 
-// first ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92)
+// First ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92).
+// Every primitive first goes through a division-free certain-rejection test that
+// uses the hardware reciprocal (v_rcp_f32, |rel err| <= 2^-22): signs are exact,
+// magnitudes get a 1e-5 relative margin, so only primitives the exact test could
+// accept reach the IEEE division -- the accepted set and every computed value are
+// exactly those of the plain loop (and of the oracle).
 template <int DIM>
 __device__ __forceinline__ bool ray_hit(const float* prims, int np, const float* o, const float* dir,
                                         float tmax, Hit* h) {
@@ -230,13 +265,20 @@ __device__ __forceinline__ bool ray_hit(const float* prims, int np, const float*
     const float* P = prims + p * PS;
     if constexpr (DIM == 2) {
       float u0 = P[0] - o[0], u1 = P[1] - o[1];
-      float v0 = P[2] - P[0], v1 = P[3] - P[1];
+      float v0 = P[2], v1 = P[3];
       float dv = dir[0] * v1 - dir[1] * v0;
       if (!(__builtin_fabsf(dv) > kFltEps)) continue;
+      float ud = u0 * dir[1] - u1 * dir[0];
+      float uv = u0 * v1 - u1 * v0;
+      float ra = __builtin_amdgcn_rcpf(dv);
+      float ta = ud * ra, da = uv * ra;
+      if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
+          (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
+        continue;
       float inv = 1.0f / dv;
-      float t = (u0 * dir[1] - u1 * dir[0]) * inv;
+      float t = ud * inv;
       if (!(t >= 0.0f && t <= 1.0f)) continue;
-      float d = (u0 * v1 - u1 * v0) * inv;
+      float d = uv * inv;
       if (!(d >= 0.0f && d <= rt)) continue;
       rt = d; found = true;
       h->d = d;
@@ -248,13 +290,22 @@ __device__ __forceinline__ bool ray_hit(const float* prims, int np, const float*
       cross3(pp, dir, v2);
       float det = dotv<3>(v1, pp);
       if (!(__builtin_fabsf(det) > kFltEps)) continue;
-      float inv = 1.0f / det;
-      float v = dotv<3>(s, pp) * inv;
-      if (!(v >= 0.0f && v <= 1.0f)) continue;
+      float ra = __builtin_amdgcn_rcpf(det);
+      float vn = dotv<3>(s, pp);
+      float va = vn * ra;
+      if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) continue;
       cross3(q, s, v1);
-      float w = dotv<3>(dir, q) * inv;
+      float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
+      float wa = wn * ra, da = dn * ra;
+      if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
+          (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
+        continue;
+      float inv = 1.0f / det;
+      float v = vn * inv;
+      if (!(v >= 0.0f && v <= 1.0f)) continue;
+      float w = wn * inv;
       if (!(w >= 0.0f && v + w <= 1.0f)) continue;
-      float d = dotv<3>(v2, q) * inv;
+      float d = dn * inv;
       if (!(d >= 0.0f && d <= rt)) continue;
       rt = d; found = true;
       h->d = d;
@@ -319,8 +370,17 @@ __device__ __forceinline__ float star_radius(const float* sil, int ns, int np, c
         float view[DIM], d;
         if constexpr (DIM == 2) {
           view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
-          d = normv<2>(view);
+          float d2raw = view[0] * view[0] + view[1] * view[1];
+          // certain rejection: fl(fl(sqrt(q))^2) >= q(1 - 2^-22) > r2 (no sqrt needed)
+          if (d2raw > r2 * 1.000001f) continue;
+          d = __builtin_sqrtf(d2raw);
         } else {
+          // certain rejection against the edge's bounding sphere before the exact query
+          float e[3], hl[3];
+          for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
+          float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
+          float lo = dm - hr;
+          if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) continue;
           float pt[3], t;
           d = cp_segment<3>(S, S + 3, x, pt, &t);
           for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
@@ -571,10 +631,51 @@ __device__ __forceinline__ void sample_unit_sphere(const float* u, float* out) {
   }
 }
 
-// sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720)
+// ---------------------------------------------------------------------------
+// Certified float fast path for the rejection test.  The accept decision
+// u < pdfRadius/bound is first evaluated with float Bessel approximations (same
+// A&S polynomials, hardware exp2/log2/rsq); only when |u - T| falls inside a
+// rigorous error band is the exact double-precision path (the reference's
+// arithmetic) evaluated.  The decision -- hence every RNG draw and every later
+// value -- is therefore identical to the exact loop.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float exp_fast(float x) {  // e^x to ~2 ulp for |x| < 87
+  const float L = 1.44269502162933349609375f, Llo = 1.925963033500011e-08f;
+  float hi = x * L;
+  float lo = __builtin_fmaf(x, L, -hi) + x * Llo;
+  return __builtin_amdgcn_exp2f(hi) * (1.0f + lo * 0.693147182f);
+}
+
+__device__ __forceinline__ float i0_fast(float x) {
+  if (x < 3.75f) {
+    float y = x / 3.75f;
+    y = y * y;
+    return 1.0f + y * (3.5156229f + y * (3.0899424f + y * (1.2067492f + y * (0.2659732f + y * (0.360768e-1f +
+           y * 0.45813e-2f)))));
+  }
+  float y = 3.75f / x;
+  float poly = 0.39894228f + y * (0.1328592e-1f + y * (0.225319e-2f + y * (-0.157565e-2f + y * (0.916281e-2f +
+               y * (-0.2057706e-1f + y * (0.2635537e-1f + y * (-0.1647633e-1f + y * 0.392377e-2f)))))));
+  return exp_fast(x) * __builtin_amdgcn_rsqf(x) * poly;
+}
+
+__device__ __forceinline__ float k0_fast(float x) {
+  if (x <= 2.0f) {
+    float y = x * x / 4.0f;
+    return (-__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * i0_fast(x) +
+           (-0.57721566f + y * (0.42278420f + y * (0.23069756f + y * (0.3488590e-1f + y * (0.262698e-2f +
+            y * (0.10750e-3f + y * 0.74e-5f))))));
+  }
+  float y = 2.0f / x;
+  return exp_fast(-x) * __builtin_amdgcn_rsqf(x) * (1.25331414f + y * (-0.7832358e-1f + y * (0.2189568e-1f +
+         y * (-0.1062446e-1f + y * (0.587872e-2f + y * (-0.251540e-2f + y * 0.53208e-3f))))));
+}
+
+// sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
+// need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM>
 __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg32& s, float* pdf, float* out,
-                                              uint32_t* iters) {
+                                              uint32_t* iters, bool need_pdf) {
   const float R = g.R;
   if (DIM == 3 && !g.yukawa) {
     float u1 = s.nextf(), u2 = s.nextf();
@@ -598,17 +699,33 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
   }
   // norm() depends only on the ball: hoisted out of the loop (same value every iteration)
   const float nrm = g.norm();
+  // fast path: 2D Yukawa while I0 stays finite in float (float Bessels need mu*r < ~88)
+  const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
+  const float rho = g.A0 / g.A1;
+  const float invNB = 1.0f / (nrm * bound);
   int iter = 0;
-  float p = 0.0f;
   do {
     float u = s.nextf();
     g.r = s.nextf() * R;
-    p = g.evaluate() / nrm;
-    float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
     iter++;
-    if (u < pdfRadius / bound) break;
+    int decided = -1;  // 1 accept, 0 reject, -1 undecided
+    if (fast) {
+      const float mur = g.r * g.sqrtLambda;
+      const float k0 = k0_fast(mur), ip = i0_fast(mur) * rho;
+      const float c = g.r * invNB;
+      const float Tf = (k0 - ip) * c;
+      const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
+      if (u < Tf - M) decided = 1;
+      else if (u > Tf + M) decided = 0;
+    }
+    if (decided < 0) {
+      float p = g.evaluate() / nrm;
+      float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
+      decided = u < pdfRadius / bound ? 1 : 0;
+    }
+    if (decided == 1 || WOS_ABL_ONE_REJ) break;
   } while (iter < 1000);
-  *pdf = p;
+  if (need_pdf) *pdf = g.evaluate() / nrm;  // pdf of the last sampled radius (before the clamps)
   *iters += (uint32_t)iter;
   g.r = smax(Gfn<DIM>::rClamp, g.r);
   if (g.r > R) g.r = R / 2.0f;
@@ -631,7 +748,7 @@ struct WalkState {
 template <int DIM>
 __device__ __forceinline__ float prim_area(const float* P) {
   if constexpr (DIM == 2) {
-    float s[2] = {P[2] - P[0], P[3] - P[1]};
+    float s[2] = {P[2], P[3]};  // record holds v = pb - pa
     return normv<2>(s);
   } else {
     float v1[3], v2[3], n[3];
@@ -645,7 +762,7 @@ __device__ __forceinline__ float prim_area(const float* P) {
 // (scene.h:176-181) the term is exactly +0 unless G or the throughput is
 // non-finite; only then the brute-force stochastic sample is evaluated.
 template <int DIM>
-__device__ __noinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM>& g,
+__device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM>& g,
                                           WalkState<DIM>& st, float R, const float* rn) {
   constexpr int PS = Layout<DIM>::prim;
   const int np = sc.n_prims;
@@ -676,7 +793,7 @@ __device__ __noinline__ void neumann_term(const DevScene& sc, const float* prims
   const float* P = prims + sel * PS;
   float sp[DIM], sn[DIM], pdf;
   if constexpr (DIM == 2) {
-    float s0 = P[2] - P[0], s1 = P[3] - P[1];
+    float s0 = P[2], s1 = P[3];  // record holds v = pb - pa
     float sv[2] = {s0, s1};
     float area = normv<2>(sv), u = rn[1];
     sp[0] = P[0] + u * s0; sp[1] = P[1] + u * s1;
@@ -728,7 +845,7 @@ __device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, co
         flip = true;
       }
     }
-    if (prm.steps_before_maximal_spheres <= st.walkLength) {
+    if (prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL) {
       starRadius = dirichletDist;
     } else {
       starRadius = star_radius<DIM>(sil, ns, np, st.pt, prm.min_star_radius, dirichletDist,
@@ -755,7 +872,7 @@ __device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, co
       for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
     }
     Hit ip;
-    bool hit = np > 0 && ray_hit<DIM>(prims, np, org, dir, starRadius, &ip);
+    bool hit = !WOS_ABL_NO_RAY && np > 0 && ray_hit<DIM>(prims, np, org, dir, starRadius, &ip);
     if (!hit) {
       for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
       ip.d = starRadius;
@@ -768,7 +885,7 @@ __device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, co
     }
     if (!prm.ignore_source) {
       float pdf, sp[DIM];
-      sample_volume<DIM>(g, dir, smp, &pdf, sp, iters);
+      sample_volume<DIM>(g, dir, smp, &pdf, sp, iters, false);
       if (g.r <= ip.d) {
         float contrib = g.norm() * source_value<DIM>(sc, sp);
         st.totalSource += st.throughput * contrib;
@@ -918,7 +1035,7 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
               if (a == 0) {
                 float dir[DIM];
                 sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-                sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, &witers);
+                sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, &witers, true);
               } else {
                 float sdv[DIM];
                 for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - st.pt[k];
@@ -1021,7 +1138,7 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
         }
         wave_sync();
         // ---- statistics in walk order (walk_on_stars.h:500-506,583-614)
-        const int cnt = (npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs;
+        const int cnt = WOS_ABL_NO_STATS ? 0 : ((npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs);
         for (int j = 0; j < cnt; ++j) {
           float cvb = __shfl(sMean, 0);
           float cvs = __shfl(sFirst / (float)(sN > 1 ? sN : 1), 0);
@@ -1113,6 +1230,8 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
     case 13: r = (double)fcos((float)v); break;
     case 14: r = (double)fcbrt((float)v); break;
     case 15: r = (double)__builtin_sqrtf((float)v); break;
+    case 16: r = (double)i0_fast((float)v); break;
+    case 17: r = (double)k0_fast((float)v); break;
     default: r = __builtin_nan("");
   }
   out[i] = r;

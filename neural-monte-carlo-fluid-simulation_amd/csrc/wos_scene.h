@@ -3,7 +3,7 @@
 //
 // HBM layout (all float32, structure-of-records, 16-byte aligned):
 //   prim  : Neumann primitives, packed per primitive
-//           2D  [pa.x pa.y pb.x pb.y]                          (4 floats)
+//           2D  [pa.x pa.y v.x v.y], v = pb - pa               (4 floats)
 //           3D  [pa.xyz pb.xyz pc.xyz]                         (9 floats)
 //   paux  : per-primitive normals used only by signed-distance queries
 //           2D  [na.xy nb.xy nseg.xy]  (vertex normals at the ends + segment normal)
@@ -67,6 +67,11 @@ struct DevParams {
   int32_t ignore_neumann;
   int32_t ignore_source;
   uint64_t seed;
+  // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
+  // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the
+  // per-point stratified samples in parallel.  n_jump entries.
+  const uint64_t* jump;
+  int32_t n_jump;
 };
 
 }  // namespace wos

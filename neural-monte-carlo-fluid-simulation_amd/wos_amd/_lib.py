@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libwos_hip.so")
+LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1

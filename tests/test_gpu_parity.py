@@ -195,3 +195,15 @@ def test_gpu_matches_golden_fixture(gpu, name):
     p, g = cases.run_case_gpu(name)
     assert_bits_equal(p, ref["p"])
     assert_bits_equal(g, ref["grad"])
+
+
+@pytest.mark.parametrize("which,ref_which", [(16, 0), (17, 2)])
+def test_fast_bessel_error_within_certified_band(gpu, oracle, which, ref_which):
+    """The float Bessel approximations of the rejection fast path must stay well inside
+    the 8e-6 relative band the kernel certifies its decisions with."""
+    x = np.concatenate([np.geomspace(1e-4, 2.0, 4000), np.linspace(2.0, 80.0, 8000)])
+    x = x.astype(np.float32).astype(np.float64)
+    got = selftest_math(which, x)
+    ref = np.array([oracle.lib().oracle_bessel(ref_which, float(v), 0) for v in x])
+    rel = np.abs(got - ref) / np.abs(ref)
+    assert rel.max() < 2e-6, rel.max()

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/wos.h"
+#include "wos_detmath.h"
 #include "wos_host_scene.h"
 #include "wos_launch.h"
 
@@ -56,6 +57,8 @@ struct wos_scene {
   int32_t* d_nest = nullptr;
   int32_t* d_steps = nullptr;
   size_t ws_points = 0;
+  uint64_t* d_jump = nullptr;  // PCG32 jump-ahead table (A_k, C_k), grow-only
+  int n_jump = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int num_cus = 0;
@@ -123,6 +126,7 @@ static void scene_release(wos_scene* s) {
   hipFree(s->d_source);
   hipFree(s->d_pts); hipFree(s->d_p); hipFree(s->d_g); hipFree(s->d_nest); hipFree(s->d_steps);
   hipFree(s->d_counters);
+  hipFree(s->d_jump);
   if (s->ev0) hipEventDestroy(s->ev0);
   if (s->ev1) hipEventDestroy(s->ev1);
 }
@@ -225,6 +229,25 @@ static int ensure_workspace(wos_scene* s, size_t npts) {
   return WOS_OK;
 }
 
+// state_k = A_k * state_0 + C_k for the PCG32 LCG (multiplier kPcgMult, increment kPcgInc)
+static int ensure_jump(wos_scene* s, int k_needed) {
+  if (k_needed <= s->n_jump) return WOS_OK;
+  const int cap = std::max(k_needed, 1024);
+  std::vector<uint64_t> t(2 * (size_t)cap);
+  uint64_t A = 1u, Cc = 0u;
+  for (int k = 0; k < cap; k++) {
+    t[2 * k] = A; t[2 * k + 1] = Cc;
+    A = A * wos::kPcgMult;
+    Cc = Cc * wos::kPcgMult + wos::kPcgInc;
+  }
+  hipFree(s->d_jump);
+  s->d_jump = nullptr; s->n_jump = 0;
+  HIP_TRY(hipMalloc((void**)&s->d_jump, t.size() * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpy(s->d_jump, t.data(), t.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  s->n_jump = cap;
+  return WOS_OK;
+}
+
 int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
               int64_t index_stride, float* p, float* grad, int32_t* n_est, int32_t* steps, wos_stats* stats,
               void* stream, uint32_t flags) {
@@ -260,6 +283,14 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   dp.ignore_neumann = prm->ignore_neumann;
   dp.ignore_source = prm->ignore_source;
   dp.seed = prm->seed;
+  {
+    // diagonal draws + shuffle draws of the stratified samples
+    const int k_needed = 2 * (2 * dp.n_pairs) * (dim - 1);
+    int rc = ensure_jump(s, k_needed);
+    if (rc != WOS_OK) return rc;
+    dp.jump = s->d_jump;
+    dp.n_jump = s->n_jump;
+  }
 
   // LDS: staged geometry + per-wave (stratified samples + one chunk of walk records)
   const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
@@ -268,7 +299,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   const int geom_floats = (primAl + s->host.n_sil * SS + 3) & ~3;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   const size_t shmem =
-      (size_t)(geom_floats + wos::kWavesPerBlockHost * (lhs_floats + wos::rec_floats(dim))) * sizeof(float);
+      (size_t)(geom_floats + wos::kWavesPerBlockHost * (2 * lhs_floats + wos::rec_floats(dim))) * sizeof(float);
   if (shmem > 160 * 1024)
     return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernel (" +
                                     std::to_string(shmem) + " bytes)");

@@ -251,16 +251,20 @@ WOS_HD double bessk1(double x) {
 // PCG32 (pcg32.h) + counter-based seeding
 // ---------------------------------------------------------------------------
 constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
+// every stream is seeded with initseq = 1 (the counter-based seed32 key selects
+// the stream through initstate), so the increment is the constant (1 << 1) | 1
+// and a generator is one 64-bit register pair.
+constexpr uint64_t kPcgInc = 3u;
 
 struct Pcg32 {
-  uint64_t state, inc;
-  WOS_HD void seed(uint64_t initstate, uint64_t initseq) {
-    state = 0u; inc = (initseq << 1u) | 1u;
+  uint64_t state;
+  WOS_HD void seed(uint64_t initstate) {
+    state = 0u;
     next(); state += initstate; next();
   }
   WOS_HD uint32_t next() {
     uint64_t old = state;
-    state = old * kPcgMult + inc;
+    state = old * kPcgMult + kPcgInc;
     uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
     uint32_t rot = (uint32_t)(old >> 59u);
     return (xs >> rot) | (xs << ((~rot + 1u) & 31));

@@ -741,8 +741,7 @@ struct WalkState {
   float prevDist, throughput;
   bool onNeumann;
   int walkLength;
-  float totalNeumann, totalSource, firstSource;
-  float sdir[DIM], bdir[DIM];
+  float totalNeumann, totalSource;
 };
 
 template <int DIM>
@@ -912,15 +911,227 @@ __device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, co
 // ---------------------------------------------------------------------------
 // the solve kernel
 // ---------------------------------------------------------------------------
-// Per-wave LDS scratch: stratified samples [2*n_pairs*(DIM-1)] then the walk
-// records of one chunk (SoA, 2*kChunkPairs entries each):
-//   total | first | bdir[DIM] | sdir[DIM] | code
+// One wave owns one query point at a time and runs it in three phases per chunk
+// of up to kChunkPairs antithetic pairs:
+//   1. first balls   -- lane = pair: source sample + boundary direction of the
+//                       first (maximal) ball for both members (walk_on_stars.h:
+//                       510-575); the members' start states go to LDS as tasks;
+//   2. walks         -- lanes pull walk tasks (pair, member) from a per-wave LDS
+//                       counter, so a lane that finishes a short walk takes the
+//                       next one instead of idling behind the longest pair;
+//   3. statistics    -- lanes 0..DIM fold the records in walk order, in lockstep
+//                       (one instruction stream: lane 0 the solution chain,
+//                       lane k the gradient component k-1).
+// The per-point stratified samples are drawn by all lanes at once from a PCG32
+// jump-ahead table; only the Fisher-Yates swaps stay serial (lane 0).
+//
+// Per-wave LDS (floats): strat[lhs] | partner[lhs] (int) | chunk SoA, kT = 2*kChunkPairs:
+//   records : total | first | bdir[DIM] | sdir[DIM] | code
+//   tasks   : pt[DIM] | throughput | totalSource | dirichletDist
 template <int DIM>
-struct RecLayout {
-  static constexpr int kRec = 2 * kChunkPairs;
-  static constexpr int total = 0, first = kRec, bdir = 2 * kRec, sdir = (2 + DIM) * kRec,
-                       code = (2 + 2 * DIM) * kRec, size = (3 + 2 * DIM) * kRec;
+struct ChunkLayout {
+  static constexpr int kT = 2 * kChunkPairs;
+  static constexpr int total = 0, first = kT, bdir = 2 * kT, sdir = (2 + DIM) * kT, code = (2 + 2 * DIM) * kT,
+                       pt = (3 + 2 * DIM) * kT, thr = (3 + 3 * DIM) * kT, tsrc = (4 + 3 * DIM) * kT,
+                       dd = (5 + 3 * DIM) * kT, size = (6 + 3 * DIM) * kT;
 };
+
+// stratifiedSample (sampling.h:435-457) on the per-point stream, drawn in parallel:
+// draw k of the stream is pcg_output(A_k * s0 + C_k).  Diagonal draws k < n*sd;
+// the shuffle's bounded draws follow in order (k = n*sd + i*n + j) unless one of
+// them hits PCG's rejection threshold, in which case lane 0 replays the shuffle
+// draws sequentially from the true stream.
+__device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
+  const uint64_t A = prm.jump[2 * k], Cc = prm.jump[2 * k + 1];
+  return A * s0 + Cc;
+}
+
+template <int DIM>
+__device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner, int lane) {
+  constexpr int sd = DIM - 1;
+  const int nstrat = 2 * prm.n_pairs;
+  const int nd = nstrat * sd;
+  Pcg32 ps;
+  ps.seed(seed32(prm.seed, (uint64_t)gidx, 0, 0));
+  const uint64_t s0 = ps.state;
+  const float ome = 1.0f - kFltEps;
+  const float inv = 1.0f / (float)nstrat;
+  for (int idx = lane; idx < nd; idx += kWave) {
+    const int i = sd == 1 ? idx : idx / sd;
+    const uint32_t r = pcg_output(jump_state(prm, s0, idx));
+    const float u = bits_to_float((r >> 9) | 0x3f800000u) - 1.0f;
+    strat[idx] = smin(((float)i + u) * inv, ome);
+  }
+  bool rej = false;
+  for (int idx = lane; idx < nd; idx += kWave) {
+    const int j = sd == 1 ? idx : idx % nstrat;
+    const uint32_t bound = (uint32_t)(nstrat - j);
+    const uint32_t th = (~bound + 1u) % bound;
+    const uint32_t r = pcg_output(jump_state(prm, s0, nd + idx));
+    rej |= r < th;
+    partner[idx] = j + (int)(r % bound);
+  }
+  const bool any_rej = __any(rej);
+  wave_sync();
+  if (lane == 0) {
+    if (any_rej) {  // exact replay of the sequential stream (rare: P ~ n^2 / 2^32)
+      Pcg32 q;
+      q.state = jump_state(prm, s0, nd);
+      for (int i = 0; i < sd; ++i)
+        for (int j = 0; j < nstrat; ++j) partner[i * nstrat + j] = j + (int)q.bounded((uint32_t)(nstrat - j));
+    }
+    for (int i = 0; i < sd; ++i)
+      for (int j = 0; j < nstrat; ++j) {
+        const int other = partner[i * nstrat + j];
+        const float t = strat[sd * j + i];
+        strat[sd * j + i] = strat[sd * other + i];
+        strat[sd * other + i] = t;
+      }
+  }
+  wave_sync();
+}
+
+// Phase 1: the first ball of pair w, both antithetic members (walk_on_stars.h:510-575).
+template <int DIM>
+__device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const float* x, float firstR,
+                                            const float* strat, float* ch, int64_t gidx, int w, int rbase,
+                                            bool yuk0, uint32_t* iters) {
+  using L = ChunkLayout<DIM>;
+  constexpr int sd = DIM - 1;
+  float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
+  for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
+  Pcg32 fs;
+  fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
+  for (int a = 0; a < prm.n_anti; a++) {
+    const int r = rbase + a;
+    Gfn<DIM> g;
+    g.init(yuk0, sc.absorption);
+    g.update_ball(x, firstR);
+    float throughput = 1.0f, totalSource = 0.0f, firstSource = 0.0f;
+    float sdir[DIM], bdir[DIM];
+    for (int k = 0; k < DIM; k++) sdir[k] = 0.0f;
+    if (!prm.ignore_source) {
+      if (a == 0) {
+        float dir[DIM];
+        sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
+        sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, iters, true);
+      } else {
+        float sdv[DIM];
+        for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - x[k];
+        for (int k = 0; k < DIM; k++) g.yVol[k] = x[k] - sdv[k];
+        g.r = normv<DIM>(sdv);
+      }
+      float gnorm = g.norm();
+      float contrib = gnorm * source_value<DIM>(sc, g.yVol);
+      totalSource += throughput * contrib;
+      firstSource = contrib;
+      float gr[DIM];
+      g.gradient(gr);
+      float den = sourcePdf * gnorm;
+      for (int k = 0; k < DIM; k++) sdir[k] = gr[k] / den;
+    }
+    if (a == 0) {
+      const float* u = &strat[sd * (2 * w + 1)];
+      float bd[DIM];
+      if (prm.use_cosine) {
+        if constexpr (DIM == 2) {
+          float u1 = 2.0f * u[0] - 1.0f;
+          bd[0] = u1; bd[1] = __builtin_sqrtf(smax(0.0f, 1.0f - u1 * u1));
+        } else {
+          float u1 = 2.0f * u[0] - 1.0f, u2 = 2.0f * u[1] - 1.0f, dx = 0.0f, dy = 0.0f;
+          if (!(u1 == 0 && u2 == 0)) {
+            float theta, rr;
+            if (__builtin_fabsf(u1) > __builtin_fabsf(u2)) { rr = u1; theta = (float)(0.25 * kPi * (double)(u2 / u1)); }
+            else { rr = u2; theta = (float)(0.5 * kPi * (double)(1.0f - 0.5f * (u1 / u2))); }
+            float sn, cs;
+            fsincos(theta, &sn, &cs);
+            dx = rr * cs; dy = rr * sn;
+          }
+          bd[0] = dx; bd[1] = dy; bd[2] = __builtin_sqrtf(smax(0.0f, 1.0f - (dx * dx + dy * dy)));
+        }
+        if (fs.nextf() < 0.5f) bd[DIM - 1] *= -1.0f;
+        float ct = __builtin_fabsf(bd[DIM - 1]);
+        float pdfc = DIM == 2 ? ct / 2.0f : (float)((double)ct / kPi);
+        boundaryPdf = 0.5f * pdfc;
+        // transformCoordinates (sampling.h:176-203) with n = (1,0[,0])
+        if constexpr (DIM == 2) {
+          const float n0 = 1.0f, n1 = 0.0f;
+          float s0 = n1, s1 = -n0;
+          float t0 = bd[0] * s0 + bd[1] * n0, t1 = bd[0] * s1 + bd[1] * n1;
+          bd[0] = t0; bd[1] = t1;
+        } else {
+          const float n[3] = {1.0f, 0.0f, 0.0f};
+          float sign = __builtin_copysignf(1.0f, n[2]);
+          const float aa = -1.0f / (sign + n[2]);
+          const float b = n[0] * n[1] * aa;
+          float b1[3] = {1.0f + sign * n[0] * n[0] * aa, sign * b, -sign * n[0]};
+          float b2[3] = {b, sign + n[1] * n[1] * aa, -n[1]};
+          float t[3];
+          for (int k = 0; k < 3; k++) t[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
+          for (int k = 0; k < 3; k++) bd[k] = t[k];
+        }
+      } else {
+        sample_unit_sphere<DIM>(u, bd);
+        boundaryPdf = pdf_sphere_uniform<DIM>(1.0f);
+      }
+      for (int k = 0; k < DIM; k++) { g.ySurf[k] = g.c[k] + g.R * bd[k]; boundaryPt[k] = g.ySurf[k]; }
+    } else {
+      float bd[DIM];
+      for (int k = 0; k < DIM; k++) bd[k] = boundaryPt[k] - x[k];
+      for (int k = 0; k < DIM; k++) g.ySurf[k] = x[k] - bd[k];
+    }
+    throughput *= g.poisson_kernel() / boundaryPdf;
+    {
+      float pg[DIM];
+      g.poisson_kernel_gradient(pg);
+      float den = boundaryPdf * throughput;
+      for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
+    }
+    ch[L::first + r] = firstSource;
+    for (int k = 0; k < DIM; k++) {
+      ch[L::bdir + k * L::kT + r] = bdir[k];
+      ch[L::sdir + k * L::kT + r] = sdir[k];
+      ch[L::pt + k * L::kT + r] = g.ySurf[k];
+    }
+    ch[L::thr + r] = throughput;
+    ch[L::tsrc + r] = totalSource;
+    ch[L::dd + r] = dirichlet_dist_lane<DIM>(sc, g.ySurf);
+  }
+}
+
+// Phase 2: one walk task (record r of the chunk; pair w's walk stream).
+template <int DIM>
+__device__ __forceinline__ uint32_t walk_task(const DevScene& sc, const DevParams& prm, const float* Lprim,
+                                              const float* Lsil, float* ch, int64_t gidx, int w, int r, bool yuk0,
+                                              uint32_t* iters, unsigned int* s_ctr) {
+  using L = ChunkLayout<DIM>;
+  WalkState<DIM> st;
+  for (int k = 0; k < DIM; k++) { st.pt[k] = ch[L::pt + k * L::kT + r]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
+  // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
+  // and they are rewritten by every step before that can happen
+  st.prevDist = 0.0f;
+  st.throughput = ch[L::thr + r];
+  st.onNeumann = false;
+  st.walkLength = 0;
+  st.totalNeumann = 0.0f;
+  st.totalSource = ch[L::tsrc + r];
+  const float dd = ch[L::dd + r];
+  Gfn<DIM> g;
+  g.init(yuk0, sc.absorption);
+  Pcg32 ws;
+  ws.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 2));
+  uint32_t wsteps = 1;  // the first ball
+  const int code = walk<DIM>(sc, prm, Lprim, Lsil, dd, ws, g, st, &wsteps, iters);
+  const bool recorded = code == WC_DIRICHLET || code == WC_RR;
+  if (recorded) {
+    const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
+    ch[L::total + r] = st.throughput * term + st.totalNeumann + st.totalSource;
+  }
+  ch[L::code + r] = recorded ? 1.0f : 0.0f;
+  atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
+  atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);
+  return wsteps;
+}
 
 template <int DIM>
 __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
@@ -928,7 +1139,10 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
     int64_t stride, float* __restrict__ p_out, float* __restrict__ g_out, int32_t* __restrict__ nest_out,
     int32_t* __restrict__ steps_out, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work,
     int geom_floats, int lhs_floats) {
+  using L = ChunkLayout<DIM>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ unsigned int s_ctr[C_NUM];
+  __shared__ unsigned int s_task[kWavesPerBlock];
   constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -938,16 +1152,16 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
   const int primAl = (primN + 3) & ~3;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
   for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
+  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
   __syncthreads();
   const float* Lprim = smem;
   const float* Lsil = smem + primAl;
-  float* wbase = smem + geom_floats + wave * (lhs_floats + RecLayout<DIM>::size);
+  float* wbase = smem + geom_floats + wave * (2 * lhs_floats + L::size);
   float* strat = wbase;
-  float* rec = wbase + lhs_floats;
+  int* partner = (int*)(wbase + lhs_floats);
+  float* ch = wbase + 2 * lhs_floats;
 
-  uint32_t c_steps = 0, c_wasted = 0, c_rec = 0, c_esc = 0, c_maxl = 0, c_rr = 0, c_dir = 0, c_pts = 0, c_iters = 0;
-
-  const int sd = DIM - 1;
+  uint32_t c_iters = 0;
   const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
 
@@ -980,193 +1194,51 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
                   : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
     const bool estimate = inside || sc.double_sided;
 
-    // statistics registers: lane 0 = solution chain, lanes 1..DIM = gradient components
-    float sMean = 0.0f, sM2 = 0.0f, sFirst = 0.0f;
+    // statistics registers: lane 0 = solution chain, lanes 1..DIM = gradient
+    // components; sN / sFirst are identical in every lane
+    float sMean = 0.0f, sFirst = 0.0f;
     int sN = 0;
     uint32_t pt_steps = 0;
 
     if (estimate) {
-      if (lane == 0) c_pts++;
-      // ---- stratified samples (sampling.h:435-457), per-point stream
-      const int nstrat = 2 * npairs;
-      if (lane == 0) {
-        Pcg32 ps;
-        ps.seed(seed32(prm.seed, (uint64_t)gidx, 0, 0), 1u);
-        const float ome = 1.0f - kFltEps;
-        const float inv = 1.0f / (float)nstrat;
-        for (int i = 0; i < nstrat; ++i)
-          for (int j = 0; j < sd; ++j) {
-            float sj = ((float)i + ps.nextf()) * inv;
-            strat[sd * i + j] = smin(sj, ome);
-          }
-        for (int i = 0; i < sd; ++i)
-          for (int j = 0; j < nstrat; ++j) {
-            int other = j + (int)ps.bounded((uint32_t)(nstrat - j));
-            float t = strat[sd * j + i];
-            strat[sd * j + i] = strat[sd * other + i];
-            strat[sd * other + i] = t;
-          }
-      }
-      wave_sync();
-
-      const float boundaryDist = smin(dDist, nDist);
-      const float firstR = 0.99f * boundaryDist;
+      if (lane == 0) atomicAdd(&s_ctr[C_PTS], 1u);
+      build_lhs<DIM>(prm, gidx, strat, partner, lane);
+      const float firstR = 0.99f * smin(dDist, nDist);
+      const int kk = (lane >= 1 && lane <= DIM) ? lane - 1 : 0;
 
       for (int c0 = 0; c0 < npairs; c0 += kChunkPairs) {
-        const int w = c0 + lane;
-        if (w < npairs) {
-          float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
-          for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
-          Pcg32 fs;
-          fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1), 1u);
-          const uint32_t wseed = seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 2);
-          for (int a = 0; a < prm.n_anti; a++) {
-            Gfn<DIM> g;
-            g.init(yuk0, sc.absorption);
-            WalkState<DIM> st;
-            for (int k = 0; k < DIM; k++) {
-              st.pt[k] = x[k]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; st.sdir[k] = 0.0f; st.bdir[k] = 0.0f;
-            }
-            st.prevDist = 0.0f; st.throughput = 1.0f; st.onNeumann = false; st.walkLength = 0;
-            st.totalNeumann = 0.0f; st.totalSource = 0.0f; st.firstSource = 0.0f;
-            g.update_ball(st.pt, firstR);
-            uint32_t wsteps = 1, witers = 0;
-            if (!prm.ignore_source) {
-              if (a == 0) {
-                float dir[DIM];
-                sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-                sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, &witers, true);
-              } else {
-                float sdv[DIM];
-                for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - st.pt[k];
-                for (int k = 0; k < DIM; k++) g.yVol[k] = st.pt[k] - sdv[k];
-                g.r = normv<DIM>(sdv);
-              }
-              float gnorm = g.norm();
-              float contrib = gnorm * source_value<DIM>(sc, g.yVol);
-              st.totalSource += st.throughput * contrib;
-              st.firstSource = contrib;
-              float gr[DIM];
-              g.gradient(gr);
-              float den = sourcePdf * gnorm;
-              for (int k = 0; k < DIM; k++) st.sdir[k] = gr[k] / den;
-            }
-            if (a == 0) {
-              const float* u = &strat[sd * (2 * w + 1)];
-              float bd[DIM];
-              if (prm.use_cosine) {
-                if constexpr (DIM == 2) {
-                  float u1 = 2.0f * u[0] - 1.0f;
-                  bd[0] = u1; bd[1] = __builtin_sqrtf(smax(0.0f, 1.0f - u1 * u1));
-                } else {
-                  float u1 = 2.0f * u[0] - 1.0f, u2 = 2.0f * u[1] - 1.0f, dx = 0.0f, dy = 0.0f;
-                  if (!(u1 == 0 && u2 == 0)) {
-                    float theta, r;
-                    if (__builtin_fabsf(u1) > __builtin_fabsf(u2)) { r = u1; theta = (float)(0.25 * kPi * (double)(u2 / u1)); }
-                    else { r = u2; theta = (float)(0.5 * kPi * (double)(1.0f - 0.5f * (u1 / u2))); }
-                    float sn, cs;
-                    fsincos(theta, &sn, &cs);
-                    dx = r * cs; dy = r * sn;
-                  }
-                  bd[0] = dx; bd[1] = dy; bd[2] = __builtin_sqrtf(smax(0.0f, 1.0f - (dx * dx + dy * dy)));
-                }
-                if (fs.nextf() < 0.5f) bd[DIM - 1] *= -1.0f;
-                float ct = __builtin_fabsf(bd[DIM - 1]);
-                float pdfc = DIM == 2 ? ct / 2.0f : (float)((double)ct / kPi);
-                boundaryPdf = 0.5f * pdfc;
-                // transformCoordinates (sampling.h:176-203) with n = (1,0[,0])
-                if constexpr (DIM == 2) {
-                  const float n0 = 1.0f, n1 = 0.0f;
-                  float s0 = n1, s1 = -n0;
-                  float t0 = bd[0] * s0 + bd[1] * n0, t1 = bd[0] * s1 + bd[1] * n1;
-                  bd[0] = t0; bd[1] = t1;
-                } else {
-                  const float n[3] = {1.0f, 0.0f, 0.0f};
-                  float sign = __builtin_copysignf(1.0f, n[2]);
-                  const float aa = -1.0f / (sign + n[2]);
-                  const float b = n[0] * n[1] * aa;
-                  float b1[3] = {1.0f + sign * n[0] * n[0] * aa, sign * b, -sign * n[0]};
-                  float b2[3] = {b, sign + n[1] * n[1] * aa, -n[1]};
-                  float t[3];
-                  for (int k = 0; k < 3; k++) t[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
-                  for (int k = 0; k < 3; k++) bd[k] = t[k];
-                }
-              } else {
-                sample_unit_sphere<DIM>(u, bd);
-                boundaryPdf = pdf_sphere_uniform<DIM>(1.0f);
-              }
-              for (int k = 0; k < DIM; k++) { g.ySurf[k] = g.c[k] + g.R * bd[k]; boundaryPt[k] = g.ySurf[k]; }
-            } else {
-              float bd[DIM];
-              for (int k = 0; k < DIM; k++) bd[k] = boundaryPt[k] - st.pt[k];
-              for (int k = 0; k < DIM; k++) g.ySurf[k] = st.pt[k] - bd[k];
-            }
-            st.prevDist = g.R;
-            for (int k = 0; k < DIM; k++) st.prevDir[k] = (g.ySurf[k] - st.pt[k]) / g.R;
-            for (int k = 0; k < DIM; k++) st.pt[k] = g.ySurf[k];
-            st.throughput *= g.poisson_kernel() / boundaryPdf;
-            {
-              float pg[DIM];
-              g.poisson_kernel_gradient(pg);
-              float den = boundaryPdf * st.throughput;
-              for (int k = 0; k < DIM; k++) st.bdir[k] = pg[k] / den;
-            }
-            const float dd = dirichlet_dist_lane<DIM>(sc, st.pt);
-            Pcg32 ws;
-            ws.seed(wseed, 1u);
-            const int code = walk<DIM>(sc, prm, Lprim, Lsil, dd, ws, g, st, &wsteps, &witers);
-            c_iters += witers;
-            pt_steps += wsteps;
-            const int r = lane * prm.n_anti + a;
-            const bool recorded = code == WC_DIRICHLET || code == WC_RR;
-            if (recorded) {
-              const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
-              rec[RecLayout<DIM>::total + r] = st.throughput * term + st.totalNeumann + st.totalSource;
-              c_steps += wsteps; c_rec++;
-              if (code == WC_RR) c_rr++; else c_dir++;
-            } else {
-              c_wasted += wsteps;
-              if (code == WC_ESCAPED) c_esc++; else c_maxl++;
-            }
-            rec[RecLayout<DIM>::first + r] = st.firstSource;
-            for (int k = 0; k < DIM; k++) {
-              rec[RecLayout<DIM>::bdir + k * RecLayout<DIM>::kRec + r] = st.bdir[k];
-              rec[RecLayout<DIM>::sdir + k * RecLayout<DIM>::kRec + r] = st.sdir[k];
-            }
-            rec[RecLayout<DIM>::code + r] = recorded ? 1.0f : 0.0f;
-          }
+        const int cnt = (npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs;
+        // ---- phase 1: first balls, lane = pair
+        if (lane < cnt) first_balls<DIM>(sc, prm, x, firstR, strat, ch, gidx, c0 + lane, lane * prm.n_anti, yuk0,
+                                         &c_iters);
+        if (lane == 0) s_task[wave] = kWave;
+        wave_sync();
+        // ---- phase 2: walk tasks pulled from the wave's LDS counter
+        const int ntask = cnt * prm.n_anti;
+        for (int t = lane; t < ntask;) {
+          const int pr = prm.n_anti == 2 ? (t >> 1) : t;
+          pt_steps += walk_task<DIM>(sc, prm, Lprim, Lsil, ch, gidx, c0 + pr, t, yuk0, &c_iters, s_ctr);
+          t = (int)atomicAdd(&s_task[wave], 1u);
         }
         wave_sync();
-        // ---- statistics in walk order (walk_on_stars.h:500-506,583-614)
-        const int cnt = WOS_ABL_NO_STATS ? 0 : ((npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs);
-        for (int j = 0; j < cnt; ++j) {
-          float cvb = __shfl(sMean, 0);
-          float cvs = __shfl(sFirst / (float)(sN > 1 ? sN : 1), 0);
+        // ---- phase 3: statistics in walk order (walk_on_stars.h:500-506,583-614)
+        const int nfold = WOS_ABL_NO_STATS ? 0 : cnt;
+        for (int j = 0; j < nfold; ++j) {
+          float cvb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sMean), 0));
+          float cvs = sFirst / (float)(sN > 1 ? sN : 1);
           if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
           for (int a = 0; a < prm.n_anti; a++) {
             const int r = j * prm.n_anti + a;
-            if (rec[RecLayout<DIM>::code + r] == 0.0f) continue;
-            const float total = rec[RecLayout<DIM>::total + r];
-            const float first = rec[RecLayout<DIM>::first + r];
-            if (lane == 0) {
-              sN += 1;
-              float delta = total - sMean;
-              sMean += delta / (float)sN;
-              float delta2 = total - sMean;
-              sM2 += delta * delta2;
-              sFirst += first;
-            } else if (lane <= DIM) {
-              const int k = lane - 1;
-              const float bc = total - first;
-              const float be = (bc - cvb) * rec[RecLayout<DIM>::bdir + k * RecLayout<DIM>::kRec + r];
-              const float se = (first - cvs) * rec[RecLayout<DIM>::sdir + k * RecLayout<DIM>::kRec + r];
-              const float ge = be + se;
-              sN += 1;
-              float delta = ge - sMean;
-              sMean += delta / (float)sN;
-              float delta2 = ge - sMean;
-              sM2 += delta * delta2;
-            }
+            if (ch[L::code + r] == 0.0f) continue;
+            const float total = ch[L::total + r];
+            const float first = ch[L::first + r];
+            const float be = (total - first - cvb) * ch[L::bdir + kk * L::kT + r];
+            const float se = (first - cvs) * ch[L::sdir + kk * L::kT + r];
+            const float xv = lane == 0 ? total : be + se;
+            sN += 1;
+            const float delta = xv - sMean;
+            sMean += delta / (float)sN;
+            sFirst += first;
           }
         }
         wave_sync();
@@ -1189,15 +1261,24 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
       for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
       if (lane == 0) steps_out[idx] = (int32_t)s;
     }
+    // keep the 32-bit LDS counters far from wrapping on huge launches
+    if (lane == 0 && s_ctr[C_STEPS] + s_ctr[C_WASTED] > (1u << 30)) {
+      atomicAdd(&counters[C_STEPS], (unsigned long long)atomicExch(&s_ctr[C_STEPS], 0u));
+      atomicAdd(&counters[C_WASTED], (unsigned long long)atomicExch(&s_ctr[C_WASTED], 0u));
+    }
   }
 
-  // ---- counters: wave reduction + one atomic per wave
-  uint32_t vals[C_NUM] = {c_steps, c_wasted, c_rec, c_esc, c_maxl, c_rr, c_dir, c_pts, c_iters};
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) {
-    unsigned long long v = vals[i];
+  // ---- counters: rejection iterations per lane (wave reduction), the rest from LDS
+  {
+    unsigned long long v = c_iters;
     for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0 && v) atomicAdd(&counters[i], v);
+    if (lane == 0 && v) atomicAdd(&counters[C_ITERS], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS) {
+    unsigned int v = s_ctr[threadIdx.x];
+    if (threadIdx.x == C_REC) v = s_ctr[C_RR] + s_ctr[C_DIR];
+    if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
   }
 }
 
@@ -1241,7 +1322,7 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
 // ---------------------------------------------------------------------------
 // host-side launchers (called from wos_capi.hip)
 // ---------------------------------------------------------------------------
-int rec_floats(int dim) { return dim == 2 ? RecLayout<2>::size : RecLayout<3>::size; }
+int rec_floats(int dim) { return dim == 2 ? ChunkLayout<2>::size : ChunkLayout<3>::size; }
 
 hipError_t launch_solve(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                         int64_t base, int64_t stride, float* p, float* g, int32_t* nest, int32_t* steps,

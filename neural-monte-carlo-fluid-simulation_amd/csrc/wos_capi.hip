@@ -59,6 +59,10 @@ struct wos_scene {
   size_t ws_points = 0;
   uint64_t* d_jump = nullptr;  // PCG32 jump-ahead table (A_k, C_k), grow-only
   int n_jump = 0;
+  float* d_tasks = nullptr;      // walk-task workspace (DevTasks arrays), grow-only
+  int64_t task_cap = 0;          // tasks
+  int32_t* d_pstate = nullptr;   // per-point state of one batch
+  int64_t pstate_cap = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int num_cus = 0;
@@ -127,6 +131,8 @@ static void scene_release(wos_scene* s) {
   hipFree(s->d_pts); hipFree(s->d_p); hipFree(s->d_g); hipFree(s->d_nest); hipFree(s->d_steps);
   hipFree(s->d_counters);
   hipFree(s->d_jump);
+  hipFree(s->d_tasks);
+  hipFree(s->d_pstate);
   if (s->ev0) hipEventDestroy(s->ev0);
   if (s->ev1) hipEventDestroy(s->ev1);
 }
@@ -167,7 +173,7 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
       e = hipMemcpy(s->d_source, d->source, nsrc * sizeof(float),
                     d->source_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) e = hipMalloc((void**)&s->d_counters, (wos::kNumCounters + 1) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&s->d_counters, wos::kNumCounterSlots * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipEventCreate(&s->ev0);
   if (e == hipSuccess) e = hipEventCreate(&s->ev1);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&s->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -227,6 +233,45 @@ static int ensure_workspace(wos_scene* s, size_t npts) {
   HIP_TRY(hipMalloc((void**)&s->d_steps, cap * sizeof(int32_t)));
   s->ws_points = cap;
   return WOS_OK;
+}
+
+// walk tasks per batch: 2^24 tasks = 0.8 GB (2D) / 1.0 GB (3D) of workspace
+static constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
+
+static int ensure_tasks(wos_scene* s, int64_t tasks, int64_t points) {
+  const int tf = wos::task_floats(s->host.dim);
+  if (tasks > s->task_cap) {
+    hipFree(s->d_tasks);
+    s->d_tasks = nullptr; s->task_cap = 0;
+    HIP_TRY(hipMalloc((void**)&s->d_tasks, (size_t)tasks * tf * sizeof(float)));
+    s->task_cap = tasks;
+  }
+  if (points > s->pstate_cap) {
+    hipFree(s->d_pstate);
+    s->d_pstate = nullptr; s->pstate_cap = 0;
+    HIP_TRY(hipMalloc((void**)&s->d_pstate, (size_t)points * sizeof(int32_t)));
+    s->pstate_cap = points;
+  }
+  return WOS_OK;
+}
+
+// SoA views into the task workspace for a batch of T tasks
+static wos::DevTasks task_view(wos_scene* s, int dim, int64_t T, int32_t wpp) {
+  wos::DevTasks tk{};
+  float* f = s->d_tasks;
+  tk.pt = f; f += dim * T;
+  tk.thr = f; f += T;
+  tk.tsrc = f; f += T;
+  tk.dd = f; f += T;
+  tk.first = f; f += T;
+  tk.bdir = f; f += dim * T;
+  tk.sdir = f; f += dim * T;
+  tk.total = f; f += T;
+  tk.code = (uint32_t*)f;
+  tk.pstate = s->d_pstate;
+  tk.T = T;
+  tk.wpp = wpp;
+  return tk;
 }
 
 // state_k = A_k * state_0 + C_k for the PCG32 LCG (multiplier kPcgMult, increment kPcgInc)
@@ -292,17 +337,18 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     dp.n_jump = s->n_jump;
   }
 
-  // LDS: staged geometry + per-wave (stratified samples + one chunk of walk records)
+  // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
+  // in the first-ball kernel)
   const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
   const int SS = dim == 2 ? wos::kSilStride2 : wos::kSilStride3;
   const int primAl = (s->host.n_prims * PS + 3) & ~3;
   const int geom_floats = (primAl + s->host.n_sil * SS + 3) & ~3;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
-  const size_t shmem =
-      (size_t)(geom_floats + wos::kWavesPerBlockHost * (2 * lhs_floats + wos::rec_floats(dim))) * sizeof(float);
-  if (shmem > 160 * 1024)
-    return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernel (" +
-                                    std::to_string(shmem) + " bytes)");
+  const size_t shmem_fb = (size_t)(geom_floats + wos::kWavesPerBlockHost * 2 * lhs_floats) * sizeof(float);
+  const size_t shmem_walk = (size_t)geom_floats * sizeof(float);
+  if (shmem_fb > 160 * 1024 - 256)
+    return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +
+                                    std::to_string(shmem_fb) + " bytes)");
 
   const float* d_pts = pts;
   float* d_p = p;
@@ -318,21 +364,38 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     d_nest = n_est ? s->d_nest : nullptr;
     d_steps = steps ? s->d_steps : nullptr;
   }
-  HIP_TRY(hipMemsetAsync(s->d_counters, 0, (wos::kNumCounters + 1) * sizeof(unsigned long long), st));
-  int grid = 0;
+  HIP_TRY(hipMemsetAsync(s->d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
+
+  // points are solved in batches whose walk tasks fit the task workspace
+  const int64_t wpp = (int64_t)dp.n_pairs * dp.n_anti;
+  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
+  int grid_fb = 0, grid_walk = 0;
   if (n > 0) {
+    int rc = ensure_tasks(s, batch * wpp, batch);
+    if (rc != WOS_OK) return rc;
     int bpc = 0;
-    HIP_TRY(wos::occupancy_blocks_per_cu(dim, shmem, &bpc));
-    if (bpc < 1) bpc = 1;
-    int64_t need = (n + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost;
-    int64_t full = (int64_t)bpc * std::max(1, s->num_cus);
-    grid = (int)std::min<int64_t>(need, full);
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb, &bpc));
+    grid_fb = (int)std::min<int64_t>((batch + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
+                                     (int64_t)std::max(1, bpc) * std::max(1, s->num_cus));
+    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc));
+    grid_walk = std::max(1, bpc) * std::max(1, s->num_cus);
   }
+  unsigned int* q_points = (unsigned int*)(s->d_counters + wos::kNumCounters);
+  unsigned int* q_tasks = (unsigned int*)(s->d_counters + wos::kNumCounters + 1);
   HIP_TRY(hipEventRecord(s->ev0, st));
-  if (grid > 0) {
-    HIP_TRY(wos::launch_solve(dim, s->dev, dp, d_pts, n, index_base, index_stride, d_p, d_g, d_nest, d_steps,
-                              s->d_counters, (unsigned int*)(s->d_counters + wos::kNumCounters), grid, shmem,
-                              geom_floats, lhs_floats, st));
+  for (int64_t b0 = 0; b0 < n; b0 += batch) {
+    const int64_t nb = std::min(batch, n - b0);
+    wos::DevTasks tk = task_view(s, dim, nb * wpp, (int32_t)wpp);
+    const int64_t bbase = index_base + b0 * index_stride;
+    if (b0 > 0)
+      HIP_TRY(hipMemsetAsync(s->d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, s->d_counters,
+                                    q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, st));
+    const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
+    HIP_TRY(wos::launch_walks(dim, s->dev, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,
+                              shmem_walk, geom_floats, st));
+    HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
+                             d_steps ? d_steps + b0 : nullptr, st));
   }
   HIP_TRY(hipEventRecord(s->ev1, st));
   if (!dev_ptrs && n > 0) {

@@ -40,8 +40,6 @@ namespace wos {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
-constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kChunkPairs = kWave;        // pairs per statistics chunk
 
 enum { WC_DIRICHLET = 0, WC_RR = 1, WC_MAXLEN = 2, WC_ESCAPED = 3 };
 
@@ -830,12 +828,16 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
   }
 }
 
+// One iteration of the walk loop (walk_on_stars.h:135-329): returns -1 while the
+// walk continues, else its termination code.  The loop test (Dirichlet distance
+// above the epsilon shell) is evaluated at the top of every step.
 template <int DIM>
-__device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, const float* prims,
-                                    const float* sil, float dirichletDist, Pcg32& smp, Gfn<DIM>& g,
-                                    WalkState<DIM>& st, uint32_t* steps, uint32_t* iters) {
+__device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& prm, const float* prims,
+                                         const float* sil, float& dirichletDist, Pcg32& smp, Gfn<DIM>& g,
+                                         WalkState<DIM>& st, uint32_t* steps, uint32_t* iters) {
   const int np = sc.n_prims, ns = sc.n_sil;
-  while (dirichletDist > prm.epsilon_shell) {
+  {
+    if (!(dirichletDist > prm.epsilon_shell)) return WC_DIRICHLET;
     float starRadius;
     bool flip = false;
     if (sc.double_sided && st.onNeumann) {
@@ -905,36 +907,27 @@ __device__ __forceinline__ int walk(const DevScene& sc, const DevParams& prm, co
     if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
     dirichletDist = dirichlet_dist_lane<DIM>(sc, st.pt);
   }
-  return WC_DIRICHLET;
+  return -1;
 }
 
 // ---------------------------------------------------------------------------
-// the solve kernel
+// the solve: three kernels over one batch of points
 // ---------------------------------------------------------------------------
-// One wave owns one query point at a time and runs it in three phases per chunk
-// of up to kChunkPairs antithetic pairs:
-//   1. first balls   -- lane = pair: source sample + boundary direction of the
-//                       first (maximal) ball for both members (walk_on_stars.h:
-//                       510-575); the members' start states go to LDS as tasks;
-//   2. walks         -- lanes pull walk tasks (pair, member) from a per-wave LDS
-//                       counter, so a lane that finishes a short walk takes the
-//                       next one instead of idling behind the longest pair;
-//   3. statistics    -- lanes 0..DIM fold the records in walk order, in lockstep
-//                       (one instruction stream: lane 0 the solution chain,
-//                       lane k the gradient component k-1).
-// The per-point stratified samples are drawn by all lanes at once from a PCG32
-// jump-ahead table; only the Fisher-Yates swaps stay serial (lane 0).
-//
-// Per-wave LDS (floats): strat[lhs] | partner[lhs] (int) | chunk SoA, kT = 2*kChunkPairs:
-//   records : total | first | bdir[DIM] | sdir[DIM] | code
-//   tasks   : pt[DIM] | throughput | totalSource | dirichletDist
-template <int DIM>
-struct ChunkLayout {
-  static constexpr int kT = 2 * kChunkPairs;
-  static constexpr int total = 0, first = kT, bdir = 2 * kT, sdir = (2 + DIM) * kT, code = (2 + 2 * DIM) * kT,
-                       pt = (3 + 2 * DIM) * kT, thr = (3 + 3 * DIM) * kT, tsrc = (4 + 3 * DIM) * kT,
-                       dd = (5 + 3 * DIM) * kT, size = (6 + 3 * DIM) * kT;
-};
+//   1. wos_first_ball_kernel  -- one wave per query point (atomic point queue):
+//      closest-point setup + inside test, the per-point stratified samples (all
+//      lanes at once from a PCG32 jump-ahead table; only the Fisher-Yates swaps
+//      are serial), then lane = antithetic pair: source sample + boundary
+//      direction of the first ball for both members (walk_on_stars.h:494-575).
+//      Each member becomes a walk task in HBM (start state + its record fields).
+//   2. wos_walk_kernel        -- persistent: every lane runs one walk task at a
+//      time, one step per loop iteration; a lane whose walk ends takes the next
+//      task from its wave's window of the global task queue at the next
+//      iteration, so lanes never idle behind the longest walk of a point.
+//   3. wos_fold_kernel        -- one lane per point: the statistics in walk order
+//      (Welford means with sequential control variates, walk_on_stars.h:500-506,
+//      583-614, 744-877) and the masked outputs (grid.h:155-179, 207-237).
+// The three stages touch HBM only for the task records (~48 B per walk in 2D),
+// which is negligible next to the walk arithmetic.
 
 // stratifiedSample (sampling.h:435-457) on the per-point stream, drawn in parallel:
 // draw k of the stream is pcg_output(A_k * s0 + C_k).  Diagonal draws k < n*sd;
@@ -991,19 +984,20 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   wave_sync();
 }
 
-// Phase 1: the first ball of pair w, both antithetic members (walk_on_stars.h:510-575).
+// The first ball of pair w, both antithetic members (walk_on_stars.h:510-575);
+// member a becomes task t0 + a.
 template <int DIM>
-__device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const float* x, float firstR,
-                                            const float* strat, float* ch, int64_t gidx, int w, int rbase,
-                                            bool yuk0, uint32_t* iters) {
-  using L = ChunkLayout<DIM>;
+__device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
+                                            const float* x, float firstR, const float* strat, int64_t gidx,
+                                            int w, int64_t t0, bool yuk0, uint32_t* iters) {
   constexpr int sd = DIM - 1;
+  const int64_t T = tk.T;
   float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
   for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
   Pcg32 fs;
   fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
   for (int a = 0; a < prm.n_anti; a++) {
-    const int r = rbase + a;
+    const int64_t t = t0 + a;
     Gfn<DIM> g;
     g.init(yuk0, sc.absorption);
     g.update_ball(x, firstR);
@@ -1057,8 +1051,8 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
         if constexpr (DIM == 2) {
           const float n0 = 1.0f, n1 = 0.0f;
           float s0 = n1, s1 = -n0;
-          float t0 = bd[0] * s0 + bd[1] * n0, t1 = bd[0] * s1 + bd[1] * n1;
-          bd[0] = t0; bd[1] = t1;
+          float q0 = bd[0] * s0 + bd[1] * n0, q1 = bd[0] * s1 + bd[1] * n1;
+          bd[0] = q0; bd[1] = q1;
         } else {
           const float n[3] = {1.0f, 0.0f, 0.0f};
           float sign = __builtin_copysignf(1.0f, n[2]);
@@ -1066,9 +1060,9 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
           const float b = n[0] * n[1] * aa;
           float b1[3] = {1.0f + sign * n[0] * n[0] * aa, sign * b, -sign * n[0]};
           float b2[3] = {b, sign + n[1] * n[1] * aa, -n[1]};
-          float t[3];
-          for (int k = 0; k < 3; k++) t[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
-          for (int k = 0; k < 3; k++) bd[k] = t[k];
+          float q[3];
+          for (int k = 0; k < 3; k++) q[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
+          for (int k = 0; k < 3; k++) bd[k] = q[k];
         }
       } else {
         sample_unit_sphere<DIM>(u, bd);
@@ -1087,81 +1081,52 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       float den = boundaryPdf * throughput;
       for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
     }
-    ch[L::first + r] = firstSource;
+    tk.first[t] = firstSource;
     for (int k = 0; k < DIM; k++) {
-      ch[L::bdir + k * L::kT + r] = bdir[k];
-      ch[L::sdir + k * L::kT + r] = sdir[k];
-      ch[L::pt + k * L::kT + r] = g.ySurf[k];
+      tk.bdir[k * T + t] = bdir[k];
+      tk.sdir[k * T + t] = sdir[k];
+      tk.pt[k * T + t] = g.ySurf[k];
     }
-    ch[L::thr + r] = throughput;
-    ch[L::tsrc + r] = totalSource;
-    ch[L::dd + r] = dirichlet_dist_lane<DIM>(sc, g.ySurf);
+    tk.thr[t] = throughput;
+    tk.tsrc[t] = totalSource;
+    tk.dd[t] = dirichlet_dist_lane<DIM>(sc, g.ySurf);
   }
 }
 
-// Phase 2: one walk task (record r of the chunk; pair w's walk stream).
 template <int DIM>
-__device__ __forceinline__ uint32_t walk_task(const DevScene& sc, const DevParams& prm, const float* Lprim,
-                                              const float* Lsil, float* ch, int64_t gidx, int w, int r, bool yuk0,
-                                              uint32_t* iters, unsigned int* s_ctr) {
-  using L = ChunkLayout<DIM>;
-  WalkState<DIM> st;
-  for (int k = 0; k < DIM; k++) { st.pt[k] = ch[L::pt + k * L::kT + r]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
-  // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
-  // and they are rewritten by every step before that can happen
-  st.prevDist = 0.0f;
-  st.throughput = ch[L::thr + r];
-  st.onNeumann = false;
-  st.walkLength = 0;
-  st.totalNeumann = 0.0f;
-  st.totalSource = ch[L::tsrc + r];
-  const float dd = ch[L::dd + r];
-  Gfn<DIM> g;
-  g.init(yuk0, sc.absorption);
-  Pcg32 ws;
-  ws.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 2));
-  uint32_t wsteps = 1;  // the first ball
-  const int code = walk<DIM>(sc, prm, Lprim, Lsil, dd, ws, g, st, &wsteps, iters);
-  const bool recorded = code == WC_DIRICHLET || code == WC_RR;
-  if (recorded) {
-    const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
-    ch[L::total + r] = st.throughput * term + st.totalNeumann + st.totalSource;
-  }
-  ch[L::code + r] = recorded ? 1.0f : 0.0f;
-  atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
-  atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);
-  return wsteps;
-}
-
-template <int DIM>
-__global__ __launch_bounds__(kBlock) void wos_solve_kernel(
-    const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base,
-    int64_t stride, float* __restrict__ p_out, float* __restrict__ g_out, int32_t* __restrict__ nest_out,
-    int32_t* __restrict__ steps_out, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work,
-    int geom_floats, int lhs_floats) {
-  using L = ChunkLayout<DIM>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ unsigned int s_ctr[C_NUM];
-  __shared__ unsigned int s_task[kWavesPerBlock];
+__device__ __forceinline__ void stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
   constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-
-  // stage Neumann primitives + silhouette candidates (every workgroup once)
-  const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
+  const int primN = sc.n_prims * PS, silN = with_sil ? sc.n_sil * SS : 0;
   const int primAl = (primN + 3) & ~3;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
   for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
-  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
+}
+
+__device__ __forceinline__ void flush_counter(unsigned long long* counters, int slot, uint32_t v, int lane) {
+  unsigned long long s = v;
+  for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0 && s) atomicAdd(&counters[slot], s);
+}
+
+// per-point state bits written by the first-ball kernel
+enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
+
+// ---- kernel 1: point setup + first balls ----------------------------------
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
+    const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
+    const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
+    int lhs_floats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  stage_geometry<DIM>(sc, smem, false);
   __syncthreads();
   const float* Lprim = smem;
-  const float* Lsil = smem + primAl;
-  float* wbase = smem + geom_floats + wave * (2 * lhs_floats + L::size);
-  float* strat = wbase;
-  int* partner = (int*)(wbase + lhs_floats);
-  float* ch = wbase + 2 * lhs_floats;
+  float* strat = smem + geom_floats + wave * 2 * lhs_floats;
+  int* partner = (int*)(strat + lhs_floats);
 
-  uint32_t c_iters = 0;
+  uint32_t c_iters = 0, c_pts = 0;
   const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
 
@@ -1190,104 +1155,197 @@ __global__ __launch_bounds__(kBlock) void wos_solve_kernel(
     } else {
       dDist = dSigned = bbox_far_dist<DIM>(sc, x);
     }
-    bool inside = !sc.watertight ? true
-                  : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
+    const bool inside = !sc.watertight ? true
+                        : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
     const bool estimate = inside || sc.double_sided;
-
-    // statistics registers: lane 0 = solution chain, lanes 1..DIM = gradient
-    // components; sN / sFirst are identical in every lane
-    float sMean = 0.0f, sFirst = 0.0f;
-    int sN = 0;
-    uint32_t pt_steps = 0;
-
-    if (estimate) {
-      if (lane == 0) atomicAdd(&s_ctr[C_PTS], 1u);
-      build_lhs<DIM>(prm, gidx, strat, partner, lane);
-      const float firstR = 0.99f * smin(dDist, nDist);
-      const int kk = (lane >= 1 && lane <= DIM) ? lane - 1 : 0;
-
-      for (int c0 = 0; c0 < npairs; c0 += kChunkPairs) {
-        const int cnt = (npairs - c0) < kChunkPairs ? (npairs - c0) : kChunkPairs;
-        // ---- phase 1: first balls, lane = pair
-        if (lane < cnt) first_balls<DIM>(sc, prm, x, firstR, strat, ch, gidx, c0 + lane, lane * prm.n_anti, yuk0,
-                                         &c_iters);
-        if (lane == 0) s_task[wave] = kWave;
-        wave_sync();
-        // ---- phase 2: walk tasks pulled from the wave's LDS counter
-        const int ntask = cnt * prm.n_anti;
-        for (int t = lane; t < ntask;) {
-          const int pr = prm.n_anti == 2 ? (t >> 1) : t;
-          pt_steps += walk_task<DIM>(sc, prm, Lprim, Lsil, ch, gidx, c0 + pr, t, yuk0, &c_iters, s_ctr);
-          t = (int)atomicAdd(&s_task[wave], 1u);
-        }
-        wave_sync();
-        // ---- phase 3: statistics in walk order (walk_on_stars.h:500-506,583-614)
-        const int nfold = WOS_ABL_NO_STATS ? 0 : cnt;
-        for (int j = 0; j < nfold; ++j) {
-          float cvb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sMean), 0));
-          float cvs = sFirst / (float)(sN > 1 ? sN : 1);
-          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
-          for (int a = 0; a < prm.n_anti; a++) {
-            const int r = j * prm.n_anti + a;
-            if (ch[L::code + r] == 0.0f) continue;
-            const float total = ch[L::total + r];
-            const float first = ch[L::first + r];
-            const float be = (total - first - cvb) * ch[L::bdir + kk * L::kT + r];
-            const float se = (first - cvs) * ch[L::sdir + kk * L::kT + r];
-            const float xv = lane == 0 ? total : be + se;
-            sN += 1;
-            const float delta = xv - sMean;
-            sMean += delta / (float)sN;
-            sFirst += first;
-          }
-        }
-        wave_sync();
-      }
-    }
-
-    // ---- masked outputs (grid.h:155-179, 207-237)
-    const float mask = prm.boundary_distance_mask;
-    const bool maskP = __builtin_fabsf(nDist) < mask;
-    const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
-    float val = estimate ? sMean : 0.0f;
     if (lane == 0) {
-      p_out[idx] = maskP ? 0.0f : val;
-      if (nest_out) nest_out[idx] = sN;
-    } else if (lane <= DIM) {
-      g_out[(int64_t)idx * DIM + (lane - 1)] = maskG ? 0.0f : val;
+      // masked outputs (grid.h:155-179, 207-237)
+      const float mask = prm.boundary_distance_mask;
+      const bool maskP = __builtin_fabsf(nDist) < mask;
+      const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
+      tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0);
     }
-    if (steps_out) {
-      uint32_t s = pt_steps;
-      for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
-      if (lane == 0) steps_out[idx] = (int32_t)s;
+    if (!estimate) continue;
+    c_pts += lane == 0;
+    build_lhs<DIM>(prm, gidx, strat, partner, lane);
+    const float firstR = 0.99f * smin(dDist, nDist);
+    for (int w = lane; w < npairs; w += kWave)
+      first_balls<DIM>(sc, prm, tk, x, firstR, strat, gidx, w, (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti,
+                       yuk0, &c_iters);
+    wave_sync();
+  }
+  flush_counter(counters, C_ITERS, c_iters, lane);
+  flush_counter(counters, C_PTS, c_pts, lane);
+}
+
+// ---- kernel 2: walks ---------------------------------------------------------
+constexpr unsigned int kTaskGrab = 256;  // tasks a wave takes from the global queue at once
+
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void wos_walk_kernel(
+    const DevScene sc, const DevParams prm, const DevTasks tk, int64_t base, int64_t stride,
+    unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ unsigned int s_ctr[C_NUM];
+  constexpr int PS = Layout<DIM>::prim;
+  const int lane = threadIdx.x & (kWave - 1);
+  stage_geometry<DIM>(sc, smem, true);
+  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
+  __syncthreads();
+  const float* Lprim = smem;
+  const float* Lsil = smem + ((sc.n_prims * PS + 3) & ~3);
+  (void)geom_floats;
+
+  const uint32_t T = (uint32_t)tk.T;
+  const uint32_t wpp = (uint32_t)tk.wpp;
+  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
+  uint32_t c_iters = 0;
+
+  uint32_t qn = 0, qe = 0;  // the wave's window [qn, qe) of the task queue (wave-uniform)
+  bool exhausted = false;
+  int64_t t = -1;           // this lane's task
+  WalkState<DIM> st;
+  Gfn<DIM> g;
+  Pcg32 ws;
+  float ddist = 0.0f;
+  uint32_t wsteps = 0;
+
+  for (;;) {
+    // ---- hand out tasks to idle lanes (uniform control flow)
+    bool fresh = false;
+    for (;;) {
+      const uint64_t need = __ballot(t < 0);
+      if (need == 0 || exhausted) break;
+      if (qn >= qe) {
+        unsigned int c = 0;
+        if (lane == 0) c = atomicAdd(tqueue, kTaskGrab);
+        c = __shfl(c, 0);
+        if (c >= T) { exhausted = true; break; }
+        qn = c;
+        qe = (T - c) < kTaskGrab ? T : c + kTaskGrab;
+      }
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      const uint32_t k = (uint32_t)__popcll(need);
+      const uint32_t avail = qe - qn;
+      if (t < 0 && rank < avail) { t = qn + rank; fresh = true; }
+      qn += k < avail ? k : avail;
     }
-    // keep the 32-bit LDS counters far from wrapping on huge launches
-    if (lane == 0 && s_ctr[C_STEPS] + s_ctr[C_WASTED] > (1u << 30)) {
-      atomicAdd(&counters[C_STEPS], (unsigned long long)atomicExch(&s_ctr[C_STEPS], 0u));
-      atomicAdd(&counters[C_WASTED], (unsigned long long)atomicExch(&s_ctr[C_WASTED], 0u));
+    if (__ballot(t >= 0) == 0) break;  // queue drained and every lane idle
+    if (t < 0) continue;
+
+    if (fresh) {
+      const uint32_t pidx = (uint32_t)t / wpp;
+      const uint32_t w = ((uint32_t)t - pidx * wpp) / (uint32_t)prm.n_anti;
+      if (!(tk.pstate[pidx] & kPtEstimate)) {  // point outside the domain: no walks
+        tk.code[t] = 0u;
+        t = -1;
+        continue;
+      }
+      for (int k = 0; k < DIM; k++) { st.pt[k] = tk.pt[k * tk.T + t]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
+      // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
+      // and every step rewrites them before that can happen
+      st.prevDist = 0.0f;
+      st.throughput = tk.thr[t];
+      st.onNeumann = false;
+      st.walkLength = 0;
+      st.totalNeumann = 0.0f;
+      st.totalSource = tk.tsrc[t];
+      ddist = tk.dd[t];
+      g.init(yuk0, sc.absorption);
+      ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
+      wsteps = 1;  // the first ball
+    }
+
+    const int code = walk_step<DIM>(sc, prm, Lprim, Lsil, ddist, ws, g, st, &wsteps, &c_iters);
+    if (code >= 0) {
+      const bool recorded = code == WC_DIRICHLET || code == WC_RR;
+      if (recorded) {
+        const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
+        tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
+      }
+      tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
+      atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
+      atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL],
+                1u);
+      t = -1;
     }
   }
 
-  // ---- counters: rejection iterations per lane (wave reduction), the rest from LDS
-  {
-    unsigned long long v = c_iters;
-    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0 && v) atomicAdd(&counters[C_ITERS], v);
-  }
+  flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();
-  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS) {
-    unsigned int v = s_ctr[threadIdx.x];
-    if (threadIdx.x == C_REC) v = s_ctr[C_RR] + s_ctr[C_DIR];
+  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
+    unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
     if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
   }
 }
 
-template __global__ void wos_solve_kernel<2>(const DevScene, const DevParams, const float*, int64_t, int64_t,
-                                             int64_t, float*, float*, int32_t*, int32_t*, unsigned long long*,
-                                             unsigned int*, int, int);
-template __global__ void wos_solve_kernel<3>(const DevScene, const DevParams, const float*, int64_t, int64_t,
-                                             int64_t, float*, float*, int32_t*, int32_t*, unsigned long long*,
-                                             unsigned int*, int, int);
+// ---- kernel 3: statistics + outputs ----------------------------------------
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
+                                                          float* __restrict__ p_out, float* __restrict__ g_out,
+                                                          int32_t* __restrict__ nest_out,
+                                                          int32_t* __restrict__ steps_out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t T = tk.T;
+  const int ps = tk.pstate[i];
+  const bool estimate = ps & kPtEstimate;
+  float mean[DIM + 1];
+  for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
+  float sFirst = 0.0f;
+  int sN = 0;
+  uint32_t steps = 0;
+  if (estimate) {
+    const int64_t t0 = i * tk.wpp;
+    for (int j = 0; j < prm.n_pairs; ++j) {
+      float cvb = mean[0];
+      float cvs = sFirst / (float)(sN > 1 ? sN : 1);
+      if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
+      for (int a = 0; a < prm.n_anti; a++) {
+        const int64_t t = t0 + j * prm.n_anti + a;
+        const uint32_t code = tk.code[t];
+        steps += code >> 1;
+        if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
+        const float total = tk.total[t];
+        const float first = tk.first[t];
+        sN += 1;
+        const float fN = (float)sN;
+        {
+          const float delta = total - mean[0];
+          mean[0] += delta / fN;
+        }
+        for (int k = 0; k < DIM; k++) {
+          const float be = (total - first - cvb) * tk.bdir[k * T + t];
+          const float se = (first - cvs) * tk.sdir[k * T + t];
+          const float delta = (be + se) - mean[k + 1];
+          mean[k + 1] += delta / fN;
+        }
+        sFirst += first;
+      }
+    }
+  }
+  const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
+  p_out[i] = maskP ? 0.0f : mean[0];
+  for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];
+  if (nest_out) nest_out[i] = sN;
+  if (steps_out) steps_out[i] = (int32_t)steps;
+}
+
+template __global__ void wos_first_ball_kernel<2>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                                  int64_t, const DevTasks, unsigned long long*, unsigned int*, int,
+                                                  int);
+template __global__ void wos_first_ball_kernel<3>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                                  int64_t, const DevTasks, unsigned long long*, unsigned int*, int,
+                                                  int);
+template __global__ void wos_walk_kernel<2>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                            unsigned long long*, unsigned int*, int);
+template __global__ void wos_walk_kernel<3>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                            unsigned long long*, unsigned int*, int);
+template __global__ void wos_fold_kernel<2>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
+                                            int32_t*);
+template __global__ void wos_fold_kernel<3>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
+                                            int32_t*);
 
 // math self-test kernel (parity of the deterministic math with the CPU oracle)
 __global__ void wos_math_selftest_kernel(int which, const double* x, double* out, int64_t n) {
@@ -1322,25 +1380,48 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
 // ---------------------------------------------------------------------------
 // host-side launchers (called from wos_capi.hip)
 // ---------------------------------------------------------------------------
-int rec_floats(int dim) { return dim == 2 ? ChunkLayout<2>::size : ChunkLayout<3>::size; }
-
-hipError_t launch_solve(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
-                        int64_t base, int64_t stride, float* p, float* g, int32_t* nest, int32_t* steps,
-                        unsigned long long* counters, unsigned int* work, int grid, size_t shmem,
-                        int geom_floats, int lhs_floats, hipStream_t s) {
+hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                              int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
+                              unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
+                              hipStream_t s) {
   if (dim == 2)
-    hipLaunchKernelGGL(wos_solve_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, p,
-                       g, nest, steps, counters, work, geom_floats, lhs_floats);
+    hipLaunchKernelGGL(wos_first_ball_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride,
+                       tk, counters, work, geom_floats, lhs_floats);
   else
-    hipLaunchKernelGGL(wos_solve_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, p,
-                       g, nest, steps, counters, work, geom_floats, lhs_floats);
+    hipLaunchKernelGGL(wos_first_ball_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride,
+                       tk, counters, work, geom_floats, lhs_floats);
   return hipGetLastError();
 }
 
-hipError_t occupancy_blocks_per_cu(int dim, size_t shmem, int* blocks) {
+hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
+                        int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
+                        int geom_floats, hipStream_t s) {
   if (dim == 2)
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_solve_kernel<2>, kBlock, shmem);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_solve_kernel<3>, kBlock, shmem);
+    hipLaunchKernelGGL(wos_walk_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters,
+                       tqueue, geom_floats);
+  else
+    hipLaunchKernelGGL(wos_walk_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters,
+                       tqueue, geom_floats);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
+                       int32_t* nest, int32_t* steps, hipStream_t s) {
+  const int grid = (int)((n + kBlock - 1) / kBlock);
+  if (grid < 1) return hipSuccess;
+  if (dim == 2)
+    hipLaunchKernelGGL(wos_fold_kernel<2>, dim3(grid), dim3(kBlock), 0, s, prm, tk, n, p, g, nest, steps);
+  else
+    hipLaunchKernelGGL(wos_fold_kernel<3>, dim3(grid), dim3(kBlock), 0, s, prm, tk, n, p, g, nest, steps);
+  return hipGetLastError();
+}
+
+hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks) {
+  if (which == 0)
+    return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2>, kBlock, shmem)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3>, kBlock, shmem);
+  return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2>, kBlock, shmem)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3>, kBlock, shmem);
 }
 
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s) {

@@ -7,11 +7,19 @@ namespace wos {
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlockHost = 4;
 constexpr int kNumCounters = 9;
-int rec_floats(int dim);
-hipError_t launch_solve(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
-                        int64_t base, int64_t stride, float* p, float* g, int32_t* nest, int32_t* steps,
-                        unsigned long long* counters, unsigned int* work, int grid, size_t shmem,
-                        int geom_floats, int lhs_floats, hipStream_t s);
-hipError_t occupancy_blocks_per_cu(int dim, size_t shmem, int* blocks);
+// queue slots after the counters: [kNumCounters] point queue, [kNumCounters + 1] task queue
+constexpr int kNumCounterSlots = kNumCounters + 2;
+
+hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                              int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
+                              unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
+                              hipStream_t s);
+hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
+                        int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
+                        int geom_floats, hipStream_t s);
+hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
+                       int32_t* nest, int32_t* steps, hipStream_t s);
+// which: 0 first-ball kernel, 1 walk kernel
+hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks);
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
 }  // namespace wos

@@ -74,4 +74,24 @@ struct DevParams {
   int32_t n_jump;
 };
 
+// Walk-task workspace of one batch of points, SoA over T = n_points * wpp tasks
+// (task t = point * wpp + pair * n_anti + member).  Written by the first-ball
+// kernel, advanced by the walk kernel, folded by the statistics kernel.
+struct DevTasks {
+  float* pt;        // [DIM][T] walk start: the first ball's boundary sample
+  float* thr;       // [T] throughput after the first ball
+  float* tsrc;      // [T] source contribution of the first ball
+  float* dd;        // [T] Dirichlet distance at pt
+  float* first;     // [T] record: first-ball source value (control variate)
+  float* bdir;      // [DIM][T] record: boundary gradient direction
+  float* sdir;      // [DIM][T] record: source gradient direction
+  float* total;     // [T] record: walk total
+  uint32_t* code;   // [T] record: (steps << 1) | recorded
+  int32_t* pstate;  // [n] bit0 estimated, bit1 mask p, bit2 mask grad p
+  int64_t T;
+  int32_t wpp;      // walks per point = n_pairs * n_anti
+};
+
+constexpr int task_floats(int dim) { return 3 * dim + 6; }
+
 }  // namespace wos

@@ -49,6 +49,7 @@ struct wos_scene {
   wos::DevScene dev{};
   float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
   float* d_source = nullptr;
+  float *d_pgroup = nullptr, *d_sgroup = nullptr;
   // workspace
   std::mutex mu;
   float* d_pts = nullptr;
@@ -128,6 +129,7 @@ static void scene_release(wos_scene* s) {
   hipSetDevice(s->device);
   hipFree(s->d_prim); hipFree(s->d_paux); hipFree(s->d_sil); hipFree(s->d_dprim); hipFree(s->d_dpaux);
   hipFree(s->d_source);
+  hipFree(s->d_pgroup); hipFree(s->d_sgroup);
   hipFree(s->d_pts); hipFree(s->d_p); hipFree(s->d_g); hipFree(s->d_nest); hipFree(s->d_steps);
   hipFree(s->d_counters);
   hipFree(s->d_jump);
@@ -165,6 +167,8 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   if (e == hipSuccess) e = upload(&s->d_sil, s->host.sil);
   if (e == hipSuccess) e = upload(&s->d_dprim, s->host.dprim);
   if (e == hipSuccess) e = upload(&s->d_dpaux, s->host.dpaux);
+  if (e == hipSuccess) e = upload(&s->d_pgroup, s->host.pgroup);
+  if (e == hipSuccess) e = upload(&s->d_sgroup, s->host.sgroup);
   size_t nsrc = 0;
   if (d->source) {
     nsrc = (size_t)d->source_dims[0] * d->source_dims[1] * (d->dim == 3 ? d->source_dims[2] : 1);
@@ -190,6 +194,8 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   ds.n_dprims = s->host.n_dprims;
   ds.prim = s->d_prim; ds.paux = s->d_paux; ds.sil = s->d_sil; ds.dprim = s->d_dprim; ds.dpaux = s->d_dpaux;
   ds.source = s->d_source;
+  ds.pgroup = s->d_pgroup; ds.sgroup = s->d_sgroup;
+  ds.n_pgroups = s->host.n_pgroups; ds.n_sgroups = s->host.n_sgroups;
   for (int k = 0; k < 3; k++) {
     ds.sdims[k] = d->source ? (k < nsd ? d->source_dims[k] : 1) : 0;
     ds.pmin[k] = s->host.pmin[k]; ds.pmax[k] = s->host.pmax[k]; ds.ext[k] = s->host.ext[k];
@@ -342,7 +348,9 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
   const int SS = dim == 2 ? wos::kSilStride2 : wos::kSilStride3;
   const int primAl = (s->host.n_prims * PS + 3) & ~3;
-  const int geom_floats = (primAl + s->host.n_sil * SS + 3) & ~3;
+  const int silAl = (s->host.n_sil * SS + 3) & ~3;
+  const int geom_floats =
+      primAl + silAl + wos::kGroupStride * s->host.n_pgroups + wos::kSGroupStride * s->host.n_sgroups;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   const size_t shmem_fb = (size_t)(geom_floats + wos::kWavesPerBlockHost * 2 * lhs_floats) * sizeof(float);
   const size_t shmem_walk = (size_t)geom_floats * sizeof(float);
@@ -406,6 +414,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   }
   if ((flags & WOS_ASYNC) && dev_ptrs) return WOS_OK;
   HIP_TRY(hipStreamSynchronize(st));
+  wos::diag_dump(dim == 2 ? "2d" : "3d");
   if (stats) {
     unsigned long long c[wos::kNumCounters];
     HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));

@@ -236,6 +236,80 @@ bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
       }
   if (in.dim == 2) { out.pmin[2] = out.pmax[2] = 0.0f; }
   for (int k = 0; k < 3; k++) out.ext[k] = out.pmax[k] - out.pmin[k];
+  // culling boxes, padded far beyond float rounding of the kernel's box tests
+  float span = 0.0f;
+  for (int k = 0; k < in.dim; k++) span = smax(span, out.ext[k]);
+  const float pad = 1e-4f * span + 1e-6f;
+  auto add_box = [&](std::vector<float>& boxes, const std::vector<const float*>& pts) {
+    float lo[3] = {kFltMax, kFltMax, kFltMax}, hi[3] = {-kFltMax, -kFltMax, -kFltMax};
+    for (const float* q : pts)
+      for (int k = 0; k < in.dim; k++) { lo[k] = smin(lo[k], q[k]); hi[k] = smax(hi[k], q[k]); }
+    for (int k = in.dim; k < 3; k++) lo[k] = hi[k] = 0.0f;
+    const float rec[kGroupStride] = {lo[0] - pad, lo[1] - pad, lo[2] - pad, 0.0f,
+                                     hi[0] + pad, hi[1] + pad, hi[2] + pad, 0.0f};
+    boxes.insert(boxes.end(), rec, rec + kGroupStride);
+  };
+  for (int g0 = 0; g0 < out.n_prims; g0 += kGroup) {
+    std::vector<const float*> pts;
+    for (int p = g0; p < std::min(out.n_prims, g0 + kGroup); p++)
+      for (int c = 0; c < in.dim; c++) pts.push_back(neu.v[neu.ix[p][c]].x);
+    add_box(out.pgroup, pts);
+    out.n_pgroups++;
+  }
+  const int SS = in.dim == 2 ? kSilStride2 : kSilStride3;
+  for (int g0 = 0; g0 < out.n_sil; g0 += kGroup) {
+    const int g1 = std::min(out.n_sil, g0 + kGroup);
+    std::vector<const float*> pts;
+    for (int q = g0; q < g1; q++) {
+      pts.push_back(&out.sil[(size_t)q * SS]);
+      if (in.dim == 3) pts.push_back(&out.sil[(size_t)q * SS + 3]);
+    }
+    std::vector<float> box;
+    add_box(box, pts);
+    // bounding sphere of the candidates (centre of the box; radius padded)
+    double c[3], rho = 0.0;
+    for (int k = 0; k < 3; k++) c[k] = 0.5 * ((double)box[k] + (double)box[4 + k]);
+    for (const float* q : pts) {
+      double r2 = 0.0;
+      for (int k = 0; k < in.dim; k++) r2 += ((double)q[k] - c[k]) * ((double)q[k] - c[k]);
+      rho = std::max(rho, std::sqrt(r2));
+    }
+    rho += pad;
+    // cone of the adjacent normals n0, n1 of every candidate
+    const int o0 = in.dim == 2 ? 2 : 6, o1 = in.dim == 2 ? 4 : 9, om = in.dim == 2 ? 6 : 12;
+    double ax[3] = {0, 0, 0};
+    bool nocull = false;
+    for (int q = g0; q < g1; q++) {
+      const float* S = &out.sil[(size_t)q * SS];
+      if (S[om] != 0.0f) nocull = true;  // candidates next to a missing primitive are always silhouettes
+      for (int k = 0; k < in.dim; k++) ax[k] += (double)S[o0 + k] + (double)S[o1 + k];
+    }
+    double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    double alpha = 0.0;
+    if (an < 1e-6) {
+      nocull = true;
+    } else {
+      for (int k = 0; k < 3; k++) ax[k] /= an;
+      for (int q = g0; q < g1; q++) {
+        const float* S = &out.sil[(size_t)q * SS];
+        for (int o : {o0, o1}) {
+          double nn = 0.0, dt = 0.0;
+          for (int k = 0; k < in.dim; k++) { nn += (double)S[o + k] * S[o + k]; dt += ax[k] * S[o + k]; }
+          nn = std::sqrt(nn);
+          double cosang = nn > 0.0 ? std::max(-1.0, std::min(1.0, dt / nn)) : -1.0;
+          alpha = std::max(alpha, std::acos(cosang));
+        }
+      }
+      alpha += 1e-3;
+      if (alpha >= 1.5) nocull = true;  // a cone this wide never certifies a face direction
+    }
+    float rec[kSGroupStride] = {box[0], box[1], box[2], (float)std::sin(alpha),
+                                box[4], box[5], box[6], (float)std::cos(alpha),
+                                (float)c[0], (float)c[1], (float)c[2], (float)rho,
+                                (float)ax[0], (float)ax[1], (float)ax[2], nocull ? 1.0f : 0.0f};
+    out.sgroup.insert(out.sgroup.end(), rec, rec + kSGroupStride);
+    out.n_sgroups++;
+  }
   return true;
 }
 

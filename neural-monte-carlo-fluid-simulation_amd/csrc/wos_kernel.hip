@@ -17,6 +17,8 @@
 // 2*pi divisors, Eigen's float-scalar conversions -- see the oracle restatement
 // (oracle/wos_oracle.c) which is the parity checker for this file.
 
+#include <cstdio>
+
 #include "wos_detmath.h"
 #include "wos_scene.h"
 
@@ -38,6 +40,10 @@ namespace wos {
 #define WOS_ABL_NO_STATS 0
 #endif
 
+#ifndef WOS_DIAG
+#define WOS_DIAG 0
+#endif
+
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 
@@ -50,6 +56,36 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
+
+// Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
+// (s_memtime) and lane-packing counters of the walk kernel.
+enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
+       D_NUM };
+__device__ unsigned long long g_diag[D_NUM];
+#if WOS_DIAG
+__shared__ unsigned long long s_diag[D_NUM];
+#endif
+#if WOS_DIAG
+#define DIAG_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(slot, v)                                                              \
+  do {                                                                                 \
+    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - (v);                           \
+    if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
+      atomicAdd(&s_diag[slot], (unsigned long long)dt_);                               \
+  } while (0)
+#define DIAG_COUNT(slot, n)                                                            \
+  do {                                                                                 \
+    const unsigned long long n_ = (n);                                                 \
+    if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
+      atomicAdd(&s_diag[slot], n_);                                                    \
+  } while (0)
+#define DIAG_LANE(slot) atomicAdd(&s_diag[slot], 1ull)
+#else
+#define DIAG_T0(v)
+#define DIAG_ADD(slot, v)
+#define DIAG_COUNT(slot, n)
+#define DIAG_LANE(slot)
+#endif
 
 template <int DIM>
 __device__ __forceinline__ float dotv(const float* a, const float* b) {
@@ -247,68 +283,140 @@ __device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
 
 struct Hit { float p[3], n[3], d; };
 
-// First ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92).
-// Every primitive first goes through a division-free certain-rejection test that
-// uses the hardware reciprocal (v_rcp_f32, |rel err| <= 2^-22): signs are exact,
-// magnitudes get a 1e-5 relative margin, so only primitives the exact test could
-// accept reach the IEEE division -- the accepted set and every computed value are
-// exactly those of the plain loop (and of the oracle).
+// Exact ray-primitive test of the reference (mbvh.inl:521-609 + wide_query_operations.h
+// 27-92, line_segments.inl / triangles.inl ray queries): accepts when the hit
+// distance d satisfies 0 <= d <= rt and then shrinks rt to d.  Visiting primitives
+// in index order this yields the minimum d, ties going to the larger index.
 template <int DIM>
-__device__ __forceinline__ bool ray_hit(const float* prims, int np, const float* o, const float* dir,
-                                        float tmax, Hit* h) {
+__device__ __forceinline__ bool ray_prim_exact(const float* P, const float* o, const float* dir, float& rt, Hit* h) {
+  if constexpr (DIM == 2) {
+    float u0 = P[0] - o[0], u1 = P[1] - o[1];
+    float v0 = P[2], v1 = P[3];  // record holds v = pb - pa
+    float dv = dir[0] * v1 - dir[1] * v0;
+    if (!(__builtin_fabsf(dv) > kFltEps)) return false;
+    float ud = u0 * dir[1] - u1 * dir[0];
+    float uv = u0 * v1 - u1 * v0;
+    float inv = 1.0f / dv;
+    float t = ud * inv;
+    if (!(t >= 0.0f && t <= 1.0f)) return false;
+    float d = uv * inv;
+    if (!(d >= 0.0f && d <= rt)) return false;
+    rt = d;
+    h->d = d;
+    h->p[0] = P[0] + t * v0; h->p[1] = P[1] + t * v1;
+    h->n[0] = v1; h->n[1] = -v0;
+    return true;
+  } else {
+    float v1[3], v2[3], pp[3], s[3], q[3];
+    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; s[k] = o[k] - P[k]; }
+    cross3(pp, dir, v2);
+    float det = dotv<3>(v1, pp);
+    if (!(__builtin_fabsf(det) > kFltEps)) return false;
+    float inv = 1.0f / det;
+    float v = dotv<3>(s, pp) * inv;
+    if (!(v >= 0.0f && v <= 1.0f)) return false;
+    cross3(q, s, v1);
+    float w = dotv<3>(dir, q) * inv;
+    if (!(w >= 0.0f && v + w <= 1.0f)) return false;
+    float d = dotv<3>(v2, q) * inv;
+    if (!(d >= 0.0f && d <= rt)) return false;
+    rt = d;
+    h->d = d;
+    for (int k = 0; k < 3; k++) h->p[k] = P[k] + v1[k] * v + v2[k] * w;
+    cross3(h->n, v1, v2);
+    return true;
+  }
+}
+
+template <int DIM>
+__device__ __forceinline__ bool ray_hit_scan(const float* prims, int np, const float* o, const float* dir,
+                                             float tmax, Hit* h) {
   constexpr int PS = Layout<DIM>::prim;
   bool found = false;
   float rt = tmax;
-  for (int p = 0; p < np; p++) {
-    const float* P = prims + p * PS;
-    if constexpr (DIM == 2) {
-      float u0 = P[0] - o[0], u1 = P[1] - o[1];
-      float v0 = P[2], v1 = P[3];
-      float dv = dir[0] * v1 - dir[1] * v0;
-      if (!(__builtin_fabsf(dv) > kFltEps)) continue;
-      float ud = u0 * dir[1] - u1 * dir[0];
-      float uv = u0 * v1 - u1 * v0;
-      float ra = __builtin_amdgcn_rcpf(dv);
-      float ta = ud * ra, da = uv * ra;
-      if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
-          (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
-        continue;
-      float inv = 1.0f / dv;
-      float t = ud * inv;
-      if (!(t >= 0.0f && t <= 1.0f)) continue;
-      float d = uv * inv;
-      if (!(d >= 0.0f && d <= rt)) continue;
-      rt = d; found = true;
-      h->d = d;
-      h->p[0] = P[0] + t * v0; h->p[1] = P[1] + t * v1;
-      h->n[0] = v1; h->n[1] = -v0;
-    } else {
-      float v1[3], v2[3], pp[3], s[3], q[3];
-      for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; s[k] = o[k] - P[k]; }
-      cross3(pp, dir, v2);
-      float det = dotv<3>(v1, pp);
-      if (!(__builtin_fabsf(det) > kFltEps)) continue;
-      float ra = __builtin_amdgcn_rcpf(det);
-      float vn = dotv<3>(s, pp);
-      float va = vn * ra;
-      if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) continue;
-      cross3(q, s, v1);
-      float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
-      float wa = wn * ra, da = dn * ra;
-      if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
-          (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
-        continue;
-      float inv = 1.0f / det;
-      float v = vn * inv;
-      if (!(v >= 0.0f && v <= 1.0f)) continue;
-      float w = wn * inv;
-      if (!(w >= 0.0f && v + w <= 1.0f)) continue;
-      float d = dn * inv;
-      if (!(d >= 0.0f && d <= rt)) continue;
-      rt = d; found = true;
-      h->d = d;
-      for (int k = 0; k < 3; k++) h->p[k] = P[k] + v1[k] * v + v2[k] * w;
-      cross3(h->n, v1, v2);
+  for (int p = 0; p < np; p++) found |= ray_prim_exact<DIM>(prims + p * PS, o, dir, rt, h);
+  if (found) normalize_rcp<DIM>(h->n);
+  return found;
+}
+
+// Geometry as staged in LDS: primitives, silhouette candidates and the culling
+// boxes of kGroup consecutive primitives / silhouettes.
+struct LGeom {
+  const float* prim;
+  const float* sil;
+  const float* pgroup;
+  const float* sgroup;
+};
+
+// Certain rejection of a whole group for a ray segment [o, o + rt*dir]: slab
+// test against the group's padded box.  The padding (1e-4 of the scene span)
+// dwarfs the rounding of the slab arithmetic, so a group whose primitives the
+// exact test could hit within rt is never skipped.  rcp(0) = inf and NaN slabs
+// (origin exactly on a padded face) fall out of min/max, which only errs
+// toward visiting.
+template <int DIM>
+__device__ __forceinline__ bool ray_box_maybe(const float* B, const float* o, const float* inv, float rt) {
+  float tn = -kFltMax, tf = kFltMax;
+  for (int k = 0; k < DIM; k++) {
+    const float t1 = (B[k] - o[k]) * inv[k], t2 = (B[4 + k] - o[k]) * inv[k];
+    tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
+    tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+  }
+  return tn <= tf && tf >= 0.0f && tn <= rt * 1.00001f + 1e-6f;
+}
+
+// First ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92)
+// in index order: min d, ties to the larger index.  Groups of primitives the
+// ray cannot reach are skipped (for the whole wave when no lane needs them);
+// inside a group every primitive first goes through a division-free
+// certain-rejection test using the hardware reciprocal (v_rcp_f32, |rel err| <=
+// 2^-22; signs exact, magnitudes with a 1e-5 relative margin), so only
+// primitives the exact test could accept reach the IEEE division.  Skipped
+// groups and pre-filtered primitives are exactly those the plain loop rejects,
+// so the result and every computed value equal the plain loop's (and the
+// oracle's).
+template <int DIM>
+__device__ __forceinline__ bool ray_hit(const LGeom& G, int np, int ng, const float* o, const float* dir,
+                                        float tmax, Hit* h) {
+  constexpr int PS = Layout<DIM>::prim;
+  float inv[DIM];
+  for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
+  bool found = false;
+  float rt = tmax;
+  for (int gi = 0; gi < ng; gi++) {
+    if (!ray_box_maybe<DIM>(G.pgroup + gi * kGroupStride, o, inv, rt)) continue;
+    const int p1 = (gi + 1) * kGroup < np ? (gi + 1) * kGroup : np;
+    for (int p = gi * kGroup; p < p1; p++) {
+      const float* P = G.prim + p * PS;
+      if constexpr (DIM == 2) {
+        const float u0 = P[0] - o[0], u1 = P[1] - o[1];
+        const float v0 = P[2], v1 = P[3];
+        const float dv = dir[0] * v1 - dir[1] * v0;
+        if (!(__builtin_fabsf(dv) > kFltEps)) continue;
+        const float ud = u0 * dir[1] - u1 * dir[0];
+        const float uv = u0 * v1 - u1 * v0;
+        const float ra = __builtin_amdgcn_rcpf(dv);
+        const float ta = ud * ra, da = uv * ra;
+        if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
+            (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
+          continue;
+      } else {
+        float v1[3], v2[3], pp[3], sv[3], q[3];
+        for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; sv[k] = o[k] - P[k]; }
+        cross3(pp, dir, v2);
+        const float det = dotv<3>(v1, pp);
+        if (!(__builtin_fabsf(det) > kFltEps)) continue;
+        const float ra = __builtin_amdgcn_rcpf(det);
+        const float vn = dotv<3>(sv, pp), va = vn * ra;
+        if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) continue;
+        cross3(q, sv, v1);
+        const float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
+        const float wa = wn * ra, da = dn * ra;
+        if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
+            (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
+          continue;
+      }
+      found |= ray_prim_exact<DIM>(P, o, dir, rt, h);
     }
   }
   if (found) normalize_rcp<DIM>(h->n);
@@ -319,7 +427,7 @@ __device__ __forceinline__ bool ray_hit(const float* prims, int np, const float*
 template <int DIM>
 __device__ bool ray_occluded(const float* prims, int np, const float* o, const float* dir, float tmax) {
   Hit h;
-  return ray_hit<DIM>(prims, np, o, dir, tmax, &h);
+  return ray_hit_scan<DIM>(prims, np, o, dir, tmax, &h);
 }
 
 // isWideSilhouetteVertex / isWideSilhouetteEdge (wide_query_operations.h:328-395)
@@ -350,9 +458,95 @@ __device__ __forceinline__ bool is_silhouette(const float* S, const float* view,
   return dot0 * dot1 < 0.0f;
 }
 
-// computeStarRadius (fcpw_scene_loader.h:621-641), brute-force closest silhouette
+// isWideSilhouetteVertex without the division and square root: the view
+// direction is normalised with the hardware rsq, whose error (with the dot-product
+// rounding) stays below 1e-6 on the unit-scale dots, so outside a 1e-5 band
+// around every threshold the decision equals the exact test's.  Returns 1/0 when
+// certain, 2 when the exact test must decide.  (2D vertex candidates.)
+__device__ __forceinline__ int silhouette_class2(const float* S, const float* view, float d2raw, bool flip,
+                                                 float prec) {
+  const float sign = flip ? 1.0f : -1.0f;
+  const float* n0 = S + 2;
+  const float* n1 = S + 4;
+  const float p2 = prec * prec;
+  if (d2raw < p2 * 0.9999f) {  // certainly d <= prec: the exact test's normal-only branch
+    const float det = n0[0] * n1[1] - n0[1] * n1[0];
+    return sign * det > prec ? 1 : 0;
+  }
+  if (d2raw <= p2 * 1.0001f) return 2;
+  const float r = __builtin_amdgcn_rsqf(d2raw);
+  const float dot0 = (view[0] * n0[0] + view[1] * n0[1]) * r;
+  const float dot1 = (view[0] * n1[0] + view[1] * n1[1]) * r;
+  const float tol = 1e-5f;
+  const float a0 = __builtin_fabsf(dot0), a1 = __builtin_fabsf(dot1);
+  float v;
+  if (a0 < prec - tol) {
+    v = sign * dot1;
+  } else if (a0 > prec + tol) {
+    if (a1 > prec + tol) return dot0 * dot1 < 0.0f ? 1 : 0;
+    if (!(a1 < prec - tol)) return 2;
+    v = sign * dot0;
+  } else {
+    return 2;
+  }
+  return v > prec + tol ? 1 : (v < prec - tol ? 0 : 2);
+}
+
+// Certain rejection of a whole silhouette group: the squared distance from x to
+// the group's padded box exceeds r2 (with margin), so every candidate in it is
+// rejected by the exact distance test too.
 template <int DIM>
-__device__ __forceinline__ float star_radius(const float* sil, int ns, int np, const float* x, float minR,
+__device__ __forceinline__ bool ball_box_maybe(const float* B, const float* x, float r2) {
+  float d2 = 0.0f;
+  for (int k = 0; k < DIM; k++) {
+    const float e = __builtin_fmaxf(__builtin_fmaxf(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
+    d2 += e * e;
+  }
+  return !(d2 > r2 * 1.00001f);
+}
+
+// Certain absence of silhouettes in a group, from the normal cone (axis a,
+// half-angle alpha) and the view cone of x on the group's bounding sphere (axis
+// w = x - c, half-angle beta = asin(rho/|w|)): every view direction u and every
+// adjacent normal n then satisfy angle(u, n) in [theta - alpha - beta, theta +
+// alpha + beta], theta = angle(w, a).  When that interval lies inside
+// [0, acos(prec + m)) every dot is > prec + m (all faces front-facing), when it
+// lies inside (pi - acos(prec + m), pi] every dot is < -(prec + m): either way the
+// exact test (isWideSilhouetteVertex/Edge) rejects every candidate.  m = 1e-3
+// dwarfs the error of the rsq/sqrt arithmetic used here.  Groups holding a
+// candidate next to a missing primitive, or x within prec of the sphere, are
+// never culled.
+template <int DIM>
+__device__ __forceinline__ bool cone_culled(const float* B, const float* x, float prec) {
+  if (B[15] != 0.0f) return false;
+  const float rho = B[11];
+  float w[DIM];
+  for (int k = 0; k < DIM; k++) w[k] = x[k] - B[8 + k];
+  const float D2 = dotv<DIM>(w, w);
+  const float lim = rho + 1.01f * prec + 1e-6f;
+  if (!(D2 > lim * lim)) return false;
+  const float invD = __builtin_amdgcn_rsqf(D2);
+  const float sinb = rho * invD, cosb = __builtin_amdgcn_sqrtf(smax(0.0f, 1.0f - sinb * sinb));
+  const float sina = B[3], cosa = B[7];
+  const float cosg = cosa * cosb - sina * sinb, sing = sina * cosb + cosa * sinb;  // gamma = alpha + beta
+  float wa = 0.0f;
+  for (int k = 0; k < DIM; k++) wa += w[k] * B[12 + k];
+  const float cost = smin(smax(wa * invD, -1.0f), 1.0f), sint = __builtin_amdgcn_sqrtf(smax(0.0f, 1.0f - cost * cost));
+  const float thr = prec + 1e-3f;
+  // front: theta + gamma in (0, pi) and cos(theta + gamma) > thr
+  const float c_p = cost * cosg - sint * sing, s_p = sint * cosg + cost * sing;
+  if (s_p > 1e-3f && c_p > thr) return true;
+  // back: theta - gamma in (0, pi) and cos(theta - gamma) < -thr
+  const float c_m = cost * cosg + sint * sing, s_m = sint * cosg - cost * sing;
+  return s_m > 1e-3f && c_m < -thr;
+}
+
+// computeStarRadius (fcpw_scene_loader.h:621-641): the closest silhouette point
+// within maxR, candidates in index order (brute force over the staged records,
+// fcpw Baseline semantics); groups out of reach are skipped, 2D candidates are
+// classified by silhouette_class2 before any exact square root or division.
+template <int DIM>
+__device__ __forceinline__ float star_radius(const LGeom& G, int ns, int nsg, int np, const float* x, float minR,
                                              float maxR, float prec, bool flipOrient) {
   constexpr int SS = Layout<DIM>::sil;
   if (minR > maxR) return maxR;
@@ -360,36 +554,49 @@ __device__ __forceinline__ float star_radius(const float* sil, int ns, int np, c
     bool flip = !flipOrient;
     float r2 = maxR < kFltMax ? maxR * maxR : kFltMax;
     float minR2 = minR * minR;
-    bool found = false;
+    bool found = false, done = false;
     float best = 0.0f;
+    DIAG_LANE(D_SCALLS);
     if (!(minR2 >= r2)) {
-      for (int s = 0; s < ns; s++) {
-        const float* S = sil + s * SS;
-        float view[DIM], d;
-        if constexpr (DIM == 2) {
-          view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
-          float d2raw = view[0] * view[0] + view[1] * view[1];
-          // certain rejection: fl(fl(sqrt(q))^2) >= q(1 - 2^-22) > r2 (no sqrt needed)
-          if (d2raw > r2 * 1.000001f) continue;
-          d = __builtin_sqrtf(d2raw);
-        } else {
-          // certain rejection against the edge's bounding sphere before the exact query
-          float e[3], hl[3];
-          for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
-          float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
-          float lo = dm - hr;
-          if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) continue;
-          float pt[3], t;
-          d = cp_segment<3>(S, S + 3, x, pt, &t);
-          for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
-        }
-        float d2 = d * d;
-        if (d2 > r2) continue;
-        const float miss = DIM == 2 ? S[6] : S[12];
-        bool sil_ok = miss != 0.0f ? true : is_silhouette<DIM>(S, view, d, flip, prec);
-        if (sil_ok && d2 <= r2) {
-          r2 = d2; best = d; found = true;
-          if (minR2 >= r2) break;
+      for (int gi = 0; gi < nsg && !done; gi++) {
+        const float* B = G.sgroup + gi * kSGroupStride;
+        if (!ball_box_maybe<DIM>(B, x, r2) || cone_culled<DIM>(B, x, prec)) continue;
+        DIAG_LANE(D_SGVISIT);
+        const int s1 = (gi + 1) * kGroup < ns ? (gi + 1) * kGroup : ns;
+        for (int s = gi * kGroup; s < s1; s++) {
+          const float* S = G.sil + s * SS;
+          const float miss = DIM == 2 ? S[6] : S[12];
+          float view[DIM], d;
+          int cls = 2;
+          if constexpr (DIM == 2) {
+            view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
+            float d2raw = view[0] * view[0] + view[1] * view[1];
+            // certain rejection: fl(fl(sqrt(q))^2) >= q(1 - 2^-22) > r2 (no sqrt needed)
+            if (d2raw > r2 * 1.000001f) continue;
+            DIAG_LANE(D_SCAND);
+            cls = miss != 0.0f ? 1 : silhouette_class2(S, view, d2raw, flip, prec);
+            if (cls == 0) continue;  // certainly not a silhouette: the exact loop skips it too
+            DIAG_LANE(D_SEXACT);
+            d = __builtin_sqrtf(d2raw);
+          } else {
+            // certain rejection against the edge's bounding sphere before the exact query
+            float e[3], hl[3];
+            for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
+            float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
+            float lo = dm - hr;
+            if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) continue;
+            float pt[3], t;
+            d = cp_segment<3>(S, S + 3, x, pt, &t);
+            for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
+            if (miss != 0.0f) cls = 1;
+          }
+          float d2 = d * d;
+          if (d2 > r2) continue;
+          bool sil_ok = cls == 1 ? true : is_silhouette<DIM>(S, view, d, flip, prec);
+          if (sil_ok && d2 <= r2) {
+            r2 = d2; best = d; found = true;
+            if (minR2 >= r2) { done = true; break; }
+          }
         }
       }
     }
@@ -832,10 +1039,11 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
 // walk continues, else its termination code.  The loop test (Dirichlet distance
 // above the epsilon shell) is evaluated at the top of every step.
 template <int DIM>
-__device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& prm, const float* prims,
-                                         const float* sil, float& dirichletDist, Pcg32& smp, Gfn<DIM>& g,
+__device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& prm, const LGeom& G,
+                                         float& dirichletDist, Pcg32& smp, Gfn<DIM>& g,
                                          WalkState<DIM>& st, uint32_t* steps, uint32_t* iters) {
   const int np = sc.n_prims, ns = sc.n_sil;
+  const float* prims = G.prim;
   {
     if (!(dirichletDist > prm.epsilon_shell)) return WC_DIRICHLET;
     float starRadius;
@@ -849,8 +1057,10 @@ __device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& pr
     if (prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL) {
       starRadius = dirichletDist;
     } else {
-      starRadius = star_radius<DIM>(sil, ns, np, st.pt, prm.min_star_radius, dirichletDist,
+      DIAG_T0(t_star);
+      starRadius = star_radius<DIM>(G, ns, sc.n_sgroups, np, st.pt, prm.min_star_radius, dirichletDist,
                                     prm.silhouette_precision, flip);
+      DIAG_ADD(D_STAR, t_star);
       if (prm.min_star_radius <= dirichletDist)
         starRadius = smax(0.99f * starRadius, prm.min_star_radius);
     }
@@ -873,7 +1083,9 @@ __device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& pr
       for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
     }
     Hit ip;
-    bool hit = !WOS_ABL_NO_RAY && np > 0 && ray_hit<DIM>(prims, np, org, dir, starRadius, &ip);
+    DIAG_T0(t_ray);
+    bool hit = !WOS_ABL_NO_RAY && np > 0 && ray_hit<DIM>(G, np, sc.n_pgroups, org, dir, starRadius, &ip);
+    DIAG_ADD(D_RAY, t_ray);
     if (!hit) {
       for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
       ip.d = starRadius;
@@ -886,7 +1098,9 @@ __device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& pr
     }
     if (!prm.ignore_source) {
       float pdf, sp[DIM];
+      DIAG_T0(t_smp);
       sample_volume<DIM>(g, dir, smp, &pdf, sp, iters, false);
+      DIAG_ADD(D_SAMPLE, t_smp);
       if (g.r <= ip.d) {
         float contrib = g.norm() * source_value<DIM>(sc, sp);
         st.totalSource += st.throughput * contrib;
@@ -1093,13 +1307,25 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   }
 }
 
+// LDS image: prims | silhouettes | prim groups | silhouette groups (each block 16-B aligned)
 template <int DIM>
-__device__ __forceinline__ void stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
+__device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
   constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
-  const int primN = sc.n_prims * PS, silN = with_sil ? sc.n_sil * SS : 0;
-  const int primAl = (primN + 3) & ~3;
+  const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
+  const int primAl = (primN + 3) & ~3, silAl = (silN + 3) & ~3;
+  const int pgN = sc.n_pgroups * kGroupStride, sgN = sc.n_sgroups * kSGroupStride;
+  LGeom G;
+  G.prim = smem;
+  G.sil = smem + primAl;
+  G.pgroup = smem + primAl + silAl;
+  G.sgroup = G.pgroup + pgN;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
-  for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
+  if (with_sil) {
+    for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
+    for (int i = threadIdx.x; i < pgN; i += kBlock) smem[primAl + silAl + i] = sc.pgroup[i];
+    for (int i = threadIdx.x; i < sgN; i += kBlock) smem[primAl + silAl + pgN + i] = sc.sgroup[i];
+  }
+  return G;
 }
 
 __device__ __forceinline__ void flush_counter(unsigned long long* counters, int slot, uint32_t v, int lane) {
@@ -1187,13 +1413,13 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int s_ctr[C_NUM];
-  constexpr int PS = Layout<DIM>::prim;
   const int lane = threadIdx.x & (kWave - 1);
-  stage_geometry<DIM>(sc, smem, true);
+  const LGeom G = stage_geometry<DIM>(sc, smem, true);
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
+#endif
   __syncthreads();
-  const float* Lprim = smem;
-  const float* Lsil = smem + ((sc.n_prims * PS + 3) & ~3);
   (void)geom_floats;
 
   const uint32_t T = (uint32_t)tk.T;
@@ -1211,6 +1437,7 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
   uint32_t wsteps = 0;
 
   for (;;) {
+    DIAG_T0(t_loop);
     // ---- hand out tasks to idle lanes (uniform control flow)
     bool fresh = false;
     for (;;) {
@@ -1257,7 +1484,11 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
       wsteps = 1;  // the first ball
     }
 
-    const int code = walk_step<DIM>(sc, prm, Lprim, Lsil, ddist, ws, g, st, &wsteps, &c_iters);
+    DIAG_COUNT(D_ITERS, 1);
+    DIAG_COUNT(D_LANES, __popcll(__ballot(1)));
+    DIAG_T0(t_step);
+    const int code = walk_step<DIM>(sc, prm, G, ddist, ws, g, st, &wsteps, &c_iters);
+    DIAG_ADD(D_STEP, t_step);
     if (code >= 0) {
       const bool recorded = code == WC_DIRICHLET || code == WC_RR;
       if (recorded) {
@@ -1270,10 +1501,14 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
                 1u);
       t = -1;
     }
+    DIAG_ADD(D_LOOP, t_loop);
   }
 
   flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+#endif
   if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
     unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
     if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
@@ -1281,34 +1516,62 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
 }
 
 // ---- kernel 3: statistics + outputs ----------------------------------------
+// One thread per point, kFoldPoints points per block.  The records of the
+// block's points are contiguous (point-major tasks), so they are staged through
+// LDS in chunks of kFoldChunk records per point with coalesced 64-B loads, then
+// every thread folds its own point's chunk in walk order.
+constexpr int kFoldPoints = 128, kFoldChunk = 16;
+
 template <int DIM>
-__global__ __launch_bounds__(kBlock) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
-                                                          float* __restrict__ p_out, float* __restrict__ g_out,
-                                                          int32_t* __restrict__ nest_out,
-                                                          int32_t* __restrict__ steps_out) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+__global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
+                                                               float* __restrict__ p_out,
+                                                               float* __restrict__ g_out,
+                                                               int32_t* __restrict__ nest_out,
+                                                               int32_t* __restrict__ steps_out) {
+  constexpr int NF = 3 + 2 * DIM;  // code | total | first | bdir[DIM] | sdir[DIM]
+  constexpr int LD = kFoldChunk + 1;
+  __shared__ float lds[NF][kFoldPoints][LD];
+  const int tid = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kFoldPoints;
+  const int nb = (int)((n - p0) < kFoldPoints ? (n - p0) : kFoldPoints);
+  const int64_t i = p0 + tid;
   const int64_t T = tk.T;
-  const int ps = tk.pstate[i];
+  const int wpp = tk.wpp;
+  const int ps = tid < nb ? tk.pstate[i] : 0;
   const bool estimate = ps & kPtEstimate;
   float mean[DIM + 1];
   for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
-  float sFirst = 0.0f;
+  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
   int sN = 0;
   uint32_t steps = 0;
-  if (estimate) {
-    const int64_t t0 = i * tk.wpp;
-    for (int j = 0; j < prm.n_pairs; ++j) {
-      float cvb = mean[0];
-      float cvs = sFirst / (float)(sN > 1 ? sN : 1);
-      if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
-      for (int a = 0; a < prm.n_anti; a++) {
-        const int64_t t = t0 + j * prm.n_anti + a;
-        const uint32_t code = tk.code[t];
+  for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
+    const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
+    for (int e = tid; e < nb * kFoldChunk; e += kFoldPoints) {
+      const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
+      if (j >= cnt) continue;
+      const int64_t t = (p0 + pp) * wpp + c0 + j;
+      lds[0][pp][j] = __uint_as_float(tk.code[t]);
+      lds[1][pp][j] = tk.total[t];
+      lds[2][pp][j] = tk.first[t];
+      for (int k = 0; k < DIM; k++) {
+        lds[3 + k][pp][j] = tk.bdir[k * T + t];
+        lds[3 + DIM + k][pp][j] = tk.sdir[k * T + t];
+      }
+    }
+    __syncthreads();
+    if (estimate) {
+      for (int j = 0; j < cnt; j++) {
+        const int r = c0 + j;
+        if (r % prm.n_anti == 0) {  // a new antithetic pair: control variates from the walks before it
+          cvb = mean[0];
+          cvs = sFirst / (float)(sN > 1 ? sN : 1);
+          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
+        }
+        const uint32_t code = __float_as_uint(lds[0][tid][j]);
         steps += code >> 1;
         if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
-        const float total = tk.total[t];
-        const float first = tk.first[t];
+        const float total = lds[1][tid][j];
+        const float first = lds[2][tid][j];
         sN += 1;
         const float fN = (float)sN;
         {
@@ -1316,15 +1579,17 @@ __global__ __launch_bounds__(kBlock) void wos_fold_kernel(const DevParams prm, c
           mean[0] += delta / fN;
         }
         for (int k = 0; k < DIM; k++) {
-          const float be = (total - first - cvb) * tk.bdir[k * T + t];
-          const float se = (first - cvs) * tk.sdir[k * T + t];
+          const float be = (total - first - cvb) * lds[3 + k][tid][j];
+          const float se = (first - cvs) * lds[3 + DIM + k][tid][j];
           const float delta = (be + se) - mean[k + 1];
           mean[k + 1] += delta / fN;
         }
         sFirst += first;
       }
     }
+    __syncthreads();
   }
+  if (tid >= nb) return;
   const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
   p_out[i] = maskP ? 0.0f : mean[0];
   for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];
@@ -1407,12 +1672,12 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
 
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s) {
-  const int grid = (int)((n + kBlock - 1) / kBlock);
+  const int grid = (int)((n + kFoldPoints - 1) / kFoldPoints);
   if (grid < 1) return hipSuccess;
   if (dim == 2)
-    hipLaunchKernelGGL(wos_fold_kernel<2>, dim3(grid), dim3(kBlock), 0, s, prm, tk, n, p, g, nest, steps);
+    hipLaunchKernelGGL(wos_fold_kernel<2>, dim3(grid), dim3(kFoldPoints), 0, s, prm, tk, n, p, g, nest, steps);
   else
-    hipLaunchKernelGGL(wos_fold_kernel<3>, dim3(grid), dim3(kBlock), 0, s, prm, tk, n, p, g, nest, steps);
+    hipLaunchKernelGGL(wos_fold_kernel<3>, dim3(grid), dim3(kFoldPoints), 0, s, prm, tk, n, p, g, nest, steps);
   return hipGetLastError();
 }
 
@@ -1422,6 +1687,24 @@ hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3>, kBlock, shmem);
   return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2>, kBlock, shmem)
                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3>, kBlock, shmem);
+}
+
+void diag_dump(const char* tag) {
+#if WOS_DIAG
+  unsigned long long d[D_NUM];
+  hipMemcpyFromSymbol(d, HIP_SYMBOL(g_diag), sizeof(d));
+  fprintf(stderr, "[diag %s] iters %llu lanes/iter %.2f  cycles/iter: step %.0f star %.0f ray %.0f sample %.0f loop %.0f  ray_overflow %llu\n",
+          tag, d[D_ITERS], (double)d[D_LANES] / (double)(d[D_ITERS] ? d[D_ITERS] : 1),
+          (double)d[D_STEP] / d[D_ITERS], (double)d[D_STAR] / d[D_ITERS], (double)d[D_RAY] / d[D_ITERS],
+          (double)d[D_SAMPLE] / d[D_ITERS], (double)d[D_LOOP] / d[D_ITERS], d[D_RAYOVF]);
+  fprintf(stderr, "[diag %s] star calls %llu: groups visited/call %.2f, candidates/call %.2f, exact/call %.2f\n", tag,
+          d[D_SCALLS], (double)d[D_SGVISIT] / d[D_SCALLS], (double)d[D_SCAND] / d[D_SCALLS],
+          (double)d[D_SEXACT] / d[D_SCALLS]);
+  unsigned long long z[D_NUM] = {};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
+#else
+  (void)tag;
+#endif
 }
 
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s) {

@@ -21,5 +21,6 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
                        int32_t* nest, int32_t* steps, hipStream_t s);
 // which: 0 first-ball kernel, 1 walk kernel
 hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks);
+void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
 }  // namespace wos

@@ -13,6 +13,8 @@
 //           3D  [pa.xyz pb.xyz n0.xyz n1.xyz miss pad pad pad] (16 floats)
 //   dprim/dpaux : same as prim/paux for the (optional) Dirichlet boundary
 //   source: the -div(u) grid, row-major; 2D (H rows ~ y, W cols ~ x), 3D (X,Y,Z)
+//   pgroup/sgroup: padded boxes of kGroup consecutive prims / silhouettes
+//           (8 / 16 floats, see kSGroupStride), used only to skip whole groups
 //
 // The Neumann prim + sil arrays are staged into LDS by every workgroup.
 #pragma once
@@ -23,6 +25,11 @@ namespace wos {
 constexpr int kPrimStride2 = 4, kPrimStride3 = 9;
 constexpr int kAuxStride2 = 6, kAuxStride3 = 21;
 constexpr int kSilStride2 = 8, kSilStride3 = 16;
+// culling groups: kGroup consecutive primitives (or silhouette candidates) share
+// one padded bounding box record [min.xyz pad max.xyz pad]; silhouette groups add
+// a bounding sphere and the cone of their adjacent normals:
+//   [min.xyz sin(alpha) | max.xyz cos(alpha) | c.xyz rho | axis.xyz nocull]
+constexpr int kGroup = 8, kGroupStride = 8, kSGroupStride = 16;
 
 template <int DIM> struct Layout;
 template <> struct Layout<2> {
@@ -41,6 +48,9 @@ struct DevScene {
   const float* dprim;
   const float* dpaux;
   const float* source;
+  const float* pgroup;   // n_pgroups boxes over consecutive Neumann primitives
+  const float* sgroup;   // n_sgroups boxes over consecutive silhouette candidates
+  int32_t n_pgroups, n_sgroups;
   int32_t sdims[3];
   float pmin[3], pmax[3], ext[3];
   float absorption;

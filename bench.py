@@ -45,10 +45,37 @@ def parse():
 
 
 def algorithmic_bytes(n_points, dim, total_steps, grid_elems):
-    """Bytes one launch must move at minimum: read the query points, write p and
-    grad, read the source grid once, plus one 4-byte source texel per ball step
-    (walk_on_stars.h:273 / :539).  Geometry (<4 KB, LDS-staged) is negligible."""
+    """Bytes one projection must move at minimum: read the query
+    points, write p and grad, read the source grid once, plus one 4-byte source
+    texel per ball step (walk_on_stars.h:273 / :539).  Geometry (<4 KB,
+    LDS-staged) is negligible."""
     return n_points * 4 * dim + n_points * 4 * (1 + dim) + 4 * grid_elems + 4 * total_steps
+
+
+def walk_kernel_bytes(walk_kernel_steps, grid_elems):
+    """Algorithmic bytes of the dominant kernel (wos_walk_kernel) per launch: one
+    4-byte source texel per walk() step plus the source grid once.  The walk-task
+    records it reads and writes are an artifact of the kernel split, not part of
+    the algorithm, so they are not counted (they show up in `traffic`)."""
+    return 4 * walk_kernel_steps + 4 * grid_elems
+
+
+def measured_traffic(points, walks):
+    """HBM bytes per walk-kernel launch from the committed rocprofv3 PMC passes
+    (tools/collect_traffic.py -> profiles/*walk_traffic.json), if they were taken
+    on this configuration; else None."""
+    prof = os.path.join(REPO, "profiles")
+    best = None
+    if os.path.isdir(prof):
+        for f in sorted(os.listdir(prof)):
+            if f.endswith("walk_traffic.json"):
+                try:
+                    d = json.load(open(os.path.join(prof, f)))
+                except (OSError, ValueError):
+                    continue
+                if d.get("points") == points and d.get("walks") == walks:
+                    best = d
+    return best
 
 
 def cpu_baseline(cfg, n_threads, budget_s):
@@ -130,12 +157,19 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     steps_rec = steps_all = 0
-    kernel_ms = []
+    kernel_ms, walk_ms, fb_ms, fold_ms, walk_kernel_steps, launches = [], [], [], [], 0, 0
     for _ in range(a.steps):
         st = step()
         steps_rec += st["walk_steps"]
         steps_all += st["walk_steps"] + st["wasted_steps"]
         kernel_ms.append(st["kernel_ms"])
+        walk_ms.append(st["walk_ms"])
+        fb_ms.append(st["first_ball_ms"])
+        fold_ms.append(st["fold_ms"])
+        launches += st["walk_launches"]
+        # every walk has exactly one first-ball step (taken in wos_first_ball_kernel)
+        n_walks_run = st["walks_recorded"] + st["walks_escaped"] + st["walks_max_length"]
+        walk_kernel_steps += st["walk_steps"] + st["wasted_steps"] - n_walks_run
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -153,9 +187,13 @@ def main():
 
     if rank == 0:
         kms = float(np.mean(kernel_ms))
+        # dominant kernel: wos_walk_kernel, timed with HIP events on the solve's stream
+        wms = float(np.sum(walk_ms) / max(1, launches))
+        wbytes = walk_kernel_bytes(walk_kernel_steps / max(1, launches), cfg["source"].size)
+        achieved = wbytes / (wms * 1e-3) / 1e9
         steps_per_launch = steps_all / a.steps / world
-        abytes = algorithmic_bytes(n_local, dim, steps_per_launch, cfg["source"].size)
-        achieved = abytes / (kms * 1e-3) / 1e9
+        pbytes = algorithmic_bytes(n_local, dim, steps_per_launch, cfg["source"].size)
+        tr = measured_traffic(a.points, a.walks)
         line = {
             "metric": "WoS walk-steps/sec + pressure-projection wall-time per step, 2D karman 64k pts",
             "value": steps_rec / elapsed,
@@ -178,7 +216,14 @@ def main():
             "walk_steps_per_projection": steps_rec / a.steps,
             "wasted_steps_per_projection": (steps_all - steps_rec) / a.steps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": tr["bytes_per_launch"] if tr else None,
+                         "kernel": "wos_walk_kernel", "kernel_ms": wms,
+                         "algorithmic_bytes_per_launch": wbytes,
+                         "traffic_source": tr["source"] if tr else None,
+                         "projection_achieved_GBps": pbytes / (kms * 1e-3) / 1e9},
+            "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
+                                "fold": float(np.mean(fold_ms)), "total": kms},
         }
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)

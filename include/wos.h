@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 1
+#define WOS_ABI_VERSION 2
 
 enum {
     WOS_OK = 0,
@@ -117,7 +117,11 @@ typedef struct wos_stats {
     uint64_t walks_dirichlet;
     uint64_t points_estimated;
     uint64_t rejection_iters;
-    double kernel_ms;           /* device time of the solve kernel (HIP events) */
+    double kernel_ms;           /* device time of the whole solve: all batches, all kernels (HIP events) */
+    double first_ball_ms;       /* of which: point setup + first balls (wos_first_ball_kernel) */
+    double walk_ms;             /* of which: the walks (wos_walk_kernel) -- the dominant kernel */
+    double fold_ms;             /* of which: statistics + masked outputs (wos_fold_kernel) */
+    uint64_t walk_launches;     /* walk-kernel launches (one per batch of points) */
 } wos_stats;
 
 /* Replaces runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d

@@ -66,6 +66,7 @@ struct wos_scene {
   int64_t pstate_cap = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> bev;  // per-batch kernel boundary events (4 per batch), grow-only
   int num_cus = 0;
 };
 
@@ -137,6 +138,7 @@ static void scene_release(wos_scene* s) {
   hipFree(s->d_pstate);
   if (s->ev0) hipEventDestroy(s->ev0);
   if (s->ev1) hipEventDestroy(s->ev1);
+  for (hipEvent_t e : s->bev) hipEventDestroy(e);
 }
 
 int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
@@ -390,20 +392,31 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   }
   unsigned int* q_points = (unsigned int*)(s->d_counters + wos::kNumCounters);
   unsigned int* q_tasks = (unsigned int*)(s->d_counters + wos::kNumCounters + 1);
+  const int64_t n_batches = n > 0 ? (n + batch - 1) / batch : 0;
+  while ((int64_t)s->bev.size() < 4 * n_batches) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreate(&e));
+    s->bev.push_back(e);
+  }
   HIP_TRY(hipEventRecord(s->ev0, st));
   for (int64_t b0 = 0; b0 < n; b0 += batch) {
+    hipEvent_t* ev = &s->bev[4 * (b0 / batch)];
     const int64_t nb = std::min(batch, n - b0);
     wos::DevTasks tk = task_view(s, dim, nb * wpp, (int32_t)wpp);
     const int64_t bbase = index_base + b0 * index_stride;
     if (b0 > 0)
       HIP_TRY(hipMemsetAsync(s->d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, s->d_counters,
                                     q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
     HIP_TRY(wos::launch_walks(dim, s->dev, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,
                               shmem_walk, geom_floats, st));
+    HIP_TRY(hipEventRecord(ev[2], st));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
                              d_steps ? d_steps + b0 : nullptr, st));
+    HIP_TRY(hipEventRecord(ev[3], st));
   }
   HIP_TRY(hipEventRecord(s->ev1, st));
   if (!dev_ptrs && n > 0) {
@@ -430,6 +443,16 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     stats->kernel_ms = ms;
+    stats->first_ball_ms = stats->walk_ms = stats->fold_ms = 0.0;
+    stats->walk_launches = (uint64_t)n_batches;
+    for (int64_t b = 0; b < n_batches; b++) {
+      hipEvent_t* ev = &s->bev[4 * b];
+      float a = 0.0f, w = 0.0f, f = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+      HIP_TRY(hipEventElapsedTime(&w, ev[1], ev[2]));
+      HIP_TRY(hipEventElapsedTime(&f, ev[2], ev[3]));
+      stats->first_ball_ms += a; stats->walk_ms += w; stats->fold_ms += f;
+    }
   }
   return WOS_OK;
 }

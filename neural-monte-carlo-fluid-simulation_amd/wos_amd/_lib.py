@@ -9,6 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
+ABI_VERSION = 2  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
@@ -60,11 +61,11 @@ class SolverParams(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_max_length",
-        "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [("kernel_ms", C.c_double)]
+        "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [
+        (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)]
 
     def as_dict(self):
-        return {n: (float(getattr(self, n)) if n == "kernel_ms" else int(getattr(self, n)))
-                for n, _ in self._fields_}
+        return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n))) for n, t in self._fields_}
 
 
 # exported symbols, exactly those declared in include/wos.h
@@ -107,6 +108,8 @@ def load():
     L.wos_last_error.argtypes = []
     L.wos_abi_version.restype = C.c_int32
     L.wos_device_count.restype = C.c_int32
+    if L.wos_abi_version() != ABI_VERSION:
+        raise WosError(f"{LIB_PATH}: ABI {L.wos_abi_version()} != binding ABI {ABI_VERSION}; rebuild the library")
     _lib = L
     return L
 

@@ -43,6 +43,9 @@ namespace wos {
 #ifndef WOS_DIAG
 #define WOS_DIAG 0
 #endif
+#ifndef WOS_RAY_WAVE
+#define WOS_RAY_WAVE 1
+#endif
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
@@ -1035,93 +1038,378 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
   }
 }
 
-// One iteration of the walk loop (walk_on_stars.h:135-329): returns -1 while the
-// walk continues, else its termination code.  The loop test (Dirichlet distance
-// above the epsilon shell) is evaluated at the top of every step.
+// One iteration of the walk loop (walk_on_stars.h:135-329), split around the
+// star-radius query so that the query can run wave-cooperatively:
+//   walk_step_begin  -- loop test (Dirichlet distance above the epsilon shell),
+//                       double-sided normal flip, whether a silhouette query is due;
+//   star_radius_wave -- (convergent, all lanes) computeStarRadius;
+//   walk_step_end    -- ball update, direction, ray, source sample, move, roulette.
+// Returns -1 while the walk continues, else its termination code.
 template <int DIM>
-__device__ __forceinline__ int walk_step(const DevScene& sc, const DevParams& prm, const LGeom& G,
-                                         float& dirichletDist, Pcg32& smp, Gfn<DIM>& g,
-                                         WalkState<DIM>& st, uint32_t* steps, uint32_t* iters) {
-  const int np = sc.n_prims, ns = sc.n_sil;
-  const float* prims = G.prim;
-  {
-    if (!(dirichletDist > prm.epsilon_shell)) return WC_DIRICHLET;
-    float starRadius;
-    bool flip = false;
-    if (sc.double_sided && st.onNeumann) {
-      if (st.prevDist > 0.0f && dotv<DIM>(st.prevDir, st.n) < 0.0f) {
-        for (int k = 0; k < DIM; k++) st.n[k] *= -1.0f;
-        flip = true;
-      }
+__device__ __forceinline__ int walk_step_begin(const DevScene& sc, const DevParams& prm, float dirichletDist,
+                                               WalkState<DIM>& st, bool* flip, bool* query) {
+  if (!(dirichletDist > prm.epsilon_shell)) return WC_DIRICHLET;
+  *flip = false;
+  if (sc.double_sided && st.onNeumann) {
+    if (st.prevDist > 0.0f && dotv<DIM>(st.prevDir, st.n) < 0.0f) {
+      for (int k = 0; k < DIM; k++) st.n[k] *= -1.0f;
+      *flip = true;
     }
-    if (prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL) {
-      starRadius = dirichletDist;
-    } else {
-      DIAG_T0(t_star);
-      starRadius = star_radius<DIM>(G, ns, sc.n_sgroups, np, st.pt, prm.min_star_radius, dirichletDist,
-                                    prm.silhouette_precision, flip);
-      DIAG_ADD(D_STAR, t_star);
-      if (prm.min_star_radius <= dirichletDist)
-        starRadius = smax(0.99f * starRadius, prm.min_star_radius);
-    }
-    g.update_ball(st.pt, starRadius);
-    (*steps)++;
-    float u[2];
-    u[0] = smp.nextf();
-    if constexpr (DIM == 3) u[1] = smp.nextf();
-    float dir[DIM];
-    sample_unit_sphere<DIM>(u, dir);
-    if (st.onNeumann && dotv<DIM>(st.n, dir) > 0.0f)
-      for (int k = 0; k < DIM; k++) dir[k] *= -1.0f;
-
-    float org[DIM];
-    if (st.onNeumann) {
-      float mn[DIM];
-      for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
-      offset_point<DIM>(st.pt, mn, org);
-    } else {
-      for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
-    }
-    Hit ip;
-    DIAG_T0(t_ray);
-    bool hit = !WOS_ABL_NO_RAY && np > 0 && ray_hit<DIM>(G, np, sc.n_pgroups, org, dir, starRadius, &ip);
-    DIAG_ADD(D_RAY, t_ray);
-    if (!hit) {
-      for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
-      ip.d = starRadius;
-    }
-    if (!prm.ignore_neumann) {
-      float rn[3] = {0.0f, 0.0f, 0.0f};
-      for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
-      bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
-      if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
-    }
-    if (!prm.ignore_source) {
-      float pdf, sp[DIM];
-      DIAG_T0(t_smp);
-      sample_volume<DIM>(g, dir, smp, &pdf, sp, iters, false);
-      DIAG_ADD(D_SAMPLE, t_smp);
-      if (g.r <= ip.d) {
-        float contrib = g.norm() * source_value<DIM>(sc, sp);
-        st.totalSource += st.throughput * contrib;
-      }
-    }
-    if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
-    st.prevDist = ip.d;
-    for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
-    st.onNeumann = hit;
-    st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
-    if (st.throughput < prm.rr_threshold) {
-      float survival = st.throughput / prm.rr_threshold;
-      if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
-      st.throughput = prm.rr_threshold;
-    }
-    st.walkLength++;
-    if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
-    if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
-    dirichletDist = dirichlet_dist_lane<DIM>(sc, st.pt);
   }
+  *query = !(prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL);
   return -1;
+}
+
+// ball + direction + ray origin; the ray query follows (walk_on_stars.h:169-210)
+template <int DIM>
+__device__ __forceinline__ float walk_step_mid(const DevParams& prm, float dirichletDist, Pcg32& smp, Gfn<DIM>& g,
+                                               WalkState<DIM>& st, uint32_t* steps, bool query, float starQ,
+                                               float* dir, float* org) {
+  float starRadius = dirichletDist;
+  if (query) {
+    starRadius = starQ;
+    if (prm.min_star_radius <= dirichletDist) starRadius = smax(0.99f * starRadius, prm.min_star_radius);
+  }
+  g.update_ball(st.pt, starRadius);
+  (*steps)++;
+  float u[2];
+  u[0] = smp.nextf();
+  if constexpr (DIM == 3) u[1] = smp.nextf();
+  sample_unit_sphere<DIM>(u, dir);
+  if (st.onNeumann && dotv<DIM>(st.n, dir) > 0.0f)
+    for (int k = 0; k < DIM; k++) dir[k] *= -1.0f;
+  if (st.onNeumann) {
+    float mn[DIM];
+    for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
+    offset_point<DIM>(st.pt, mn, org);
+  } else {
+    for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
+  }
+  return starRadius;
+}
+
+// after the ray query: Neumann term, source sample, move, roulette (walk_on_stars.h:200-327)
+template <int DIM>
+__device__ __forceinline__ int walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
+                                             float& dirichletDist, Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st,
+                                             uint32_t* iters, float starRadius, const float* dir, const float* org,
+                                             bool hit, Hit& ip) {
+  const int np = sc.n_prims;
+  const float* prims = G.prim;
+  if (!hit) {
+    for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
+    ip.d = starRadius;
+  }
+  if (!prm.ignore_neumann) {
+    float rn[3] = {0.0f, 0.0f, 0.0f};
+    for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
+    bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
+    if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
+  }
+  if (!prm.ignore_source) {
+    float pdf, sp[DIM];
+    DIAG_T0(t_smp);
+    sample_volume<DIM>(g, dir, smp, &pdf, sp, iters, false);
+    DIAG_ADD(D_SAMPLE, t_smp);
+    if (g.r <= ip.d) {
+      float contrib = g.norm() * source_value<DIM>(sc, sp);
+      st.totalSource += st.throughput * contrib;
+    }
+  }
+  if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
+  st.prevDist = ip.d;
+  for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
+  st.onNeumann = hit;
+  st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
+  if (st.throughput < prm.rr_threshold) {
+    float survival = st.throughput / prm.rr_threshold;
+    if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
+    st.throughput = prm.rr_threshold;
+  }
+  st.walkLength++;
+  if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
+  if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
+  dirichletDist = dirichlet_dist_lane<DIM>(sc, st.pt);
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
+// First ray hit (intersectWithNeumann, fcpw_scene_loader.h:458-484), wave-cooperative.
+// The sequential scan keeps the LAST primitive accepted with d <= rt (rt shrinking
+// to each accepted d): that is the minimum d, ties to the larger index.  So the
+// (lane, primitive) work spreads over the wave like the silhouette query: lanes
+// mark the primitive groups their ray segment can reach (slab test with the
+// initial tmax), the pairs are compacted, every lane evaluates items with the
+// rcp pre-filter + exact test against tmax, and accepted hits fold into the
+// owner's atomicMin on (d bits with -0 -> +0, ~index).  The owner then reruns
+// the exact test on the winner for the hit record (identical arithmetic).
+// ---------------------------------------------------------------------------
+constexpr int kRayChunk = 16;
+
+template <int DIM>
+struct RayLDS {
+  uint32_t list[kWave * kRayChunk];
+  float qo[DIM][kWave], qd[DIM][kWave];
+  float rt[kWave];
+  unsigned long long best[kWave];
+};
+
+// rcp pre-filter of one primitive against rt (certain rejections only), then the exact test
+template <int DIM>
+__device__ __forceinline__ bool ray_prim_filtered(const float* P, const float* o, const float* dir, float& rt,
+                                                  Hit* h) {
+  if constexpr (DIM == 2) {
+    const float u0 = P[0] - o[0], u1 = P[1] - o[1];
+    const float v0 = P[2], v1 = P[3];
+    const float dv = dir[0] * v1 - dir[1] * v0;
+    if (!(__builtin_fabsf(dv) > kFltEps)) return false;
+    const float ud = u0 * dir[1] - u1 * dir[0];
+    const float uv = u0 * v1 - u1 * v0;
+    const float ra = __builtin_amdgcn_rcpf(dv);
+    const float ta = ud * ra, da = uv * ra;
+    if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
+        (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
+      return false;
+  } else {
+    float v1[3], v2[3], pp[3], sv[3], q[3];
+    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; sv[k] = o[k] - P[k]; }
+    cross3(pp, dir, v2);
+    const float det = dotv<3>(v1, pp);
+    if (!(__builtin_fabsf(det) > kFltEps)) return false;
+    const float ra = __builtin_amdgcn_rcpf(det);
+    const float vn = dotv<3>(sv, pp), va = vn * ra;
+    if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) return false;
+    cross3(q, sv, v1);
+    const float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
+    const float wa = wn * ra, da = dn * ra;
+    if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
+        (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
+      return false;
+  }
+  return ray_prim_exact<DIM>(P, o, dir, rt, h);
+}
+
+// Convergent: every lane of the wave calls it; lanes with active == false get false.
+template <int DIM>
+__device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc, bool active, const float* o,
+                                             const float* dir, float tmax, Hit* h, RayLDS<DIM>* L, int lane) {
+  constexpr int PS = Layout<DIM>::prim;
+  const int np = sc.n_prims, ng = sc.n_pgroups;
+  const bool need = active && np > 0;
+  if (__ballot(need) == 0) return false;
+  float inv[DIM];
+  for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
+  if (need) {
+    for (int k = 0; k < DIM; k++) { L->qo[k][lane] = o[k]; L->qd[k][lane] = dir[k]; }
+    L->rt[lane] = tmax;
+    L->best[lane] = ~0ull;
+  }
+  for (int g0 = 0; g0 < ng; g0 += kRayChunk) {
+    uint32_t mask = 0;
+    if (need) {
+      const int gn = (ng - g0) < kRayChunk ? (ng - g0) : kRayChunk;
+      for (int j = 0; j < gn; j++)
+        if (ray_box_maybe<DIM>(G.pgroup + (g0 + j) * kGroupStride, o, inv, tmax)) mask |= 1u << j;
+    }
+    const uint32_t cnt = (uint32_t)__popc(mask);
+    uint32_t incl = cnt;
+    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
+      const uint32_t v = __shfl_up(incl, dlt);
+      if (lane >= dlt) incl += v;
+    }
+    const uint32_t total = __shfl(incl, kWave - 1);
+    uint32_t pos = incl - cnt;
+    for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
+    wave_sync();
+    const uint32_t items = total * kGroup;
+    for (uint32_t k = lane; k < items; k += kWave) {
+      const uint32_t e = L->list[k / kGroup];
+      const int owner = (int)(e >> 26);
+      const int p = (int)(e & 0x3FFFFFFu) * kGroup + (int)(k % kGroup);
+      if (p >= np) continue;
+      float oo[DIM], dd[DIM];
+      for (int q = 0; q < DIM; q++) { oo[q] = L->qo[q][owner]; dd[q] = L->qd[q][owner]; }
+      float rt = L->rt[owner];
+      Hit hh;
+      if (ray_prim_filtered<DIM>(G.prim + p * PS, oo, dd, rt, &hh))
+        atomicMin(&L->best[owner],
+                  ((unsigned long long)__float_as_uint(hh.d + 0.0f) << 32) | (0xFFFFFFFFu - (uint32_t)p));
+    }
+    wave_sync();
+  }
+  bool found = false;
+  if (need) {
+    const unsigned long long key = L->best[lane];
+    if (key != ~0ull) {
+      const int p = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+      float rt = tmax;
+      found = ray_prim_exact<DIM>(G.prim + p * PS, o, dir, rt, h);
+      if (found) normalize_rcp<DIM>(h->n);
+    }
+  }
+  wave_sync();
+  return found;
+}
+
+// ---------------------------------------------------------------------------
+// computeStarRadius (fcpw_scene_loader.h:621-641), wave-cooperative.
+//
+// The sequential query visits the silhouette candidates in index order, accepts
+// a candidate when it is a silhouette with d^2 <= r2 (r2 = the current best,
+// initially maxR^2), and stops at the first accepted candidate with d^2 <= minR^2.
+// Its result is therefore order-free: the d of the first (lowest-index) accepted
+// candidate with d^2 <= minR^2 if there is one, else the d of the candidate with
+// the minimum d^2, ties to the larger index -- each candidate judged against
+// maxR^2 alone.  So the (lane, candidate) work can be spread over the wave:
+//   1. each querying lane marks the silhouette groups it must visit (padded-box
+//      distance within maxR, normal cone not certainly front/back facing);
+//   2. the (lane, group) pairs are compacted into an LDS list (wave prefix sum);
+//   3. all 64 lanes evaluate the candidate items of the list with the exact
+//      per-candidate test and fold accepted ones into the owner's LDS slots with
+//      atomicMin on (d^2 bits, ~index) and on the index (for the minR break);
+//   4. the owner recomputes d of the winning candidate.
+// The lane-divergent group loops of the sequential form (the wave paid for the
+// union of every lane's groups) become ~(total work)/64 wave iterations.
+// ---------------------------------------------------------------------------
+constexpr int kStarChunk = 16;  // groups per compaction round: at most 64 * 16 list entries
+
+template <int DIM>
+struct StarLDS {
+  uint32_t list[kWave * kStarChunk];
+  float qx[DIM][kWave];
+  float r2[kWave], minR2[kWave];
+  uint32_t flip[kWave];
+  uint32_t brk[kWave];
+  unsigned long long best[kWave];
+};
+
+template <int DIM>
+__host__ __device__ constexpr size_t walk_scratch_bytes() {
+  return ((sizeof(StarLDS<DIM>) > sizeof(RayLDS<DIM>) ? sizeof(StarLDS<DIM>) : sizeof(RayLDS<DIM>)) + 15) & ~size_t(15);
+}
+
+// Exact per-candidate test of the sequential loop against r2 (see star_radius).
+template <int DIM>
+__device__ __forceinline__ bool star_candidate(const LGeom& G, int s, const float* x, float r2, bool flip,
+                                               float prec, float* d2out) {
+  constexpr int SS = Layout<DIM>::sil;
+  const float* S = G.sil + s * SS;
+  const float miss = DIM == 2 ? S[6] : S[12];
+  float view[DIM], d;
+  int cls = 2;
+  if constexpr (DIM == 2) {
+    view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
+    const float d2raw = view[0] * view[0] + view[1] * view[1];
+    if (d2raw > r2 * 1.000001f) return false;  // certain: fl(fl(sqrt(q))^2) >= q(1 - 2^-22)
+    cls = miss != 0.0f ? 1 : silhouette_class2(S, view, d2raw, flip, prec);
+    if (cls == 0) return false;
+    d = __builtin_sqrtf(d2raw);
+  } else {
+    float e[3], hl[3];
+    for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
+    const float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
+    const float lo = dm - hr;
+    if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) return false;
+    float pt[3], t;
+    d = cp_segment<3>(S, S + 3, x, pt, &t);
+    for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
+    if (miss != 0.0f) cls = 1;
+  }
+  const float d2 = d * d;
+  if (!(d2 <= r2)) return false;
+  if (cls != 1 && !is_silhouette<DIM>(S, view, d, flip, prec)) return false;
+  *d2out = d2;
+  return true;
+}
+
+template <int DIM>
+__device__ __forceinline__ float star_candidate_dist(const LGeom& G, int s, const float* x) {
+  constexpr int SS = Layout<DIM>::sil;
+  const float* S = G.sil + s * SS;
+  if constexpr (DIM == 2) {
+    const float v0 = x[0] - S[0], v1 = x[1] - S[1];
+    return __builtin_sqrtf(v0 * v0 + v1 * v1);
+  } else {
+    float pt[3], t;
+    return cp_segment<3>(S, S + 3, x, pt, &t);
+  }
+}
+
+// Convergent: every lane of the wave calls it.  Lanes with query == false get 0.
+template <int DIM>
+__device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene& sc, const DevParams& prm,
+                                                  bool query, const float* x, float maxR, bool flipOrient,
+                                                  StarLDS<DIM>* L, int lane) {
+  const float minR = prm.min_star_radius, prec = prm.silhouette_precision;
+  float result = 0.0f, r2 = 0.0f, minR2 = 0.0f;
+  bool need = false;
+  if (query) {
+    if (minR > maxR) {
+      result = maxR;
+    } else {
+      result = smax(maxR, minR);
+      if (sc.n_prims > 0) {
+        r2 = maxR < kFltMax ? maxR * maxR : kFltMax;
+        minR2 = minR * minR;
+        need = !(minR2 >= r2);
+      }
+    }
+  }
+  if (__ballot(need) == 0) return result;
+  if (need) {
+    for (int k = 0; k < DIM; k++) L->qx[k][lane] = x[k];
+    L->r2[lane] = r2;
+    L->minR2[lane] = minR2;
+    L->flip[lane] = flipOrient ? 0u : 1u;  // computeStarRadius passes !flipNormalOrientation
+    L->brk[lane] = 0xFFFFFFFFu;
+    L->best[lane] = ~0ull;
+  }
+  const int nsg = sc.n_sgroups, ns = sc.n_sil;
+  for (int g0 = 0; g0 < nsg; g0 += kStarChunk) {
+    uint32_t mask = 0;
+    if (need) {
+      const int gn = (nsg - g0) < kStarChunk ? (nsg - g0) : kStarChunk;
+      for (int j = 0; j < gn; j++) {
+        const float* B = G.sgroup + (g0 + j) * kSGroupStride;
+        if (ball_box_maybe<DIM>(B, x, r2) && !cone_culled<DIM>(B, x, prec)) mask |= 1u << j;
+      }
+    }
+    const uint32_t cnt = (uint32_t)__popc(mask);
+    uint32_t incl = cnt;
+    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
+      const uint32_t v = __shfl_up(incl, dlt);
+      if (lane >= dlt) incl += v;
+    }
+    const uint32_t total = __shfl(incl, kWave - 1);
+    uint32_t pos = incl - cnt;
+    for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
+    wave_sync();
+    const uint32_t items = total * kGroup;
+    for (uint32_t k = lane; k < items; k += kWave) {
+      const uint32_t e = L->list[k / kGroup];
+      const int owner = (int)(e >> 26);
+      const int s = (int)(e & 0x3FFFFFFu) * kGroup + (int)(k % kGroup);
+      if (s >= ns) continue;
+      float xo[DIM];
+      for (int q = 0; q < DIM; q++) xo[q] = L->qx[q][owner];
+      float d2;
+      if (star_candidate<DIM>(G, s, xo, L->r2[owner], L->flip[owner] != 0u, prec, &d2)) {
+        atomicMin(&L->best[owner], ((unsigned long long)__float_as_uint(d2) << 32) | (0xFFFFFFFFu - (uint32_t)s));
+        if (d2 <= L->minR2[owner]) atomicMin(&L->brk[owner], (uint32_t)s);
+      }
+    }
+    wave_sync();
+  }
+  if (need) {
+    const uint32_t b = L->brk[lane];
+    const unsigned long long key = L->best[lane];
+    int s = -1;
+    if (b != 0xFFFFFFFFu) s = (int)b;
+    else if (key != ~0ull) s = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+    if (s >= 0) result = smax(star_candidate_dist<DIM>(G, s, x), minR);
+  }
+  wave_sync();
+  return result;
 }
 
 // ---------------------------------------------------------------------------
@@ -1415,12 +1703,16 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
   __shared__ unsigned int s_ctr[C_NUM];
   const int lane = threadIdx.x & (kWave - 1);
   const LGeom G = stage_geometry<DIM>(sc, smem, true);
+  // per-wave scratch shared by the star and ray queries (used one after the other)
+  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + (threadIdx.x / kWave) * walk_scratch_bytes<DIM>();
+  StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
+  RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
+  (void)rayL;
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
-  (void)geom_floats;
 
   const uint32_t T = (uint32_t)tk.T;
   const uint32_t wpp = (uint32_t)tk.wpp;
@@ -1459,37 +1751,56 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
       qn += k < avail ? k : avail;
     }
     if (__ballot(t >= 0) == 0) break;  // queue drained and every lane idle
-    if (t < 0) continue;
 
-    if (fresh) {
+    if (t >= 0 && fresh) {
       const uint32_t pidx = (uint32_t)t / wpp;
       const uint32_t w = ((uint32_t)t - pidx * wpp) / (uint32_t)prm.n_anti;
       if (!(tk.pstate[pidx] & kPtEstimate)) {  // point outside the domain: no walks
         tk.code[t] = 0u;
         t = -1;
-        continue;
+      } else {
+        for (int k = 0; k < DIM; k++) { st.pt[k] = tk.pt[k * tk.T + t]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
+        // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
+        // and every step rewrites them before that can happen
+        st.prevDist = 0.0f;
+        st.throughput = tk.thr[t];
+        st.onNeumann = false;
+        st.walkLength = 0;
+        st.totalNeumann = 0.0f;
+        st.totalSource = tk.tsrc[t];
+        ddist = tk.dd[t];
+        g.init(yuk0, sc.absorption);
+        ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
+        wsteps = 1;  // the first ball
       }
-      for (int k = 0; k < DIM; k++) { st.pt[k] = tk.pt[k * tk.T + t]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
-      // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
-      // and every step rewrites them before that can happen
-      st.prevDist = 0.0f;
-      st.throughput = tk.thr[t];
-      st.onNeumann = false;
-      st.walkLength = 0;
-      st.totalNeumann = 0.0f;
-      st.totalSource = tk.tsrc[t];
-      ddist = tk.dd[t];
-      g.init(yuk0, sc.absorption);
-      ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
-      wsteps = 1;  // the first ball
     }
 
     DIAG_COUNT(D_ITERS, 1);
-    DIAG_COUNT(D_LANES, __popcll(__ballot(1)));
+    DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
     DIAG_T0(t_step);
-    const int code = walk_step<DIM>(sc, prm, G, ddist, ws, g, st, &wsteps, &c_iters);
+    int code = -1;
+    bool flip = false, query = false;
+    if (t >= 0) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query);
+    DIAG_T0(t_star);
+    const float starQ = star_radius_wave<DIM>(G, sc, prm, t >= 0 && code < 0 && query, st.pt, ddist, flip,
+                                              starL, lane);
+    DIAG_ADD(D_STAR, t_star);
+    const bool live = t >= 0 && code < 0;
+    float dir[DIM], org[DIM], starR = 0.0f;
+    for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
+    if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org);
+    Hit ip;
+    DIAG_T0(t_ray);
+#if WOS_RAY_WAVE
+    const bool hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM>(G, sc, live, org, dir, starR, &ip, rayL, lane);
+#else
+    const bool hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 &&
+                     ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
+#endif
+    DIAG_ADD(D_RAY, t_ray);
+    if (live) code = walk_step_end<DIM>(sc, prm, G, ddist, ws, g, st, &c_iters, starR, dir, org, hit, ip);
     DIAG_ADD(D_STEP, t_step);
-    if (code >= 0) {
+    if (t >= 0 && code >= 0) {
       const bool recorded = code == WC_DIRICHLET || code == WC_RR;
       if (recorded) {
         const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
@@ -1680,6 +1991,8 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
     hipLaunchKernelGGL(wos_fold_kernel<3>, dim3(grid), dim3(kFoldPoints), 0, s, prm, tk, n, p, g, nest, steps);
   return hipGetLastError();
 }
+
+size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
 hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks) {
   if (which == 0)

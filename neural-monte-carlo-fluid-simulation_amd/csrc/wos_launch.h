@@ -19,6 +19,8 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
                         int geom_floats, hipStream_t s);
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s);
+// per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
+size_t walk_wave_lds_bytes(int dim);
 // which: 0 first-ball kernel, 1 walk kernel
 hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics

@@ -181,3 +181,39 @@ def cube_config(res=128, n_walks=64, src_res=82):
     solver = dict(SOLVER_BASE, nWalks=n_walks)
     return {"name": f"cube3d_{res}", "dim": 3, "scene": dict(SCENE_BASE, boundary=CUBE_OBJ), "solver": solver,
             "output": dict(OUTPUT_BASE, gridRes=100), "source": src, "points": pts, "obj": CUBE_OBJ}
+
+
+def gear_config(n_teeth=160, n_walks=64, res=24, holes=3, seed=7):
+    """Stress scene for the culling / compaction paths (no reference analogue):
+    fluid inside a counter-clockwise gear (2*n_teeth segments alternating between
+    radii 1.0 and 0.93 -> n_teeth reflex silhouette vertices) around `holes`
+    clockwise polygonal obstacles.  With the defaults there are >128 silhouette
+    candidates and >128 segments, i.e. more than one 16-group compaction chunk."""
+    t = np.arange(2 * n_teeth) / (2 * n_teeth) * 2 * np.pi
+    r = np.where(np.arange(2 * n_teeth) % 2 == 0, 1.0, 0.93)
+    v = [np.stack([r * np.cos(t), r * np.sin(t)], -1).astype(np.float32)]
+    ix = [np.stack([np.arange(2 * n_teeth), (np.arange(2 * n_teeth) + 1) % (2 * n_teeth)], -1).astype(np.int32)]
+    base = 2 * n_teeth
+    centres = [(0.35 * np.cos(a), 0.35 * np.sin(a)) for a in np.arange(holes) / max(1, holes) * 2 * np.pi + 0.3]
+    for c in centres:
+        hv, hix = circle_2d(c, 0.12, n=24, clockwise=True)
+        v.append(hv)
+        ix.append(hix + base)
+        base += hv.shape[0]
+    v = np.concatenate(v)
+    ix = np.concatenate(ix)
+    size = (np.array([-1.0, -1.0], np.float32) - 1e-3, np.array([1.0, 1.0], np.float32) + 1e-3)
+    gy = np.linspace(size[0][1], size[1][1], 203)
+    gx = np.linspace(size[0][0], size[1][0], 203)
+    X, Y = np.meshgrid(gx, gy, indexing="xy")
+    src = (np.sin(3 * X) * np.cos(2 * Y) + 0.5 * np.cos(5 * X + 1)).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    ang = rng.uniform(0, 2 * np.pi, res * res)
+    rad = 0.95 * np.sqrt(rng.uniform(0, 1, res * res))
+    pts = np.stack([rad * np.cos(ang), rad * np.sin(ang)], -1).astype(np.float32)
+    for c in centres:  # drop points inside the obstacles
+        pts = pts[np.linalg.norm(pts - np.asarray(c, np.float32), axis=1) > 0.125]
+    solver = dict(SOLVER_BASE, nWalks=n_walks)
+    return {"name": "gear2d", "dim": 2, "vertices": v, "prims": ix, "source": src, "points": pts,
+            "solver": solver, "output": dict(OUTPUT_BASE), "absorption": 350.0}
+

@@ -156,6 +156,17 @@ def test_dirichlet_obstacle_bit_exact(gpu, oracle):
     _compare(oracle, osc, sc, cfg, cfg["points"])
 
 
+def test_gear_many_groups_bit_exact(gpu, oracle):
+    """>16 silhouette groups and >16 segment groups: the multi-chunk compaction
+    rounds of the wave-cooperative star-radius and ray queries."""
+    cfg = workloads.gear_config()
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+    info = sc.info()
+    assert info["n_silhouettes"] > 8 * 16 and info["n_prims"] > 8 * 16, info
+    _compare(oracle, osc, sc, cfg, cfg["points"])
+
+
 def test_cube3d_bit_exact(gpu, oracle):
     cfg = workloads.cube_config(res=10, n_walks=64)
     osc, sc = _pair(cfg, oracle, dim=3)

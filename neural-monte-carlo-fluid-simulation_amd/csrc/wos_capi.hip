@@ -285,7 +285,8 @@ static wos::DevTasks task_view(wos_scene* s, int dim, int64_t T, int32_t wpp) {
 // state_k = A_k * state_0 + C_k for the PCG32 LCG (multiplier kPcgMult, increment kPcgInc)
 static int ensure_jump(wos_scene* s, int k_needed) {
   if (k_needed <= s->n_jump) return WOS_OK;
-  const int cap = std::max(k_needed, 1024);
+  // >= 2 * 1000 + 2: the wave-cooperative rejection sampler jumps up to 1000 iterations ahead
+  const int cap = std::max(k_needed, 4096);
   std::vector<uint64_t> t(2 * (size_t)cap);
   uint64_t A = 1u, Cc = 0u;
   for (int k = 0; k < cap; k++) {

@@ -941,6 +941,154 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
 }
 
 // ---------------------------------------------------------------------------
+// Wave-cooperative rejection sampling (rejectionSampleGreensFn, distributions.h:
+// 362-383) for the 2D Yukawa fast path.  Iteration j of a lane's loop consumes
+// draws 2j and 2j+1 of its PCG32 stream, and state_k = A_k * state_0 + C_k (the
+// jump table), so the iterations of all lanes can be evaluated in any order by
+// any lane.  Each generation gives every unfinished lane a block of B = 64 /
+// (#unfinished) consecutive iterations spread over the wave; the owner then scans
+// its block in order -- the first certain accept wins, an undecided iteration is
+// decided by the owner with the exact double-precision test -- exactly the
+// sequential loop's decisions, so the accepted radius, the iteration count and
+// the stream position after the loop are the sequential ones.  This removes the
+// geometric tail (the wave paid for the longest loop of its lanes).  Lanes off
+// the fast path (3D, harmonic, mu*R >= 80) run the sequential loop.
+// ---------------------------------------------------------------------------
+constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
+
+// PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
+__device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
+  const uint64_t A = prm.jump[2 * k], Cc = prm.jump[2 * k + 1];
+  return A * s0 + Cc;
+}
+
+
+struct RejLDS {
+  unsigned long long s0[kWave];
+  float R[kWave], sqrtL[kWave], rho[kWave], invNB[kWave];
+  uint32_t base[kWave], acc[kWave], und[kWave];
+  uint32_t owner_of[kWave];
+};
+
+__device__ __forceinline__ float draw_float(uint64_t state) {
+  return bits_to_float((pcg_output(state) >> 9) | 0x3f800000u) - 1.0f;
+}
+
+// the two draws of rejection iteration j from stream start s0
+__device__ __forceinline__ void rej_draws(const DevParams& prm, uint64_t s0, int j, float* u, float* x) {
+  const uint64_t st = jump_state(prm, s0, 2 * j);
+  *u = draw_float(st);
+  *x = draw_float(st * kPcgMult + kPcgInc);
+}
+
+// fast decision of one iteration: 1 accept, 0 reject, -1 undecided (see sample_volume)
+__device__ __forceinline__ int rej_fast_decide(float u, float r, float sqrtL, float rho, float invNB) {
+  const float mur = r * sqrtL;
+  const float k0 = k0_fast(mur), ip = i0_fast(mur) * rho;
+  const float c = r * invNB;
+  const float Tf = (k0 - ip) * c;
+  const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
+  return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
+}
+
+// Convergent: every lane calls it.  Inactive lanes do nothing.
+template <int DIM>
+__device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM>& g, const float* dir,
+                                                   Pcg32& s, float* pdf, float* out, uint32_t* iters,
+                                                   bool need_pdf, RejLDS* L, int lane) {
+  bool coop = false;
+  float bound = 0.0f, nrm = 1.0f;
+  if (active && DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ && !WOS_ABL_ONE_REJ) {
+    const float R = g.R, lam = g.lambda, sl = g.sqrtLambda;
+    const float a = 2.2f, b = 0.6f;
+    bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
+                     : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
+    nrm = g.norm();
+    coop = true;
+  }
+  if (__ballot(coop) != 0) {
+    const uint64_t s0 = s.state;
+    if (coop) {
+      L->s0[lane] = s0;
+      L->R[lane] = g.R;
+      L->sqrtL[lane] = g.sqrtLambda;
+      L->rho[lane] = g.A0 / g.A1;
+      L->invNB[lane] = 1.0f / (nrm * bound);
+    }
+    int j0 = 0, jacc = -1;
+    bool done = !coop;
+    for (;;) {
+      const uint64_t pend = __ballot(!done);
+      if (pend == 0) break;
+      const int nact = __popcll(pend);
+      const int B = nact >= kWave ? 1 : (kWave / nact > 32 ? 32 : kWave / nact);
+      if (!done) {
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
+        L->owner_of[rank] = (uint32_t)lane;
+        L->base[lane] = (uint32_t)j0;
+        L->acc[lane] = 0u;
+        L->und[lane] = 0u;
+      }
+      wave_sync();
+      {
+        const int orank = lane / B, b = lane - orank * B;
+        if (orank < nact) {
+          const int owner = (int)L->owner_of[orank];
+          const int j = (int)L->base[owner] + b;
+          if (j < kRejMax) {
+            float u, x;
+            rej_draws(prm, L->s0[owner], j, &u, &x);
+            const int dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->rho[owner], L->invNB[owner]);
+            if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
+            else if (dcs < 0) atomicOr(&L->und[owner], 1u << b);
+          }
+        }
+      }
+      wave_sync();
+      if (!done) {
+        const uint32_t acc = L->acc[lane], und = L->und[lane];
+        int b = 0;
+        while (!done && b < B) {
+          if (j0 + b >= kRejMax) { jacc = kRejMax - 1; done = true; break; }  // limit: last radius kept
+          const uint32_t m = (acc | und) >> b;
+          if (m == 0u) { b = B; break; }
+          b += __builtin_ctz(m);
+          if (b >= B) break;
+          if (j0 + b >= kRejMax) { jacc = kRejMax - 1; done = true; break; }
+          if ((acc >> b) & 1u) { jacc = j0 + b; done = true; break; }
+          // undecided: the exact test of sample_volume, by the owner
+          float u, x;
+          rej_draws(prm, s0, j0 + b, &u, &x);
+          g.r = x * g.R;
+          const float p = g.evaluate() / nrm;
+          const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
+          if (u < pdfRadius / bound) { jacc = j0 + b; done = true; break; }
+          b++;
+        }
+        if (!done) {
+          j0 += B;
+          if (j0 >= kRejMax) { jacc = kRejMax - 1; done = true; }
+        }
+      }
+      wave_sync();
+    }
+    if (coop) {
+      float u, x;
+      rej_draws(prm, s0, jacc, &u, &x);
+      g.r = x * g.R;
+      s.state = jump_state(prm, s0, 2 * jacc + 2);
+      *iters += (uint32_t)(jacc + 1);
+      if (need_pdf) *pdf = g.evaluate() / nrm;
+      g.r = smax(Gfn<DIM>::rClamp, g.r);
+      if (g.r > g.R) g.r = g.R / 2.0f;
+      for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
+    }
+  }
+  if (active && !coop) sample_volume<DIM>(g, dir, s, pdf, out, iters, need_pdf);
+}
+
+// ---------------------------------------------------------------------------
 // walk (walk_on_stars.h:135-329)
 // ---------------------------------------------------------------------------
 template <int DIM>
@@ -1088,12 +1236,12 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
   return starRadius;
 }
 
-// after the ray query: Neumann term, source sample, move, roulette (walk_on_stars.h:200-327)
+// after the ray query: the miss point and the Neumann term (walk_on_stars.h:200-260);
+// the source sample (convergent, sample_volume_wave) and walk_step_tail follow
 template <int DIM>
-__device__ __forceinline__ int walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
-                                             float& dirichletDist, Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st,
-                                             uint32_t* iters, float starRadius, const float* dir, const float* org,
-                                             bool hit, Hit& ip) {
+__device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
+                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, float starRadius,
+                                              const float* dir, const float* org, bool hit, Hit& ip) {
   const int np = sc.n_prims;
   const float* prims = G.prim;
   if (!hit) {
@@ -1106,11 +1254,14 @@ __device__ __forceinline__ int walk_step_end(const DevScene& sc, const DevParams
     bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
     if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
   }
+}
+
+// after the source sample (walk_on_stars.h:270-327)
+template <int DIM>
+__device__ __forceinline__ int walk_step_tail(const DevScene& sc, const DevParams& prm, float& dirichletDist,
+                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, const float* dir,
+                                              bool hit, const Hit& ip, const float* sp) {
   if (!prm.ignore_source) {
-    float pdf, sp[DIM];
-    DIAG_T0(t_smp);
-    sample_volume<DIM>(g, dir, smp, &pdf, sp, iters, false);
-    DIAG_ADD(D_SAMPLE, t_smp);
     if (g.r <= ip.d) {
       float contrib = g.norm() * source_value<DIM>(sc, sp);
       st.totalSource += st.throughput * contrib;
@@ -1285,7 +1436,8 @@ struct StarLDS {
 
 template <int DIM>
 __host__ __device__ constexpr size_t walk_scratch_bytes() {
-  return ((sizeof(StarLDS<DIM>) > sizeof(RayLDS<DIM>) ? sizeof(StarLDS<DIM>) : sizeof(RayLDS<DIM>)) + 15) & ~size_t(15);
+  constexpr size_t a = sizeof(StarLDS<DIM>), b = sizeof(RayLDS<DIM>), c = sizeof(RejLDS);
+  return ((a > b ? (a > c ? a : c) : (b > c ? b : c)) + 15) & ~size_t(15);
 }
 
 // Exact per-candidate test of the sequential loop against r2 (see star_radius).
@@ -1436,10 +1588,6 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
 // the shuffle's bounded draws follow in order (k = n*sd + i*n + j) unless one of
 // them hits PCG's rejection threshold, in which case lane 0 replays the shuffle
 // draws sequentially from the true stream.
-__device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
-  const uint64_t A = prm.jump[2 * k], Cc = prm.jump[2 * k + 1];
-  return A * s0 + Cc;
-}
 
 template <int DIM>
 __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner, int lane) {
@@ -1707,6 +1855,7 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
   char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + (threadIdx.x / kWave) * walk_scratch_bytes<DIM>();
   StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
   RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
+  RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
   (void)rayL;
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
 #if WOS_DIAG
@@ -1798,7 +1947,14 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
                      ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
 #endif
     DIAG_ADD(D_RAY, t_ray);
-    if (live) code = walk_step_end<DIM>(sc, prm, G, ddist, ws, g, st, &c_iters, starR, dir, org, hit, ip);
+    if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
+    float sp[DIM], pdf_unused;
+    for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
+    DIAG_T0(t_smp);
+    if (!prm.ignore_source)
+      sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, &c_iters, false, rejL, lane);
+    DIAG_ADD(D_SAMPLE, t_smp);
+    if (live) code = walk_step_tail<DIM>(sc, prm, ddist, ws, g, st, dir, hit, ip, sp);
     DIAG_ADD(D_STEP, t_step);
     if (t >= 0 && code >= 0) {
       const bool recorded = code == WC_DIRICHLET || code == WC_RR;

@@ -1646,11 +1646,14 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
   Pcg32 fs;
   fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
+  // the first ball (centre x, radius firstR) is the same for both members: its
+  // Bessel constants are evaluated once (identical values either way)
+  Gfn<DIM> g0;
+  g0.init(yuk0, sc.absorption);
+  g0.update_ball(x, firstR);
   for (int a = 0; a < prm.n_anti; a++) {
     const int64_t t = t0 + a;
-    Gfn<DIM> g;
-    g.init(yuk0, sc.absorption);
-    g.update_ball(x, firstR);
+    Gfn<DIM> g = g0;
     float throughput = 1.0f, totalSource = 0.0f, firstSource = 0.0f;
     float sdir[DIM], bdir[DIM];
     for (int k = 0; k < DIM; k++) sdir[k] = 0.0f;

@@ -13,10 +13,16 @@
 //     (walk_on_stars.h:498,639).
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define WOS_HD __host__ __device__ __forceinline__
+#else
+// plain host C++ (g++): the scene preparation is also built this way by the CPU
+// test suite (tests/test_host_scene.py), which checks the culling records
+#define WOS_HD inline
+#endif
 
 namespace wos {
 

@@ -1,0 +1,162 @@
+"""CPU checks of the culling records the kernels rely on for exactness
+(csrc/wos_host_scene.cpp, built here with plain g++ through tests/native/host_scene_shim.cpp):
+
+* every primitive / silhouette candidate lies inside its group's padded box;
+* every adjacent normal of a group lies inside the group's normal cone, every
+  candidate inside its bounding sphere;
+* soundness of the cone test (wos_kernel.hip cone_culled): for random query points,
+  a group the test culls never holds a candidate the exact silhouette test
+  (isWideSilhouetteVertex, wide_query_operations.h:328-358) accepts.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import objparse
+from wos_amd import workloads
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "neural-monte-carlo-fluid-simulation_amd", "csrc")
+KGROUP = 8
+
+
+@pytest.fixture(scope="module")
+def shim(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("hs") / "libhs.so")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-fPIC", "-shared", "-ffp-contract=off", "-I", CSRC,
+                    os.path.join(HERE, "native", "host_scene_shim.cpp"), os.path.join(CSRC, "wos_host_scene.cpp"),
+                    "-o", out], check=True)
+    return C.CDLL(out)
+
+
+def prepare(shim, v, ix, dim, double_sided=False):
+    v = np.ascontiguousarray(v, np.float32)
+    ix = np.ascontiguousarray(ix, np.int32)
+    cap = 64 * (ix.shape[0] + 16) * 4
+    bufs = [np.zeros(cap, np.float32) for _ in range(4)]
+    counts = np.zeros(4, np.int32)
+    f = C.POINTER(C.c_float)
+    rc = shim.hs_prepare(dim, v.ctypes.data_as(f), v.shape[0], ix.ctypes.data_as(C.POINTER(C.c_int)), ix.shape[0],
+                         int(double_sided), *[x for b in bufs for x in (b.ctypes.data_as(f), cap)],
+                         counts.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc == 0, rc
+    npr, nsil, npg, nsg = counts.tolist()
+    ps, ss = (4, 8) if dim == 2 else (9, 16)
+    return dict(prim=bufs[0][:npr * ps].reshape(npr, ps), sil=bufs[1][:nsil * ss].reshape(nsil, ss),
+                pg=bufs[2][:npg * 8].reshape(npg, 8), sg=bufs[3][:nsg * 16].reshape(nsg, 16))
+
+
+def scenes():
+    out = []
+    cfg = workloads.karman_config(n_walks=8)
+    out.append(("karman", 2) + objparse.load(cfg["obj"], 2))
+    g = workloads.gear_config()
+    out.append(("gear", 2, g["vertices"], g["prims"]))
+    c = workloads.cube_config(res=2, n_walks=8)
+    v, ix = objparse.load(c["obj"], 3)
+    out.append(("cube", 3, v, ix))
+    out.append(("open_box", 3, v, ix[2:]))  # two faces' triangles removed: open edges -> silhouettes
+    return out
+
+
+@pytest.mark.parametrize("name,dim,v,ix", scenes(), ids=[s[0] for s in scenes()])
+def test_group_boxes_contain_members(shim, name, dim, v, ix):
+    r = prepare(shim, v, ix, dim)
+    prim, sil, pg, sg = r["prim"], r["sil"], r["pg"], r["sg"]
+    assert pg.shape[0] == (prim.shape[0] + KGROUP - 1) // KGROUP
+    for p in range(prim.shape[0]):
+        B = pg[p // KGROUP]
+        if dim == 2:
+            pts = [prim[p, 0:2], prim[p, 0:2] + prim[p, 2:4]]  # record holds [pa, pb - pa]
+        else:
+            pts = [prim[p, 0:3], prim[p, 3:6], prim[p, 6:9]]
+        for q in pts:
+            assert np.all(q >= B[0:dim]) and np.all(q <= B[4:4 + dim]), (name, p)
+    for s in range(sil.shape[0]):
+        B = sg[s // KGROUP]
+        pts = [sil[s, 0:2]] if dim == 2 else [sil[s, 0:3], sil[s, 3:6]]
+        for q in pts:
+            assert np.all(q >= B[0:dim]) and np.all(q <= B[4:4 + dim])
+            assert np.linalg.norm(q.astype(np.float64) - B[8:8 + dim]) <= B[11]
+
+
+@pytest.mark.parametrize("name,dim,v,ix", scenes(), ids=[s[0] for s in scenes()])
+def test_normal_cones_contain_normals(shim, name, dim, v, ix):
+    r = prepare(shim, v, ix, dim)
+    sil, sg = r["sil"], r["sg"]
+    o0, o1, om = (2, 4, 6) if dim == 2 else (6, 9, 12)
+    for gi in range(sg.shape[0]):
+        B = sg[gi]
+        members = sil[gi * KGROUP:(gi + 1) * KGROUP]
+        if np.any(members[:, om] != 0):
+            assert B[15] != 0  # a candidate next to a missing primitive disables culling
+        if B[15] != 0:
+            continue
+        alpha = np.arctan2(B[3], B[7])
+        for S in members:
+            for o in (o0, o1):
+                n = S[o:o + dim].astype(np.float64)
+                ang = np.arccos(np.clip(n @ B[12:12 + dim] / np.linalg.norm(n), -1, 1))
+                assert ang <= alpha + 1e-6
+
+
+def cone_culled(B, x, prec, dim):
+    """numpy float64 restatement of wos_kernel.hip cone_culled"""
+    if B[15] != 0:
+        return False
+    rho = B[11]
+    w = x - B[8:8 + dim]
+    D2 = w @ w
+    lim = rho + 1.01 * prec + 1e-6
+    if not D2 > lim * lim:
+        return False
+    invD = 1 / np.sqrt(D2)
+    sinb = rho * invD
+    cosb = np.sqrt(max(0.0, 1 - sinb * sinb))
+    sina, cosa = B[3], B[7]
+    cosg, sing = cosa * cosb - sina * sinb, sina * cosb + cosa * sinb
+    cost = np.clip((w @ B[12:12 + dim]) * invD, -1, 1)
+    sint = np.sqrt(max(0.0, 1 - cost * cost))
+    thr = prec + 1e-3
+    if sint * cosg + cost * sing > 1e-3 and cost * cosg - sint * sing > thr:
+        return True
+    return sint * cosg - cost * sing > 1e-3 and cost * cosg + sint * sing < -thr
+
+
+def silhouette_2d(S, x, prec, flip=True):
+    """isWideSilhouetteVertex (float64 evaluation of the kernel's is_silhouette<2>)"""
+    sign = 1.0 if flip else -1.0
+    view = x - S[0:2]
+    d = np.linalg.norm(view)
+    n0, n1 = S[2:4].astype(np.float64), S[4:6].astype(np.float64)
+    if not d > prec:
+        return sign * (n0[0] * n1[1] - n0[1] * n1[0]) > prec
+    u = view / d
+    d0, d1 = u @ n0, u @ n1
+    if abs(d0) <= prec:
+        return sign * d1 > prec
+    if abs(d1) <= prec:
+        return sign * d0 > prec
+    return d0 * d1 < 0
+
+
+@pytest.mark.parametrize("name", ["karman", "gear"])
+def test_cone_culling_is_sound(shim, name):
+    s = [t for t in scenes() if t[0] == name][0]
+    r = prepare(shim, s[2], s[3], 2)
+    sil, sg = r["sil"], r["sg"]
+    lo, hi = s[2].min(0) - 0.2, s[2].max(0) + 0.2
+    rng = np.random.default_rng(3)
+    culled = 0
+    for x in rng.uniform(lo, hi, (3000, 2)):
+        for gi in range(sg.shape[0]):
+            if not cone_culled(sg[gi].astype(np.float64), x, 1e-3, 2):
+                continue
+            culled += 1
+            for S in sil[gi * KGROUP:(gi + 1) * KGROUP]:
+                for flip in (True, False):
+                    assert not (S[6] != 0 or silhouette_2d(S, x, 1e-3, flip)), (name, gi, x)
+    assert culled > 1000  # the test culls a real share of the groups

@@ -62,7 +62,7 @@ struct wos_scene {
   int n_jump = 0;
   float* d_tasks = nullptr;      // walk-task workspace (DevTasks arrays), grow-only
   int64_t task_cap = 0;          // tasks
-  int32_t* d_pstate = nullptr;   // per-point state of one batch
+  int32_t* d_pstate = nullptr;   // per-point state + queue permutation of one batch, then bucket counters
   int64_t pstate_cap = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -257,7 +257,7 @@ static int ensure_tasks(wos_scene* s, int64_t tasks, int64_t points) {
   if (points > s->pstate_cap) {
     hipFree(s->d_pstate);
     s->d_pstate = nullptr; s->pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&s->d_pstate, (size_t)points * sizeof(int32_t)));
+    HIP_TRY(hipMalloc((void**)&s->d_pstate, ((size_t)2 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
     s->pstate_cap = points;
   }
   return WOS_OK;
@@ -277,6 +277,8 @@ static wos::DevTasks task_view(wos_scene* s, int dim, int64_t T, int32_t wpp) {
   tk.total = f; f += T;
   tk.code = (uint32_t*)f;
   tk.pstate = s->d_pstate;
+  tk.perm = (uint32_t*)(s->d_pstate + s->pstate_cap);
+  tk.hist = (uint32_t*)(s->d_pstate + 2 * s->pstate_cap);
   tk.T = T;
   tk.wpp = wpp;
   return tk;
@@ -408,9 +410,11 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     const int64_t bbase = index_base + b0 * index_stride;
     if (b0 > 0)
       HIP_TRY(hipMemsetAsync(s->d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), st));
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, s->d_counters,
                                     q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, st));
+    HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(hipEventRecord(ev[1], st));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
     HIP_TRY(wos::launch_walks(dim, s->dev, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,

@@ -1783,9 +1783,11 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
     int lhs_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ uint32_t s_hist[kCostBuckets];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   stage_geometry<DIM>(sc, smem, false);
+  if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
   __syncthreads();
   const float* Lprim = smem;
   float* strat = smem + geom_floats + wave * 2 * lhs_floats;
@@ -1828,7 +1830,17 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
       const float mask = prm.boundary_distance_mask;
       const bool maskP = __builtin_fabsf(nDist) < mask;
       const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
-      tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0);
+      // cost bucket for the walk-queue order: walks from points close to the boundary
+      // (small first ball) run longest, so they are queued first (longest-first
+      // scheduling shortens the tail of the persistent walk kernel)
+      const float bd = smin(dDist, nDist);
+      int bucket = 0;
+      if (estimate) {
+        const float l2 = __builtin_amdgcn_logf(smax(bd, 1e-9f));  // log2
+        bucket = (int)sclamp((int)(-2.0f * l2) + 8, 1, kCostBuckets - 1);
+      }
+      tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
+      atomicAdd(&s_hist[bucket], 1u);
     }
     if (!estimate) continue;
     c_pts += lane == 0;
@@ -1841,6 +1853,37 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
+  __syncthreads();
+  if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
+}
+
+// ---- walk-queue order: bucket offsets (descending cost) and the permutation ---
+__global__ void wos_lpt_offsets_kernel(uint32_t* __restrict__ hist) {
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int b = kCostBuckets - 1; b >= 0; b--) { hist[kCostBuckets + b] = acc; acc += hist[b]; }
+  }
+}
+
+// block-aggregated: LDS bucket counts, one global range reservation per bucket per
+// block, then LDS-local placement (the global offsets see kCostBuckets atomics per
+// block instead of one per point)
+__global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk, int64_t n) {
+  __shared__ uint32_t cnt[kCostBuckets], base[kCostBuckets];
+  if (threadIdx.x < kCostBuckets) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int b = 0;
+  uint32_t local = 0;
+  if (i < n) {
+    b = (tk.pstate[i] >> 8) & (kCostBuckets - 1);
+    local = atomicAdd(&cnt[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kCostBuckets && cnt[threadIdx.x])
+    base[threadIdx.x] = atomicAdd(&tk.hist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (i < n) tk.perm[base[b] + local] = (uint32_t)i;
 }
 
 // ---- kernel 2: walks ---------------------------------------------------------
@@ -1899,7 +1942,11 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       const uint32_t k = (uint32_t)__popcll(need);
       const uint32_t avail = qe - qn;
-      if (t < 0 && rank < avail) { t = qn + rank; fresh = true; }
+      if (t < 0 && rank < avail) {
+        const uint32_t q = qn + rank, qp = q / wpp;
+        t = (int64_t)tk.perm[qp] * wpp + (q - qp * wpp);  // queue position -> task of the permuted point
+        fresh = true;
+      }
       qn += k < avail ? k : avail;
     }
     if (__ballot(t >= 0) == 0) break;  // queue drained and every lane idle
@@ -2125,6 +2172,13 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
   else
     hipLaunchKernelGGL(wos_first_ball_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride,
                        tk, counters, work, geom_floats, lhs_floats);
+  return hipGetLastError();
+}
+
+hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(wos_lpt_offsets_kernel, dim3(1), dim3(64), 0, s, tk.hist);
+  const int grid = (int)((n + 255) / 256);
+  if (grid > 0) hipLaunchKernelGGL(wos_lpt_scatter_kernel, dim3(grid), dim3(256), 0, s, tk, n);
   return hipGetLastError();
 }
 

@@ -14,6 +14,8 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                               unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
                               hipStream_t s);
+// bucket offsets + point permutation for the walk queue (after the first-ball kernel)
+hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s);
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                         int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
                         int geom_floats, hipStream_t s);

@@ -97,11 +97,14 @@ struct DevTasks {
   float* sdir;      // [DIM][T] record: source gradient direction
   float* total;     // [T] record: walk total
   uint32_t* code;   // [T] record: (steps << 1) | recorded
-  int32_t* pstate;  // [n] bit0 estimated, bit1 mask p, bit2 mask grad p
+  int32_t* pstate;  // [n] bit0 estimated, bit1 mask p, bit2 mask grad p, bits 8..12 cost bucket
+  uint32_t* perm;   // [n] walk-queue order of the points (longest expected walks first)
+  uint32_t* hist;   // [2 * kCostBuckets] bucket counts, then running bucket offsets
   int64_t T;
   int32_t wpp;      // walks per point = n_pairs * n_anti
 };
 
 constexpr int task_floats(int dim) { return 3 * dim + 6; }
+constexpr int kCostBuckets = 32;
 
 }  // namespace wos

@@ -1,0 +1,71 @@
+"""Times the HIP path on every SURVEY §8 configuration that fits one GPU (the bench
+line is config B only): kernel-split times, walk steps, throughput.  GPU box only.
+    python3 tools/time_configs.py [names...]     (default: all)
+"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "neural-monte-carlo-fluid-simulation_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import objparse  # noqa: E402
+from wos_amd import WosScene, solver_params, workloads  # noqa: E402
+
+
+def scene_for(name):
+    if name == "B_karman64k":
+        cfg = workloads.karman_config(n_walks=128)
+        v, ix = objparse.load(cfg["obj"], 2)
+        return cfg, WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    if name == "B_karman_grid32k":
+        cfg = workloads.karman_config(n_walks=128, grid_points=True)
+        v, ix = objparse.load(cfg["obj"], 2)
+        return cfg, WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    if name == "C_dirichlet512":
+        cfg = workloads.dirichlet_obstacle_config(n_walks=256, res=512)
+        return cfg, WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"],
+                             dvertices=cfg["dvertices"], dprims=cfg["dprims"], dirichlet_value=1.0, watertight=True)
+    if name.startswith("D_cube"):
+        res = int(name.split("_cube")[1])
+        cfg = workloads.cube_config(res=res, n_walks=64)
+        v, ix = objparse.load(cfg["obj"], 3)
+        return cfg, WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    if name == "gear":
+        cfg = workloads.gear_config(res=256)
+        return cfg, WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+    raise KeyError(name)
+
+
+def main():
+    names = sys.argv[1:] or ["B_karman64k", "B_karman_grid32k", "C_dirichlet512", "D_cube64", "D_cube128", "gear"]
+    dev = torch.device("cuda", 0)
+    for name in names:
+        cfg, sc = scene_for(name)
+        x = torch.from_numpy(np.ascontiguousarray(cfg["points"])).to(dev)
+        prm = solver_params(cfg["solver"], cfg["output"])
+        sc.solve(x, prm)
+        res = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            p, g, st = sc.solve(x, prm)
+            torch.cuda.synchronize()
+            res.append((time.perf_counter() - t0, st))
+        wall, st = sorted(res, key=lambda r: r[0])[1]
+        steps = st["walk_steps"] + st["wasted_steps"]
+        print(json.dumps({"config": name, "points": int(x.shape[0]), "walks": cfg["solver"]["nWalks"],
+                          "wall_ms": wall * 1e3, "kernel_ms": st["kernel_ms"], "first_ball_ms": st["first_ball_ms"],
+                          "walk_ms": st["walk_ms"], "fold_ms": st["fold_ms"], "walk_steps": st["walk_steps"],
+                          "wasted_steps": st["wasted_steps"], "steps_per_s": st["walk_steps"] / (st["kernel_ms"] * 1e-3),
+                          "rejection_iters": st["rejection_iters"],
+                          "finite": bool(torch.isfinite(p).all().item() and torch.isfinite(g).all().item())}),
+              flush=True)
+        sc.close()
+
+
+if __name__ == "__main__":
+    main()

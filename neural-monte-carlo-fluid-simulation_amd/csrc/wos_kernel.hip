@@ -965,7 +965,9 @@ __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0
 
 struct RejLDS {
   unsigned long long s0[kWave];
-  float R[kWave], sqrtL[kWave], rho[kWave], invNB[kWave];
+  float R[kWave], sqrtL[kWave];
+  float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
+  float nrm[kWave], bound[kWave];
   uint32_t base[kWave], acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
 };
@@ -991,16 +993,35 @@ __device__ __forceinline__ int rej_fast_decide(float u, float r, float sqrtL, fl
   return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
 }
 
-// Convergent: every lane calls it.  Inactive lanes do nothing.
+// exact 3D Yukawa test of one iteration with an owner's ball constants: the same
+// Gfn::evaluate / pdf arithmetic as sample_volume, hence the same decision
+__device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, float sqrtL, float A0, float A1, float nrm,
+                                                 float bound) {
+  Gfn<3> h;
+  h.yukawa = true;
+  h.sqrtLambda = sqrtL;
+  h.A0 = A0;
+  h.A1 = A1;
+  h.R = R;
+  h.r = r;
+  const float p = h.evaluate() / nrm;
+  const float pdfRadius = p / pdf_sphere_uniform<3>(r);
+  return u < pdfRadius / bound ? 1 : 0;
+}
+
+// Convergent: every lane calls it.  Inactive lanes do nothing.  2D: certified float
+// decisions by any lane, undecided ones by the owner (exact); 3D: exact decisions by
+// any lane (the 3D test is cheap single-precision arithmetic plus one exp).
 template <int DIM>
 __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM>& g, const float* dir,
                                                    Pcg32& s, float* pdf, float* out, uint32_t* iters,
                                                    bool need_pdf, RejLDS* L, int lane) {
   bool coop = false;
   float bound = 0.0f, nrm = 1.0f;
-  if (active && DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ && !WOS_ABL_ONE_REJ) {
+  if (active && g.yukawa && !WOS_ABL_ONE_REJ &&
+      (DIM == 3 || (g.muR < 80.0f && !WOS_NO_FASTREJ))) {
     const float R = g.R, lam = g.lambda, sl = g.sqrtLambda;
-    const float a = 2.2f, b = 0.6f;
+    const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
     bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
                      : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
     nrm = g.norm();
@@ -1012,8 +1033,15 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
-      L->rho[lane] = g.A0 / g.A1;
-      L->invNB[lane] = 1.0f / (nrm * bound);
+      if constexpr (DIM == 2) {
+        L->c0[lane] = g.A0 / g.A1;
+        L->c1[lane] = 1.0f / (nrm * bound);
+      } else {
+        L->c0[lane] = g.A0;
+        L->c1[lane] = g.A1;
+        L->nrm[lane] = nrm;
+        L->bound[lane] = bound;
+      }
     }
     int j0 = 0, jacc = -1;
     bool done = !coop;
@@ -1039,7 +1067,9 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           if (j < kRejMax) {
             float u, x;
             rej_draws(prm, L->s0[owner], j, &u, &x);
-            const int dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->rho[owner], L->invNB[owner]);
+            const int dcs = DIM == 2 ? rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner])
+                                     : rej_exact_decide3(u, x * L->R[owner], L->R[owner], L->sqrtL[owner], L->c0[owner],
+                                                         L->c1[owner], L->nrm[owner], L->bound[owner]);
             if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
             else if (dcs < 0) atomicOr(&L->und[owner], 1u << b);
           }

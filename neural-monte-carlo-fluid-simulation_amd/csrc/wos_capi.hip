@@ -357,7 +357,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   const int geom_floats =
       primAl + silAl + wos::kGroupStride * s->host.n_pgroups + wos::kSGroupStride * s->host.n_sgroups;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
-  const size_t shmem_fb = (size_t)(geom_floats + wos::kWavesPerBlockHost * 2 * lhs_floats) * sizeof(float);
+  const size_t shmem_fb =
+      (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
   const size_t shmem_walk =
       (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
   if (std::max(shmem_fb, shmem_walk) > 160 * 1024 - 256)

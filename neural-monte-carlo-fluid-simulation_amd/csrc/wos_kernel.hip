@@ -63,7 +63,7 @@ __device__ __forceinline__ void wave_sync() {
 // Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_NUM };
+       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_NUM };
 __device__ unsigned long long g_diag[D_NUM];
 #if WOS_DIAG
 __shared__ unsigned long long s_diag[D_NUM];
@@ -1666,11 +1666,19 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 
 // The first ball of pair w, both antithetic members (walk_on_stars.h:510-575);
 // member a becomes task t0 + a.
+// Called by every lane of the wave (the 3D source sample is wave-cooperative);
+// lanes with active == false run pair 0's arithmetic for nothing (helping the
+// cooperative sampler) and write and count nothing.
 template <int DIM>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
-                                            int w, int64_t t0, bool yuk0, uint32_t* iters) {
+                                            bool active, int w, int64_t t0, bool yuk0, uint32_t* iters,
+                                            RejLDS* rejL, int lane) {
   constexpr int sd = DIM - 1;
+  if (DIM == 2 && !active) return;
+  if (!active) w = 0;
+  uint32_t dummy_iters = 0;
+  if (!active) iters = &dummy_iters;
   const int64_t T = tk.T;
   float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
   for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
@@ -1691,7 +1699,10 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       if (a == 0) {
         float dir[DIM];
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-        sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, iters, true);
+        if constexpr (DIM == 3)
+          sample_volume_wave<DIM>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
+        else
+          sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, iters, true);
       } else {
         float sdv[DIM];
         for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - x[k];
@@ -1764,6 +1775,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       float den = boundaryPdf * throughput;
       for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
     }
+    if (!active) continue;
     tk.first[t] = firstSource;
     for (int k = 0; k < DIM; k++) {
       tk.bdir[k * T + t] = bdir[k];
@@ -1818,10 +1830,14 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
   const int wave = threadIdx.x / kWave;
   stage_geometry<DIM>(sc, smem, false);
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
+#endif
   __syncthreads();
   const float* Lprim = smem;
-  float* strat = smem + geom_floats + wave * 2 * lhs_floats;
+  float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(sizeof(RejLDS) / sizeof(float)));
   int* partner = (int*)(strat + lhs_floats);
+  RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);
 
   uint32_t c_iters = 0, c_pts = 0;
   const int npairs = prm.n_pairs;
@@ -1838,6 +1854,7 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
     for (int k = 0; k < DIM; k++) x[k] = pts[(int64_t)idx * DIM + k];
 
     // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
+    DIAG_T0(t_fb0);
     float nDist = kFltMax, nSigned = kFltMax;
     if (sc.n_prims > 0) {
       Closest c = closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
@@ -1874,17 +1891,29 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
     }
     if (!estimate) continue;
     c_pts += lane == 0;
+    DIAG_ADD(D_FB_SETUP, t_fb0);
+    DIAG_COUNT(D_FB_PTS, 1);
+    DIAG_T0(t_fb1);
     build_lhs<DIM>(prm, gidx, strat, partner, lane);
+    DIAG_ADD(D_FB_LHS, t_fb1);
+    DIAG_T0(t_fb2);
     const float firstR = 0.99f * smin(dDist, nDist);
-    for (int w = lane; w < npairs; w += kWave)
-      first_balls<DIM>(sc, prm, tk, x, firstR, strat, gidx, w, (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti,
-                       yuk0, &c_iters);
+    for (int w0 = 0; w0 < npairs; w0 += kWave) {
+      const int w = w0 + lane;
+      first_balls<DIM>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
+                       (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
+    }
+    DIAG_ADD(D_FB_BALLS, t_fb2);
+    DIAG_ADD(D_FB_TOTAL, t_fb0);
     wave_sync();
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
   __syncthreads();
   if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+#endif
 }
 
 // ---- walk-queue order: bucket offsets (descending cost) and the permutation ---
@@ -2235,6 +2264,8 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
   return hipGetLastError();
 }
 
+size_t first_ball_wave_lds_bytes(int lhs_floats) { return (size_t)2 * lhs_floats * sizeof(float) + sizeof(RejLDS); }
+
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
 hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks) {
@@ -2253,6 +2284,9 @@ void diag_dump(const char* tag) {
           tag, d[D_ITERS], (double)d[D_LANES] / (double)(d[D_ITERS] ? d[D_ITERS] : 1),
           (double)d[D_STEP] / d[D_ITERS], (double)d[D_STAR] / d[D_ITERS], (double)d[D_RAY] / d[D_ITERS],
           (double)d[D_SAMPLE] / d[D_ITERS], (double)d[D_LOOP] / d[D_ITERS], d[D_RAYOVF]);
+  const double fp = (double)(d[D_FB_PTS] ? d[D_FB_PTS] : 1);
+  fprintf(stderr, "[diag %s] first-ball: points %llu cycles/point: setup %.0f lhs %.0f balls %.0f total %.0f\n", tag,
+          d[D_FB_PTS], d[D_FB_SETUP] / fp, d[D_FB_LHS] / fp, d[D_FB_BALLS] / fp, d[D_FB_TOTAL] / fp);
   fprintf(stderr, "[diag %s] star calls %llu: groups visited/call %.2f, candidates/call %.2f, exact/call %.2f\n", tag,
           d[D_SCALLS], (double)d[D_SGVISIT] / d[D_SCALLS], (double)d[D_SCAND] / d[D_SCALLS],
           (double)d[D_SEXACT] / d[D_SCALLS]);

@@ -21,6 +21,8 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
                         int geom_floats, hipStream_t s);
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s);
+// per-wave LDS scratch of the first-ball kernel (after the staged geometry)
+size_t first_ball_wave_lds_bytes(int lhs_floats);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
 // which: 0 first-ball kernel, 1 walk kernel

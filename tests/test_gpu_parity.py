@@ -167,6 +167,39 @@ def test_gear_many_groups_bit_exact(gpu, oracle):
     _compare(oracle, osc, sc, cfg, cfg["points"])
 
 
+def test_open_box3d_silhouette_edges_bit_exact(gpu, oracle):
+    """3D with silhouette edges (one face of the cube removed -> open edges, like the
+    karman3d cube): edge silhouette candidates, 3D cone culling, the cooperative
+    star-radius and rejection paths in 3D."""
+    cfg = workloads.cube_config(res=10, n_walks=64)
+    v, ix = objparse.load(cfg["obj"], 3)
+    ix = ix[2:]
+    lam = float(cfg["scene"]["absorptionCoeff"])
+    osc = oracle.OracleScene(v, ix, cfg["source"], lam, watertight=False)
+    sc = WosScene(v, ix, cfg["source"], lam, watertight=False)
+    assert sc.info()["n_silhouettes"] > 0
+    _compare(oracle, osc, sc, cfg, cfg["points"])
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_double_sided_bit_exact(gpu, oracle, dim):
+    """isDoubleSided: every point is estimated, normals flip toward the walk's side
+    (walk_on_stars.h:150-160), silhouettes use both orientations."""
+    if dim == 2:
+        cfg = workloads.karman_config(n_walks=32)
+        v, ix = objparse.load(cfg["obj"], 2)
+        pts = cfg["points"][:512]
+    else:
+        cfg = workloads.cube_config(res=8, n_walks=32)
+        v, ix = objparse.load(cfg["obj"], 3)
+        ix = ix[2:]
+        pts = cfg["points"]
+    lam = float(cfg["scene"]["absorptionCoeff"])
+    osc = oracle.OracleScene(v, ix, cfg["source"], lam, watertight=True, double_sided=True)
+    sc = WosScene(v, ix, cfg["source"], lam, watertight=True, double_sided=True)
+    _compare(oracle, osc, sc, cfg, pts)
+
+
 def test_cube3d_bit_exact(gpu, oracle):
     cfg = workloads.cube_config(res=10, n_walks=64)
     osc, sc = _pair(cfg, oracle, dim=3)

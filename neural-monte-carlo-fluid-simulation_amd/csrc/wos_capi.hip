@@ -68,6 +68,10 @@ struct wos_scene {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> bev;  // per-batch kernel boundary events (4 per batch), grow-only
   int num_cus = 0;
+  // star-radius cell grid, built on first use for the solver's (precision, minR)
+  wos::StarGrid sgrid;
+  bool sgrid_built = false, sgrid_ok = false;
+  uint32_t* d_sgrid = nullptr;
 };
 
 extern "C" {
@@ -136,6 +140,7 @@ static void scene_release(wos_scene* s) {
   hipFree(s->d_jump);
   hipFree(s->d_tasks);
   hipFree(s->d_pstate);
+  hipFree(s->d_sgrid);
   if (s->ev0) hipEventDestroy(s->ev0);
   if (s->ev1) hipEventDestroy(s->ev1);
   for (hipEvent_t e : s->bev) hipEventDestroy(e);
@@ -304,6 +309,29 @@ static int ensure_jump(wos_scene* s, int k_needed) {
   return WOS_OK;
 }
 
+// LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
+static constexpr size_t kStarGridBudget = 16 * 1024;
+
+static bool star_grid_enabled() {
+  const char* e = std::getenv("WOS_STAR_GRID");  // "0": always the cooperative group scan (A/B runs, tests)
+  return !(e && e[0] == '0');
+}
+
+// (re)build the star grid for the solver's silhouette precision and minR
+static int ensure_star_grid(wos_scene* s, float prec, float min_r) {
+  if (s->sgrid_built && s->sgrid.prec == prec && s->sgrid.min_r == min_r) return WOS_OK;
+  hipFree(s->d_sgrid);
+  s->d_sgrid = nullptr;
+  s->sgrid_ok = wos::build_star_grid(s->host, prec, min_r, kStarGridBudget, s->sgrid);
+  s->sgrid_built = true;
+  if (s->sgrid_ok) {
+    HIP_TRY(hipMalloc((void**)&s->d_sgrid, s->sgrid.words.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(s->d_sgrid, s->sgrid.words.data(), s->sgrid.words.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
+  }
+  return WOS_OK;
+}
+
 int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
               int64_t index_stride, float* p, float* grad, int32_t* n_est, int32_t* steps, wos_stats* stats,
               void* stream, uint32_t flags) {
@@ -356,11 +384,36 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   const int silAl = (s->host.n_sil * SS + 3) & ~3;
   const int geom_floats =
       primAl + silAl + wos::kGroupStride * s->host.n_pgroups + wos::kSGroupStride * s->host.n_sgroups;
+  // the walk kernel also stages the star-radius grid (after the silhouette groups)
+  wos::DevScene dsc = s->dev;
+  dsc.sgrid = nullptr;
+  dsc.sgrid_words = dsc.sgrid_off_words = 0;
+  if (star_grid_enabled() && s->host.n_sil > 0) {
+    int rc = ensure_star_grid(s, prm->silhouette_precision, prm->min_star_radius);
+    if (rc != WOS_OK) return rc;
+    if (s->sgrid_ok) {
+      dsc.sgrid = s->d_sgrid;
+      dsc.sgrid_words = (int32_t)s->sgrid.words.size();
+      dsc.sgrid_off_words = s->sgrid.off_words;
+      for (int k = 0; k < 3; k++) {
+        dsc.sgrid_n[k] = s->sgrid.n[k];
+        dsc.sgrid_min[k] = s->sgrid.gmin[k];
+        dsc.sgrid_inv[k] = s->sgrid.inv[k];
+      }
+    }
+  }
+  int geom_floats_walk = geom_floats + ((dsc.sgrid_words + 3) & ~3);
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   const size_t shmem_fb =
       (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
-  const size_t shmem_walk =
-      (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+  size_t shmem_walk =
+      (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+  if (dsc.sgrid != nullptr && shmem_walk > 160 * 1024 - 256) {  // no room: the group scan alone
+    dsc.sgrid = nullptr;
+    dsc.sgrid_words = dsc.sgrid_off_words = 0;
+    geom_floats_walk = geom_floats;
+    shmem_walk = (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+  }
   if (std::max(shmem_fb, shmem_walk) > 160 * 1024 - 256)
     return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +
                                     std::to_string(std::max(shmem_fb, shmem_walk)) + " bytes)");
@@ -418,8 +471,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(hipEventRecord(ev[1], st));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
-    HIP_TRY(wos::launch_walks(dim, s->dev, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,
-                              shmem_walk, geom_floats, st));
+    HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,
+                              shmem_walk, geom_floats_walk, st));
     HIP_TRY(hipEventRecord(ev[2], st));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
                              d_steps ? d_steps + b0 : nullptr, st));

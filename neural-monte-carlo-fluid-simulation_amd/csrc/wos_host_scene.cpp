@@ -9,6 +9,7 @@
 // and packs everything into the flat records described in wos_scene.h.
 #include "wos_host_scene.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -311,6 +312,185 @@ bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
     out.n_sgroups++;
   }
   return true;
+}
+
+// ---------------------------------------------------------------------------
+// star-radius cell grid (wos_host_scene.h StarGrid)
+// ---------------------------------------------------------------------------
+namespace {
+
+struct SilGeo {
+  double a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, mid[3] = {0, 0, 0};
+  double n0[3] = {0, 0, 0}, n1[3] = {0, 0, 0};
+  double e0 = 0.0, e1 = 0.0;  // slack of the normal components along the edge (3D)
+  double half = 0.0;
+  bool miss = false;
+};
+
+double seg_point_dist(const SilGeo& s, const double* q, int dim) {
+  double u[3] = {0, 0, 0}, uu = 0.0, uv = 0.0;
+  for (int k = 0; k < dim; k++) {
+    u[k] = s.b[k] - s.a[k];
+    uu += u[k] * u[k];
+    uv += u[k] * (q[k] - s.a[k]);
+  }
+  const double t = uu > 0.0 ? std::min(1.0, std::max(0.0, uv / uu)) : 0.0;
+  double d2 = 0.0;
+  for (int k = 0; k < dim; k++) {
+    const double w = q[k] - (s.a[k] + t * u[k]);
+    d2 += w * w;
+  }
+  return std::sqrt(d2);
+}
+
+double box_point_dist(const double* lo, const double* hi, const double* p, int dim) {
+  double d2 = 0.0;
+  for (int k = 0; k < dim; k++) {
+    const double e = std::max(std::max(lo[k] - p[k], p[k] - hi[k]), 0.0);
+    d2 += e * e;
+  }
+  return std::sqrt(d2);
+}
+
+}  // namespace
+
+// For a cell box C (enlarged beyond the kernel's cell-index rounding) and a
+// candidate s with adjacent normals n0, n1:
+//   * f_i(x) = (x - a).n_i is linear in x, so its range over C is spanned by the
+//     corners (3D edges: the closest point slides along the edge, which moves f_i
+//     by at most |(b - a).n_i|, ~0 up to the records' rounding);
+//   * the view length |x - closest(s)| is convex in x: at most its corner maximum
+//     dmax, at least the box distance dmin (3D: box distance of the midpoint minus
+//     the half length);
+// so f_i > t*dmax over C proves the normalised dot u.n_i > t for every x in C.
+// With t = prec + 1e-4 (the kernel's dots are accurate to ~1e-6) and dmin above
+// prec (the exact test's direction branch): both dots of one sign -> the exact
+// test rejects everywhere (culled); opposite signs -> it accepts everywhere
+// (certain).  U = min over certain candidates of dmax bounds the result; a
+// candidate with dmin > max(U, minR) (with margin) is strictly farther than a
+// certain silhouette and cannot be the minR break either, so it never decides.
+bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget_bytes, StarGrid& out) {
+  out = StarGrid();
+  out.prec = prec;
+  out.min_r = min_r;
+  const int dim = hs.dim, ns = hs.n_sil;
+  if (ns <= 0 || ns > 255) return false;
+  const int SS = dim == 2 ? kSilStride2 : kSilStride3;
+  const int o0 = dim == 2 ? 2 : 6, o1 = dim == 2 ? 4 : 9, om = dim == 2 ? 6 : 12;
+  std::vector<SilGeo> sg(ns);
+  for (int s = 0; s < ns; s++) {
+    const float* S = &hs.sil[(size_t)s * SS];
+    SilGeo& g = sg[s];
+    double len2 = 0.0, d0 = 0.0, d1 = 0.0;
+    for (int k = 0; k < dim; k++) {
+      g.a[k] = S[k];
+      g.b[k] = dim == 2 ? S[k] : S[3 + k];
+      g.n0[k] = S[o0 + k];
+      g.n1[k] = S[o1 + k];
+      g.mid[k] = 0.5 * (g.a[k] + g.b[k]);
+      const double e = g.b[k] - g.a[k];
+      len2 += e * e;
+      d0 += e * g.n0[k];
+      d1 += e * g.n1[k];
+    }
+    g.miss = S[om] != 0.0f;
+    g.half = 0.5 * std::sqrt(len2);
+    g.e0 = std::fabs(d0) + 1e-6 * std::sqrt(len2);
+    g.e1 = std::fabs(d1) + 1e-6 * std::sqrt(len2);
+  }
+  double span = 0.0;
+  for (int k = 0; k < dim; k++) span = std::max(span, (double)hs.ext[k]);
+  if (!(span > 0.0)) return false;
+  const double gpad = 1e-3 * span + 1e-6;
+  double glo[3] = {0, 0, 0}, gext[3] = {1, 1, 1}, vol = 1.0;
+  for (int k = 0; k < dim; k++) {
+    glo[k] = (double)hs.pmin[k] - gpad;
+    gext[k] = ((double)hs.pmax[k] + gpad) - glo[k];
+    vol *= gext[k];
+  }
+  const double t = (double)prec + 1e-4;
+  const double near = 1.01 * (double)prec + 1e-6 * span + 1e-7;
+  const double dslack = 1e-5 * span;
+  const int ncorner = 1 << dim;
+  std::vector<double> mind(ns), maxd(ns);
+  std::vector<char> culled(ns);
+  for (int target = 4096; target >= 64; target /= 2) {
+    const double h = std::pow(vol / target, 1.0 / dim);
+    int n[3] = {1, 1, 1};
+    float gmin[3] = {0, 0, 0}, inv[3] = {0, 0, 0};
+    for (int k = 0; k < dim; k++) {
+      n[k] = std::max(1, (int)std::ceil(gext[k] / h));
+      gmin[k] = (float)glo[k];
+      inv[k] = (float)((double)n[k] / gext[k]);
+    }
+    const int ncell = n[0] * n[1] * n[2];
+    std::vector<uint16_t> off((size_t)ncell + 1, 0);
+    std::vector<uint8_t> lst;
+    bool overflow = false;
+    for (int c = 0; c < ncell && !overflow; c++) {
+      const int ic[3] = {c % n[0], (c / n[0]) % n[1], c / (n[0] * n[1])};
+      double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+      for (int k = 0; k < dim; k++) {
+        const double w = 1.0 / (double)inv[k];
+        const double delta = 1e-3 * w + 1e-5 * span;
+        lo[k] = (double)gmin[k] + ic[k] * w - delta;
+        hi[k] = (double)gmin[k] + (ic[k] + 1) * w + delta;
+      }
+      double U = HUGE_VAL;
+      for (int s = 0; s < ns; s++) {
+        const SilGeo& g = sg[s];
+        double dmax = 0.0, f0lo = HUGE_VAL, f0hi = -HUGE_VAL, f1lo = HUGE_VAL, f1hi = -HUGE_VAL;
+        for (int q = 0; q < ncorner; q++) {
+          double cq[3] = {0, 0, 0};
+          for (int k = 0; k < dim; k++) cq[k] = ((q >> k) & 1) ? hi[k] : lo[k];
+          dmax = std::max(dmax, seg_point_dist(g, cq, dim));
+          double f0 = 0.0, f1 = 0.0;
+          for (int k = 0; k < dim; k++) {
+            f0 += (cq[k] - g.a[k]) * g.n0[k];
+            f1 += (cq[k] - g.a[k]) * g.n1[k];
+          }
+          f0lo = std::min(f0lo, f0); f0hi = std::max(f0hi, f0);
+          f1lo = std::min(f1lo, f1); f1hi = std::max(f1hi, f1);
+        }
+        f0lo -= g.e0; f0hi += g.e0; f1lo -= g.e1; f1hi += g.e1;
+        const double dmin = dim == 2 ? box_point_dist(lo, hi, g.a, dim)
+                                     : std::max(0.0, box_point_dist(lo, hi, g.mid, dim) - g.half);
+        mind[s] = dmin;
+        maxd[s] = dmax * (1.0 + 1e-9);
+        culled[s] = 0;
+        bool certain = g.miss;
+        if (!g.miss && dmin > near) {
+          const double tm = t * dmax;
+          const bool pos0 = f0lo > tm, neg0 = f0hi < -tm, pos1 = f1lo > tm, neg1 = f1hi < -tm;
+          culled[s] = (pos0 && pos1) || (neg0 && neg1);
+          certain = (pos0 && neg1) || (neg0 && pos1);
+        }
+        if (certain) U = std::min(U, maxd[s]);
+      }
+      const double thr = std::max(U, (double)min_r) * (1.0 + 1e-4) + dslack;
+      for (int s = 0; s < ns; s++)
+        if (!culled[s] && !(mind[s] > thr)) lst.push_back((uint8_t)s);
+      if (lst.size() > 65535) overflow = true;
+      off[(size_t)c + 1] = (uint16_t)lst.size();
+    }
+    if (overflow) continue;
+    const int off_words = (ncell + 2) / 2;
+    const int list_words = ((int)lst.size() + 3) / 4;
+    if ((size_t)(off_words + list_words) * 4 > budget_bytes) continue;
+    out.words.assign((size_t)off_words + list_words, 0u);
+    std::memcpy(out.words.data(), off.data(), off.size() * sizeof(uint16_t));
+    if (!lst.empty()) std::memcpy(out.words.data() + off_words, lst.data(), lst.size());
+    for (int k = 0; k < 3; k++) {
+      out.n[k] = n[k];
+      out.gmin[k] = gmin[k];
+      out.inv[k] = inv[k];
+    }
+    out.ncell = ncell;
+    out.off_words = off_words;
+    out.list_len = lst.size();
+    return true;
+  }
+  return false;
 }
 
 // ---------------------------------------------------------------------------

@@ -31,6 +31,27 @@ struct HostScene {
   float pmin[3] = {0, 0, 0}, pmax[3] = {0, 0, 0}, ext[3] = {0, 0, 0};
 };
 
+// Star-radius cell grid: a uniform grid over the padded bounding box; cell c
+// holds the ascending list of the silhouette candidates that can decide
+// computeStarRadius (fcpw_scene_loader.h:621-641) for any point of the cell.
+// A candidate is left out only when, for every point of the (slightly enlarged)
+// cell, the exact test certainly rejects it (its two adjacent faces both face the
+// point, or both face away, with margin) or it certainly lies farther than a
+// candidate that is certainly a silhouette there (and farther than minR), so the
+// sequential scan over the list returns the full scan's result bit for bit.
+struct StarGrid {
+  int n[3] = {1, 1, 1};
+  float gmin[3] = {0.0f, 0.0f, 0.0f}, inv[3] = {0.0f, 0.0f, 0.0f};
+  int ncell = 0;
+  int off_words = 0;             // 32-bit words of the u16 offset table (ncell + 1 entries)
+  std::vector<uint32_t> words;   // [u16 offsets | u8 candidate indices], little-endian packed
+  size_t list_len = 0;
+  float prec = -1.0f, min_r = -1.0f;  // the solver settings it was built for
+};
+// false when the scene has no / too many (> 255) silhouette candidates or the grid
+// does not fit budget_bytes at a useful resolution (the kernel then scans groups)
+bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget_bytes, StarGrid& out);
+
 bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err);
 bool load_obj(const std::string& path, int dim, bool flip, bool normalize_domain, std::vector<float>& verts,
               std::vector<int32_t>& prims, std::string& err);

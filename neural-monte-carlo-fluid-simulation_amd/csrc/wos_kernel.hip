@@ -349,6 +349,8 @@ struct LGeom {
   const float* sil;
   const float* pgroup;
   const float* sgroup;
+  const uint32_t* sgrid;  // star-radius cell grid (u16 offsets | u8 lists), nullptr if none
+  int sgrid_off_words;
 };
 
 // Certain rejection of a whole group for a ray segment [o, o + rt*dir]: slab
@@ -1473,7 +1475,7 @@ __host__ __device__ constexpr size_t walk_scratch_bytes() {
 // Exact per-candidate test of the sequential loop against r2 (see star_radius).
 template <int DIM>
 __device__ __forceinline__ bool star_candidate(const LGeom& G, int s, const float* x, float r2, bool flip,
-                                               float prec, float* d2out) {
+                                               float prec, float* d2out, float* dout = nullptr) {
   constexpr int SS = Layout<DIM>::sil;
   const float* S = G.sil + s * SS;
   const float miss = DIM == 2 ? S[6] : S[12];
@@ -1501,7 +1503,49 @@ __device__ __forceinline__ bool star_candidate(const LGeom& G, int s, const floa
   if (!(d2 <= r2)) return false;
   if (cls != 1 && !is_silhouette<DIM>(S, view, d, flip, prec)) return false;
   *d2out = d2;
+  if (dout) *dout = d;
   return true;
+}
+
+// Cell of the star-radius grid holding x (cell = (iz * ny + iy) * nx + ix), or -1
+// when there is no grid or x lies outside it.  The host built every cell's list for
+// the cell enlarged well beyond the rounding of this index arithmetic.
+template <int DIM>
+__device__ __forceinline__ int star_cell(const DevScene& sc, const float* x) {
+  int c = 0;
+  for (int k = DIM - 1; k >= 0; k--) {
+    const int nk = sc.sgrid_n[k];
+    const float v = (x[k] - sc.sgrid_min[k]) * sc.sgrid_inv[k];
+    if (!(v >= 0.0f && v < (float)nk)) return -1;
+    int i = (int)v;
+    if (i > nk - 1) i = nk - 1;
+    c = c * nk + i;
+  }
+  return c;
+}
+
+// computeStarRadius for one lane from its cell's candidate list: the sequential
+// scan of star_radius (candidates in index order, r2 shrinking, minR break) over
+// the only candidates that can decide it (wos_host_scene.h StarGrid), hence the
+// full scan's result.
+template <int DIM>
+__device__ __forceinline__ float star_radius_cell(const LGeom& G, int cell, const float* x, float r2, float minR2,
+                                                  float minR, float dflt, bool flip, float prec) {
+  const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
+  const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
+  const int e1 = off[cell + 1];
+  bool found = false;
+  float best = 0.0f;
+  for (int e = off[cell]; e < e1; e++) {
+    float d2, d;
+    if (star_candidate<DIM>(G, (int)lst[e], x, r2, flip, prec, &d2, &d)) {
+      r2 = d2;
+      best = d;
+      found = true;
+      if (minR2 >= r2) break;
+    }
+  }
+  return found ? smax(best, minR) : dflt;
 }
 
 template <int DIM>
@@ -1535,6 +1579,15 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
         minR2 = minR * minR;
         need = !(minR2 >= r2);
       }
+    }
+  }
+  // lanes inside the star grid scan their cell's short list; the rest (no grid,
+  // outside it) share the wave-cooperative group scan below
+  if (need && G.sgrid != nullptr) {
+    const int cell = star_cell<DIM>(sc, x);
+    if (cell >= 0) {
+      result = star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
+      need = false;
     }
   }
   if (__ballot(need) == 0) return result;
@@ -1800,11 +1853,16 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
   G.sil = smem + primAl;
   G.pgroup = smem + primAl + silAl;
   G.sgroup = G.pgroup + pgN;
+  uint32_t* gw = reinterpret_cast<uint32_t*>(smem + primAl + silAl + pgN + sgN);
+  G.sgrid = (with_sil && sc.sgrid != nullptr) ? gw : nullptr;
+  G.sgrid_off_words = sc.sgrid_off_words;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
   if (with_sil) {
     for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
     for (int i = threadIdx.x; i < pgN; i += kBlock) smem[primAl + silAl + i] = sc.pgroup[i];
     for (int i = threadIdx.x; i < sgN; i += kBlock) smem[primAl + silAl + pgN + i] = sc.sgroup[i];
+    if (sc.sgrid != nullptr)
+      for (int i = threadIdx.x; i < sc.sgrid_words; i += kBlock) gw[i] = sc.sgrid[i];
   }
   return G;
 }

@@ -57,6 +57,12 @@ struct DevScene {
   float g_dirichlet;
   int32_t watertight;
   int32_t double_sided;
+  // star-radius cell grid (wos_host_scene.h StarGrid; nullptr: none): u16 cell
+  // offsets then u8 candidate lists, staged into LDS by the walk kernel
+  const uint32_t* sgrid;
+  int32_t sgrid_words, sgrid_off_words;
+  int32_t sgrid_n[3];
+  float sgrid_min[3], sgrid_inv[3];
 };
 
 struct DevParams {

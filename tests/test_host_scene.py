@@ -143,6 +143,66 @@ def silhouette_2d(S, x, prec, flip=True):
     return d0 * d1 < 0
 
 
+def _grid_check(shim, v, ix, dim, pts, double_sided=False, prec=1e-3, min_r=1e-3, budget=16384):
+    v = np.ascontiguousarray(v, np.float32)
+    ix = np.ascontiguousarray(ix, np.int32)
+    pts = np.ascontiguousarray(pts, np.float32)
+    info = np.zeros(10, np.int32)
+    f = C.POINTER(C.c_float)
+    shim.hs_star_grid_check.restype = C.c_int
+    bad = shim.hs_star_grid_check(dim, v.ctypes.data_as(f), v.shape[0], ix.ctypes.data_as(C.POINTER(C.c_int)),
+                                  ix.shape[0], int(double_sided), C.c_float(prec), C.c_float(min_r),
+                                  pts.ctypes.data_as(f), pts.shape[0], budget, info.ctypes.data_as(C.POINTER(C.c_int)))
+    return bad, dict(zip(["ok", "ncell", "list_len", "bytes", "n0", "n1", "n2", "checked", "max_list"], info[:9]))
+
+
+def _grid_points(v, dim, sil_pts, n=6000, seed=5):
+    """uniform points over the bbox (+5 % band), points within 1e-4..3e-2 of every
+    silhouette candidate, and points on a fine lattice (cell boundaries)"""
+    rng = np.random.default_rng(seed)
+    lo, hi = v.min(0), v.max(0)
+    span = (hi - lo).max()
+    out = [rng.uniform(lo - 0.05 * span, hi + 0.05 * span, (n, dim))]
+    for q in sil_pts:
+        r = np.exp(rng.uniform(np.log(1e-4), np.log(3e-2), (40, 1)))
+        d = rng.normal(size=(40, dim))
+        out.append(q + r * d / np.linalg.norm(d, axis=1, keepdims=True))
+    g = np.linspace(0.0, 1.0, 41 if dim == 2 else 13)
+    mesh = np.stack(np.meshgrid(*([g] * dim), indexing="ij"), -1).reshape(-1, dim)
+    out.append(lo + mesh * (hi - lo))
+    return np.concatenate(out).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,dim,v,ix", scenes(), ids=[s[0] for s in scenes()])
+@pytest.mark.parametrize("double_sided", [False, True])
+def test_star_grid_lists_decide_the_full_scan(shim, name, dim, v, ix, double_sided):
+    """The star-radius grid (wos_host_scene.cpp build_star_grid) must give, for every
+    point of its cells, the same computeStarRadius as the full sequential scan over
+    all silhouette candidates -- bit for bit, both normal orientations."""
+    r = prepare(shim, v, ix, dim, double_sided)
+    sil_pts = r["sil"][:, 0:dim] if dim == 2 else 0.5 * (r["sil"][:, 0:3] + r["sil"][:, 3:6])
+    pts = _grid_points(np.asarray(v, np.float64), dim, sil_pts)
+    bad, info = _grid_check(shim, v, ix, dim, pts, double_sided)
+    if r["sil"].shape[0] == 0 or r["sil"].shape[0] > 255:  # no grid: the kernel scans groups
+        assert not info["ok"]
+        return
+    assert info["ok"], info
+    assert info["bytes"] <= 16384
+    assert info["checked"] > 0.8 * pts.shape[0], info
+    assert bad == 0, (bad, info)
+
+
+@pytest.mark.parametrize("prec,min_r", [(1e-3, 1e-3), (1e-2, 0.05), (1e-4, 1e-4)])
+def test_star_grid_other_settings(shim, prec, min_r):
+    s = [t for t in scenes() if t[0] == "karman"][0]
+    r = prepare(shim, s[2], s[3], 2)
+    pts = _grid_points(np.asarray(s[2], np.float64), 2, r["sil"][:, 0:2], n=4000, seed=11)
+    bad, info = _grid_check(shim, s[2], s[3], 2, pts, prec=prec, min_r=min_r)
+    assert info["ok"] and bad == 0, (bad, info)
+    # the lists are short: far fewer candidates than the 44 of a full scan
+    assert info["list_len"] / info["ncell"] < 12, info
+
+
 @pytest.mark.parametrize("name", ["karman", "gear"])
 def test_cone_culling_is_sound(shim, name):
     s = [t for t in scenes() if t[0] == name][0]

@@ -1719,7 +1719,8 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 
 // The first ball of pair w, both antithetic members (walk_on_stars.h:510-575);
 // member a becomes task t0 + a.
-// Called by every lane of the wave (the 3D source sample is wave-cooperative);
+// Called by every lane of the wave (the 3D source sample is wave-cooperative;
+// 2D keeps the per-lane loop: measured faster for first balls, r1d);
 // lanes with active == false run pair 0's arithmetic for nothing (helping the
 // cooperative sampler) and write and count nothing.
 template <int DIM>

@@ -309,6 +309,10 @@ static int ensure_jump(wos_scene* s, int k_needed) {
   return WOS_OK;
 }
 
+// dynamic LDS a workgroup may use: 160 KB per CU minus the kernels' static LDS
+// (rejection jump table 2 KB, counters, histogram)
+static constexpr size_t kLdsDynamicMax = 160 * 1024 - 4096;
+
 // LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
 static constexpr size_t kStarGridBudget = 16 * 1024;
 
@@ -408,13 +412,13 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
       (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
   size_t shmem_walk =
       (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
-  if (dsc.sgrid != nullptr && shmem_walk > 160 * 1024 - 256) {  // no room: the group scan alone
+  if (dsc.sgrid != nullptr && shmem_walk > kLdsDynamicMax) {  // no room: the group scan alone
     dsc.sgrid = nullptr;
     dsc.sgrid_words = dsc.sgrid_off_words = 0;
     geom_floats_walk = geom_floats;
     shmem_walk = (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
   }
-  if (std::max(shmem_fb, shmem_walk) > 160 * 1024 - 256)
+  if (std::max(shmem_fb, shmem_walk) > kLdsDynamicMax)
     return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +
                                     std::to_string(std::max(shmem_fb, shmem_walk)) + " bytes)");
 

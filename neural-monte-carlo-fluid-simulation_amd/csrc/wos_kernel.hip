@@ -36,6 +36,14 @@ namespace wos {
 #ifndef WOS_NO_FASTREJ
 #define WOS_NO_FASTREJ 0
 #endif
+// timing-only ablations (wrong results): float Bessels in the ball update and the
+// direction-sampled Poisson kernel; a constant source texel
+#ifndef WOS_ABL_FAST_BESSEL
+#define WOS_ABL_FAST_BESSEL 0
+#endif
+#ifndef WOS_ABL_CONST_SRC
+#define WOS_ABL_CONST_SRC 0
+#endif
 #ifndef WOS_ABL_NO_STATS
 #define WOS_ABL_NO_STATS 0
 #endif
@@ -63,7 +71,9 @@ __device__ __forceinline__ void wave_sync() {
 // Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_NUM };
+       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_NUM };
+// slots holding maxima (folded with atomicMax)
+__host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 __device__ unsigned long long g_diag[D_NUM];
 #if WOS_DIAG
 __shared__ unsigned long long s_diag[D_NUM];
@@ -83,11 +93,13 @@ __shared__ unsigned long long s_diag[D_NUM];
       atomicAdd(&s_diag[slot], n_);                                                    \
   } while (0)
 #define DIAG_LANE(slot) atomicAdd(&s_diag[slot], 1ull)
+#define DIAG_MAX(slot, v) atomicMax(&s_diag[slot], (unsigned long long)(v))
 #else
 #define DIAG_T0(v)
 #define DIAG_ADD(slot, v)
 #define DIAG_COUNT(slot, n)
 #define DIAG_LANE(slot)
+#define DIAG_MAX(slot, v)
 #endif
 
 template <int DIM>
@@ -625,6 +637,7 @@ __device__ __forceinline__ void offset_point(const float* p, const float* n, flo
 template <int DIM>
 __device__ __forceinline__ float source_value(const DevScene& sc, const float* x) {
   if (sc.source == nullptr) return 0.0f;
+  if (WOS_ABL_CONST_SRC) return 0.5f;
   if constexpr (DIM == 2) {
     float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
     float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
@@ -651,6 +664,12 @@ __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x)
   return false;
 }
 
+// float Bessel approximations (defined with the certified rejection fast path below)
+__device__ __forceinline__ float i0_fast(float x);
+__device__ __forceinline__ float k0_fast(float x);
+__device__ __forceinline__ float i1_fast(float x);
+__device__ __forceinline__ float k1_fast(float x);
+
 // ---------------------------------------------------------------------------
 // Green's functions on balls (distributions.h:273-832)
 // ---------------------------------------------------------------------------
@@ -673,10 +692,14 @@ struct Gfn {
     if (!yukawa) return;
     muR = R * sqrtLambda;
     if constexpr (DIM == 2) {
+#if WOS_ABL_FAST_BESSEL
+      A0 = k0_fast(muR); A1 = i0_fast(muR); B0 = k1_fast(muR); B1 = i1_fast(muR);
+#else
       A0 = (float)bessk0((double)muR);
       A1 = (float)bessi0((double)muR);
       B0 = (float)bessk1((double)muR);
       B1 = (float)bessi1((double)muR);
+#endif
     } else {
       float expmuR = fexp(-muR);
       float exp2muR = expmuR * expmuR;
@@ -776,8 +799,12 @@ struct Gfn {
     float rr = smax(rClamp, normv<DIM>(d));
     float mur = rr * sqrtLambda;
     if constexpr (DIM == 2) {
+#if WOS_ABL_FAST_BESSEL
+      float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
+#else
       float K1mur = (float)bessk1((double)mur);
       float I1mur = (float)bessi1((double)mur);
+#endif
       float Q = K1mur + I1mur * A0 / A1;
       return mur * Q;
     } else {
@@ -881,6 +908,31 @@ __device__ __forceinline__ float k0_fast(float x) {
          y * (-0.1062446e-1f + y * (0.587872e-2f + y * (-0.251540e-2f + y * 0.53208e-3f))))));
 }
 
+__device__ __forceinline__ float i1_fast(float x) {
+  if (x < 3.75f) {
+    float y = x / 3.75f;
+    y = y * y;
+    return x * (0.5f + y * (0.87890594f + y * (0.51498869f + y * (0.15084934f + y * (0.2658733e-1f +
+           y * (0.301532e-2f + y * 0.32411e-3f))))));
+  }
+  float y = 3.75f / x;
+  float a = 0.2282967e-1f + y * (-0.2895312e-1f + y * (0.1787654e-1f - y * 0.420059e-2f));
+  a = 0.39894228f + y * (-0.3988024e-1f + y * (-0.362018e-2f + y * (0.163801e-2f + y * (-0.1031555e-1f + y * a))));
+  return exp_fast(x) * __builtin_amdgcn_rsqf(x) * a;
+}
+
+__device__ __forceinline__ float k1_fast(float x) {
+  if (x <= 2.0f) {
+    float y = x * x / 4.0f;
+    return (__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * i1_fast(x) +
+           (1.0f / x) * (1.0f + y * (0.15443144f + y * (-0.67278579f + y * (-0.18156897f + y * (-0.1919402e-1f +
+           y * (-0.110404e-2f + y * (-0.4686e-4f)))))));
+  }
+  float y = 2.0f / x;
+  return exp_fast(-x) * __builtin_amdgcn_rsqf(x) * (1.25331414f + y * (0.23498619f + y * (-0.3655620e-1f +
+         y * (0.1504268e-1f + y * (-0.780353e-2f + y * (0.325614e-2f + y * (-0.68245e-3f)))))));
+}
+
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM>
@@ -964,11 +1016,27 @@ __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0
   return A * s0 + Cc;
 }
 
+// The jump constants of the first kRejJumpLds rejection iterations (draw 2j) are
+// staged in LDS by every kernel that samples (stage_rej_jump); later iterations
+// (P ~ 1e-4 per sample) read the global table.
+constexpr int kRejJumpLds = 128;
+__shared__ unsigned long long s_rej_jump[2 * kRejJumpLds];
+
+__device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
+  for (int i = threadIdx.x; i < 2 * kRejJumpLds; i += blockDim.x) s_rej_jump[i] = prm.jump[4 * (i >> 1) + (i & 1)];
+}
+
+// stream state before rejection iteration j (draw 2j) from stream start s0
+__device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0, int j) {
+  if (j < kRejJumpLds) return s_rej_jump[2 * j] * s0 + s_rej_jump[2 * j + 1];
+  return jump_state(prm, s0, 2 * j);
+}
 
 struct RejLDS {
   unsigned long long s0[kWave];
   float R[kWave], sqrtL[kWave];
   float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
+  float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
   float nrm[kWave], bound[kWave];
   uint32_t base[kWave], acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
@@ -980,7 +1048,7 @@ __device__ __forceinline__ float draw_float(uint64_t state) {
 
 // the two draws of rejection iteration j from stream start s0
 __device__ __forceinline__ void rej_draws(const DevParams& prm, uint64_t s0, int j, float* u, float* x) {
-  const uint64_t st = jump_state(prm, s0, 2 * j);
+  const uint64_t st = rej_state(prm, s0, j);
   *u = draw_float(st);
   *x = draw_float(st * kPcgMult + kPcgInc);
 }
@@ -992,6 +1060,25 @@ __device__ __forceinline__ int rej_fast_decide(float u, float r, float sqrtL, fl
   const float c = r * invNB;
   const float Tf = (k0 - ip) * c;
   const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
+  return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
+}
+
+// 3D analogue: e = exp(-mu r) from exp_fast (<= ~3 ulp) and an approximate
+// reciprocal; the band M covers their error carried through the cancellation in
+// sinh(mu r) = (1 - e^2) / 2e and Q = e - (A0/A1) sinh, plus the rounding of the
+// exact path's float/double steps (~4 ulp of T), with a >= 4x margin.  Non-finite
+// or underflowed e leaves M non-finite: undecided.
+__device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, float rho, float invNB) {
+  const float mur = r * sqrtL;
+  const float e = exp_fast(-mur);
+  const float ie = __builtin_amdgcn_rcpf(e);
+  const float sh = (1.0f - e * e) * 0.5f * ie;
+  const float Q = e - rho * sh;
+  const float c = r * invNB;
+  const float Tf = Q * c;
+  const float ar = __builtin_fabsf(rho);
+  const float M = (2e-6f * e + ar * (3e-7f * ie + 2e-6f * e + 4e-6f * __builtin_fabsf(sh))) * c +
+                  4e-6f * __builtin_fabsf(Tf) + 1e-30f;
   return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
 }
 
@@ -1012,8 +1099,9 @@ __device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, floa
 }
 
 // Convergent: every lane calls it.  Inactive lanes do nothing.  2D: certified float
-// decisions by any lane, undecided ones by the owner (exact); 3D: exact decisions by
-// any lane (the 3D test is cheap single-precision arithmetic plus one exp).
+// decisions by any lane, undecided ones by the owner (exact); 3D: certified float
+// decisions by any lane, undecided ones by the same lane with the exact test (cheap
+// single-precision arithmetic plus one exp).
 template <int DIM>
 __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM>& g, const float* dir,
                                                    Pcg32& s, float* pdf, float* out, uint32_t* iters,
@@ -1041,6 +1129,8 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       } else {
         L->c0[lane] = g.A0;
         L->c1[lane] = g.A1;
+        L->rho3[lane] = g.A0 / g.A1;
+        L->inv3[lane] = 1.0f / (nrm * bound);
         L->nrm[lane] = nrm;
         L->bound[lane] = bound;
       }
@@ -1069,9 +1159,16 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           if (j < kRejMax) {
             float u, x;
             rej_draws(prm, L->s0[owner], j, &u, &x);
-            const int dcs = DIM == 2 ? rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner])
-                                     : rej_exact_decide3(u, x * L->R[owner], L->R[owner], L->sqrtL[owner], L->c0[owner],
-                                                         L->c1[owner], L->nrm[owner], L->bound[owner]);
+            int dcs;
+            if constexpr (DIM == 2) {
+              dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
+            } else {
+              const float rr = x * L->R[owner];
+              dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
+              if (dcs < 0)
+                dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
+                                        L->bound[owner]);
+            }
             if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
             else if (dcs < 0) atomicOr(&L->und[owner], 1u << b);
           }
@@ -1109,7 +1206,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       float u, x;
       rej_draws(prm, s0, jacc, &u, &x);
       g.r = x * g.R;
-      s.state = jump_state(prm, s0, 2 * jacc + 2);
+      s.state = rej_state(prm, s0, jacc + 1);
       *iters += (uint32_t)(jacc + 1);
       if (need_pdf) *pdf = g.evaluate() / nrm;
       g.r = smax(Gfn<DIM>::rClamp, g.r);
@@ -1888,6 +1985,7 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   stage_geometry<DIM>(sc, smem, false);
+  stage_rej_jump(prm);
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
@@ -1964,6 +2062,7 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
     }
     DIAG_ADD(D_FB_BALLS, t_fb2);
     DIAG_ADD(D_FB_TOTAL, t_fb0);
+    DIAG_MAX(D_FB_MAX, __builtin_amdgcn_s_memtime() - t_fb0);
     wave_sync();
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
@@ -1971,7 +2070,10 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
   __syncthreads();
   if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
 #if WOS_DIAG
-  if (threadIdx.x < D_NUM) atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+  if (threadIdx.x < D_NUM) {
+    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+  }
 #endif
 }
 
@@ -2007,14 +2109,28 @@ __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk,
 // ---- kernel 2: walks ---------------------------------------------------------
 constexpr unsigned int kTaskGrab = 256;  // tasks a wave takes from the global queue at once
 
+// experiments (0 = off): WOS_PRIO=n raises the wave priority with the age of its
+// oldest walk (steps / n); WOS_DRAIN=n stops handing tasks to a wave whose oldest
+// walk is n steps old, so the long walks run in light waves
+#ifndef WOS_PRIO
+#define WOS_PRIO 0
+#endif
+#ifndef WOS_DRAIN
+#define WOS_DRAIN 0
+#endif
+// 4 waves per SIMD (<= 128 VGPRs): latency hiding for the walk's long dependent chains
+#ifndef WOS_WALK_WAVES_PER_EU
+#define WOS_WALK_WAVES_PER_EU 4
+#endif
 template <int DIM>
-__global__ __launch_bounds__(kBlock) void wos_walk_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK_WAVES_PER_EU))) void wos_walk_kernel(
     const DevScene sc, const DevParams prm, const DevTasks tk, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int s_ctr[C_NUM];
   const int lane = threadIdx.x & (kWave - 1);
   const LGeom G = stage_geometry<DIM>(sc, smem, true);
+  stage_rej_jump(prm);
   // per-wave scratch shared by the star and ray queries (used one after the other)
   char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + (threadIdx.x / kWave) * walk_scratch_bytes<DIM>();
   StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
@@ -2032,9 +2148,55 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
   uint32_t c_iters = 0;
 
-  uint32_t qn = 0, qe = 0;  // the wave's window [qn, qe) of the task queue (wave-uniform)
+  DIAG_T0(t_wave);
+  // ---- task supply: a window [wq, we) of the global queue (wave-uniform; lane i
+  // holds perm[wp0 + i]) feeds a 64-slot ring of staged tasks, one per lane: ring
+  // position (lane - head) & 63, positions [0, S) valid.  The ring is refilled at
+  // the end of every iteration, so the loads of a staged task (its record and its
+  // point's state) are in flight during a whole step and a lane that finishes a
+  // walk starts the next one from registers (cross-lane shuffles) instead of a
+  // chain of dependent global loads.
+  const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;  // <= 64 points per window
+  uint32_t wq = 0, we = 0, wp0 = 0, wperm = 0;
   bool exhausted = false;
+  int head = 0, S = 0;
+  uint32_t s_t = 0, s_ok = 0;  // staged task index, its point is estimated
+  float s_pt[DIM], s_thr = 0.0f, s_tsrc = 0.0f, s_dd = 0.0f;
+  for (int k = 0; k < DIM; k++) s_pt[k] = 0.0f;
+  auto refill = [&]() {
+    while (S < kWave && !exhausted) {
+      if (wq >= we) {
+        unsigned int c = 0;
+        if (lane == 0) c = atomicAdd(tqueue, G_win);
+        c = __shfl(c, 0);
+        if (c >= T) { exhausted = true; break; }
+        wq = c;
+        we = (T - c) < G_win ? T : c + G_win;
+        wp0 = c / wpp;
+        const uint32_t np = (we - 1) / wpp - wp0 + 1;
+        wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
+      }
+      const int avail = (int)(we - wq);
+      const int take = (kWave - S) < avail ? (kWave - S) : avail;
+      const int pos = ((lane - head) & (kWave - 1)) - S;
+      const bool mine = pos >= 0 && pos < take;
+      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = q / wpp;
+      const uint32_t pidx = (uint32_t)__shfl((int)wperm, (int)(qp - wp0));  // queue position -> permuted point
+      if (mine) {
+        s_t = pidx * wpp + (q - qp * wpp);
+        s_ok = tk.pstate[pidx] & kPtEstimate;
+        for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
+        s_thr = tk.thr[s_t];
+        s_tsrc = tk.tsrc[s_t];
+        s_dd = tk.dd[s_t];
+      }
+      S += take;
+      wq += (uint32_t)take;
+    }
+  };
+  refill();
   int64_t t = -1;           // this lane's task
+  int wmax = 0;             // longest live walk of the wave (steps), wave-uniform
   WalkState<DIM> st;
   Gfn<DIM> g;
   Pcg32 ws;
@@ -2043,54 +2205,65 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
 
   for (;;) {
     DIAG_T0(t_loop);
-    // ---- hand out tasks to idle lanes (uniform control flow)
-    bool fresh = false;
-    for (;;) {
+    // ---- hand staged tasks to idle lanes (uniform control flow)
+    {
       const uint64_t need = __ballot(t < 0);
-      if (need == 0 || exhausted) break;
-      if (qn >= qe) {
-        unsigned int c = 0;
-        if (lane == 0) c = atomicAdd(tqueue, kTaskGrab);
-        c = __shfl(c, 0);
-        if (c >= T) { exhausted = true; break; }
-        qn = c;
-        qe = (T - c) < kTaskGrab ? T : c + kTaskGrab;
-      }
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      const uint32_t k = (uint32_t)__popcll(need);
-      const uint32_t avail = qe - qn;
-      if (t < 0 && rank < avail) {
-        const uint32_t q = qn + rank, qp = q / wpp;
-        t = (int64_t)tk.perm[qp] * wpp + (q - qp * wpp);  // queue position -> task of the permuted point
-        fresh = true;
-      }
-      qn += k < avail ? k : avail;
-    }
-    if (__ballot(t >= 0) == 0) break;  // queue drained and every lane idle
-
-    if (t >= 0 && fresh) {
-      const uint32_t pidx = (uint32_t)t / wpp;
-      const uint32_t w = ((uint32_t)t - pidx * wpp) / (uint32_t)prm.n_anti;
-      if (!(tk.pstate[pidx] & kPtEstimate)) {  // point outside the domain: no walks
-        tk.code[t] = 0u;
-        t = -1;
-      } else {
-        for (int k = 0; k < DIM; k++) { st.pt[k] = tk.pt[k * tk.T + t]; st.n[k] = 0.0f; st.prevDir[k] = 0.0f; }
-        // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
-        // and every step rewrites them before that can happen
-        st.prevDist = 0.0f;
-        st.throughput = tk.thr[t];
-        st.onNeumann = false;
-        st.walkLength = 0;
-        st.totalNeumann = 0.0f;
-        st.totalSource = tk.tsrc[t];
-        ddist = tk.dd[t];
-        g.init(yuk0, sc.absorption);
-        ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
-        wsteps = 1;  // the first ball
+      if (need != 0 && S > 0 && (WOS_DRAIN == 0 || wmax < WOS_DRAIN)) {
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const int k = __popcll(need);
+        const int take = k < S ? k : S;
+        const int src = (head + (rank < take ? rank : 0)) & (kWave - 1);
+        const uint32_t v_t = (uint32_t)__shfl((int)s_t, src);
+        const uint32_t v_ok = (uint32_t)__shfl((int)s_ok, src);
+        float v_pt[DIM];
+        for (int kk = 0; kk < DIM; kk++) v_pt[kk] = __shfl(s_pt[kk], src);
+        const float v_thr = __shfl(s_thr, src), v_tsrc = __shfl(s_tsrc, src), v_dd = __shfl(s_dd, src);
+        if (t < 0 && rank < take) {
+          t = (int64_t)v_t;
+          if (!v_ok) {  // point outside the domain: no walks
+            tk.code[t] = 0u;
+            t = -1;
+          } else {
+            const uint32_t pidx = v_t / wpp;
+            const uint32_t w = (v_t - pidx * wpp) / (uint32_t)prm.n_anti;
+            for (int kk = 0; kk < DIM; kk++) { st.pt[kk] = v_pt[kk]; st.n[kk] = 0.0f; st.prevDir[kk] = 0.0f; }
+            // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
+            // and every step rewrites them before that can happen
+            st.prevDist = 0.0f;
+            st.throughput = v_thr;
+            st.onNeumann = false;
+            st.walkLength = 0;
+            st.totalNeumann = 0.0f;
+            st.totalSource = v_tsrc;
+            ddist = v_dd;
+            g.init(yuk0, sc.absorption);
+            ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
+            wsteps = 1;  // the first ball
+          }
+        }
+        head = (head + take) & (kWave - 1);
+        S -= take;
       }
     }
+    if (__ballot(t >= 0) == 0) {
+      if (S == 0 && exhausted) break;  // queue drained and every lane idle
+      refill();
+      continue;
+    }
+#if WOS_PRIO || WOS_DRAIN
+    {
+      int wl = t >= 0 ? st.walkLength : 0;
+      for (int off = kWave / 2; off > 0; off >>= 1) wl = smax(wl, __shfl_xor(wl, off));
+      wmax = __builtin_amdgcn_readfirstlane(wl);
+    }
+#endif
+#if WOS_PRIO
+    if (wmax >= 3 * WOS_PRIO) __builtin_amdgcn_s_setprio(3);
+    else if (wmax >= 2 * WOS_PRIO) __builtin_amdgcn_s_setprio(2);
+    else if (wmax >= WOS_PRIO) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
 
     DIAG_COUNT(D_ITERS, 1);
     DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
@@ -2131,18 +2304,24 @@ __global__ __launch_bounds__(kBlock) void wos_walk_kernel(
         tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
       }
       tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
+      DIAG_MAX(D_WMAXLEN, wsteps);
       atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
       atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL],
                 1u);
       t = -1;
     }
+    refill();
     DIAG_ADD(D_LOOP, t_loop);
   }
 
+  DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
   flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();
 #if WOS_DIAG
-  if (threadIdx.x < D_NUM) atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+  if (threadIdx.x < D_NUM) {
+    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+  }
 #endif
   if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
     unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
@@ -2346,6 +2525,8 @@ void diag_dump(const char* tag) {
   const double fp = (double)(d[D_FB_PTS] ? d[D_FB_PTS] : 1);
   fprintf(stderr, "[diag %s] first-ball: points %llu cycles/point: setup %.0f lhs %.0f balls %.0f total %.0f\n", tag,
           d[D_FB_PTS], d[D_FB_SETUP] / fp, d[D_FB_LHS] / fp, d[D_FB_BALLS] / fp, d[D_FB_TOTAL] / fp);
+  fprintf(stderr, "[diag %s] max cycles/point (first balls) %llu, longest walk %llu steps, longest walk-kernel wave %llu cycles\n",
+          tag, d[D_FB_MAX], d[D_WMAXLEN], d[D_WAVEMAX]);
   fprintf(stderr, "[diag %s] star calls %llu: groups visited/call %.2f, candidates/call %.2f, exact/call %.2f\n", tag,
           d[D_SCALLS], (double)d[D_SGVISIT] / d[D_SCALLS], (double)d[D_SCAND] / d[D_SCALLS],
           (double)d[D_SEXACT] / d[D_SCALLS]);

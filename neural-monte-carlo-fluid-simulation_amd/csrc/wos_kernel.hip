@@ -933,6 +933,22 @@ __device__ __forceinline__ float k1_fast(float x) {
          y * (0.1504268e-1f + y * (-0.780353e-2f + y * (0.325614e-2f + y * (-0.68245e-3f)))))));
 }
 
+// Certain-reject bound of the Yukawa rejection test.  The test accepts iff
+// u < T(r) = (K0(mu r) - rho I0(mu r)) r / (norm bound) (2D) or
+// (e^{-mu r} - rho sinh(mu r)) r / (norm bound) (3D), with rho = A0/A1 > 0 and the
+// subtracted term >= 0 for 0 <= r <= R, so T(r) <= r K0(mu r) / (norm bound)
+// <= 0.46652 / (mu norm bound) (max_z z K0(z) at z = 0.595) and in 3D
+// T(r) <= r e^{-mu r} / (norm bound) <= 1 / (e mu norm bound).  The constants carry
+// a 1e-3 margin (far above the A&S polynomial error and the float rounding of the
+// exact path), so u above the bound is the exact test's reject without evaluating
+// r at all.  A non-positive or non-finite bound disables the shortcut.
+template <int DIM>
+__device__ __forceinline__ float rej_quick_bound(float sqrtL, float invNB) {
+  const float C = DIM == 2 ? 0.4670f : 0.3683f;
+  const float q = C * invNB / sqrtL;
+  return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
+}
+
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM>
@@ -965,13 +981,16 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
   const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
   const float rho = g.A0 / g.A1;
   const float invNB = 1.0f / (nrm * bound);
+  const float quick = g.yukawa ? rej_quick_bound<DIM>(g.sqrtLambda, invNB) : 3.0e38f;
   int iter = 0;
   do {
     float u = s.nextf();
     g.r = s.nextf() * R;
     iter++;
     int decided = -1;  // 1 accept, 0 reject, -1 undecided
-    if (fast) {
+    if (u > quick) {
+      decided = 0;
+    } else if (fast) {
       const float mur = g.r * g.sqrtLambda;
       const float k0 = k0_fast(mur), ip = i0_fast(mur) * rho;
       const float c = g.r * invNB;
@@ -1009,6 +1028,16 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
 // the fast path (3D, harmonic, mu*R >= 80) run the sequential loop.
 // ---------------------------------------------------------------------------
 constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
+// minimum iterations per unfinished lane and generation of the cooperative sampler
+// (2D acceptance ~21 %, 3D ~7 % on the shipped scenes)
+#ifndef WOS_REJ_BMIN2
+#define WOS_REJ_BMIN2 1
+#endif
+#ifndef WOS_REJ_BMIN3
+#define WOS_REJ_BMIN3 16
+#endif
+template <int DIM>
+constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3;
 
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
@@ -1037,6 +1066,7 @@ struct RejLDS {
   float R[kWave], sqrtL[kWave];
   float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
   float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
+  float qb[kWave];                 // certain-reject bound (rej_quick_bound)
   float nrm[kWave], bound[kWave];
   uint32_t base[kWave], acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
@@ -1123,6 +1153,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
+      L->qb[lane] = rej_quick_bound<DIM>(g.sqrtLambda, 1.0f / (nrm * bound));
       if constexpr (DIM == 2) {
         L->c0[lane] = g.A0 / g.A1;
         L->c1[lane] = 1.0f / (nrm * bound);
@@ -1141,7 +1172,12 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       const uint64_t pend = __ballot(!done);
       if (pend == 0) break;
       const int nact = __popcll(pend);
-      const int B = nact >= kWave ? 1 : (kWave / nact > 32 ? 32 : kWave / nact);
+      // B consecutive iterations per unfinished lane, at least kRejBmin (fewer
+      // generations -- each costs three wave syncs and the owners' scan -- for a
+      // few iterations evaluated past an accept)
+      int B = kWave / nact;
+      B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > 32 ? 32 : B);
+      const int items = nact * B, per = (items + kWave - 1) / kWave;
       if (!done) {
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
@@ -1151,18 +1187,23 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         L->und[lane] = 0u;
       }
       wave_sync();
-      {
-        const int orank = lane / B, b = lane - orank * B;
+      for (int q = 0; q < per; q++) {
+        const int item = lane * per + q;
+        const int orank = item / B, b = item - orank * B;
         if (orank < nact) {
           const int owner = (int)L->owner_of[orank];
           const int j = (int)L->base[owner] + b;
           if (j < kRejMax) {
-            float u, x;
-            rej_draws(prm, L->s0[owner], j, &u, &x);
-            int dcs;
-            if constexpr (DIM == 2) {
+            const uint64_t st = rej_state(prm, L->s0[owner], j);
+            const float u = draw_float(st);
+            int dcs = 0;
+            if (u > L->qb[owner]) {
+              // certain reject: the radius draw is not needed
+            } else if constexpr (DIM == 2) {
+              const float x = draw_float(st * kPcgMult + kPcgInc);
               dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
             } else {
+              const float x = draw_float(st * kPcgMult + kPcgInc);
               const float rr = x * L->R[owner];
               dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
               if (dcs < 0)
@@ -1769,8 +1810,91 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
 // them hits PCG's rejection threshold, in which case lane 0 replays the shuffle
 // draws sequentially from the true stream.
 
+// The shuffle `for j: swap(a[j], a[partner[j]])` (partner[j] >= j), wave-parallel
+// and exact.  Position j is final after step j and receives the value position
+// q = partner[j] holds just before step j.  Let V(k) be the original index held by
+// position k just before step k: V(k) = V(link(k)) where link(k) = the last step
+// m < k with partner[m] = k (it moved V(m) into k and nothing wrote k since), or k
+// itself if no step wrote k.  Then the final a'[j] = a[P(j)] with P(j) = V(j) when
+// q = j, else V(pred(j)) with pred(j) = the last step m < j with partner[m] = q,
+// or q if none.  link is an atomicMax; V resolves by pointer jumping (chains are
+// short for random partners); pred is the predecessor among equal targets, found
+// chunk by chunk (64 steps) with a lane mask per target plus the running last
+// writer of earlier chunks.  Scratch: 7 words per stratum (fb_union_bytes).
+__device__ __forceinline__ void lhs_permute(float* strat, const int* partner, int nstrat, int sd, int dimi,
+                                            char* scratch, int lane) {
+  int* link = reinterpret_cast<int*>(scratch);
+  int* val = link + nstrat;
+  int* last = val + nstrat;
+  int* perm = last + nstrat;
+  float* tmp = reinterpret_cast<float*>(perm + nstrat);
+  unsigned long long* cmask = reinterpret_cast<unsigned long long*>(tmp + nstrat + (nstrat & 1));
+  const int* pd = partner + dimi * nstrat;
+  for (int j = lane; j < nstrat; j += kWave) { link[j] = -1; last[j] = -1; cmask[j] = 0ull; }
+  wave_sync();
+  for (int j = lane; j < nstrat; j += kWave) {
+    const int q = pd[j];
+    if (q != j) atomicMax(&link[q], j);
+  }
+  wave_sync();
+  for (int j = lane; j < nstrat; j += kWave) val[j] = j;
+  wave_sync();
+  // pointer jumping: link[j] >= 0 means "V(j) = V(link[j])", unresolved
+  for (;;) {
+    bool pending = false;
+    int nl[4], nv[4];
+    for (int c = 0, j = lane; j < nstrat; j += kWave, c++) {
+      const int p = link[j];
+      nl[c] = p;
+      nv[c] = val[j];
+      if (p >= 0) {
+        const int pp = link[p];
+        if (pp < 0) { nv[c] = val[p]; nl[c] = -1; } else { nl[c] = pp; pending = true; }
+      }
+    }
+    wave_sync();
+    for (int c = 0, j = lane; j < nstrat; j += kWave, c++) { link[j] = nl[c]; val[j] = nv[c]; }
+    wave_sync();
+    if (!__any(pending)) break;
+  }
+  // predecessor among steps with the same target, 64 steps at a time
+  for (int c0 = 0; c0 < nstrat; c0 += kWave) {
+    const int j = c0 + lane;
+    const int q = j < nstrat ? pd[j] : j;
+    const bool mover = j < nstrat && q != j;
+    if (mover) atomicOr(&cmask[q], 1ull << lane);
+    wave_sync();
+    int P = 0;
+    if (j < nstrat) {
+      if (!mover) {
+        P = val[j];
+      } else {
+        const unsigned long long below = cmask[q] & ((1ull << lane) - 1ull);
+        const int pred = below ? c0 + 63 - __builtin_clzll(below) : last[q];
+        P = pred >= 0 ? val[pred] : q;
+      }
+      perm[j] = P;
+    }
+    wave_sync();
+    if (mover) { atomicMax(&last[q], j); cmask[q] = 0ull; }
+    wave_sync();
+  }
+  for (int j = lane; j < nstrat; j += kWave) tmp[j] = strat[sd * perm[j] + dimi];
+  wave_sync();
+  for (int j = lane; j < nstrat; j += kWave) strat[sd * j + dimi] = tmp[j];
+  wave_sync();
+}
+
+// per-wave first-ball scratch after the stratified samples and partners: the
+// rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute
+__host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
+  const size_t a = sizeof(RejLDS), b = (size_t)28 * lhs_floats + 64;
+  return ((a > b ? a : b) + 15) & ~size_t(15);
+}
+
 template <int DIM>
-__device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner, int lane) {
+__device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
+                                          char* scratch, int lane) {
   constexpr int sd = DIM - 1;
   const int nstrat = 2 * prm.n_pairs;
   const int nd = nstrat * sd;
@@ -1796,13 +1920,20 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   }
   const bool any_rej = __any(rej);
   wave_sync();
-  if (lane == 0) {
-    if (any_rej) {  // exact replay of the sequential stream (rare: P ~ n^2 / 2^32)
+  if (any_rej) {  // exact replay of the sequential stream (rare: P ~ n^2 / 2^32)
+    if (lane == 0) {
       Pcg32 q;
       q.state = jump_state(prm, s0, nd);
       for (int i = 0; i < sd; ++i)
         for (int j = 0; j < nstrat; ++j) partner[i * nstrat + j] = j + (int)q.bounded((uint32_t)(nstrat - j));
     }
+    wave_sync();
+  }
+  if (nstrat <= 4 * kWave) {
+    for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);
+    return;
+  }
+  if (lane == 0) {  // more strata than lhs_permute's per-lane registers: the serial shuffle
     for (int i = 0; i < sd; ++i)
       for (int j = 0; j < nstrat; ++j) {
         const int other = partner[i * nstrat + j];
@@ -1975,8 +2106,11 @@ __device__ __forceinline__ void flush_counter(unsigned long long* counters, int 
 enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
 
 // ---- kernel 1: point setup + first balls ----------------------------------
+#ifndef WOS_FB_WAVES_PER_EU
+#define WOS_FB_WAVES_PER_EU 1
+#endif
 template <int DIM>
-__global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
     int lhs_floats) {
@@ -1992,7 +2126,7 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
 #endif
   __syncthreads();
   const float* Lprim = smem;
-  float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(sizeof(RejLDS) / sizeof(float)));
+  float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
   int* partner = (int*)(strat + lhs_floats);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);
 
@@ -2000,15 +2134,21 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
   const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
 
+  // point queue, one point ahead: the next index is taken (and its coordinates
+  // loaded) while the current point is processed, so neither the queue atomic nor
+  // the point load sits on a point's critical path
+  unsigned int idx = 0;
+  if (lane == 0) idx = atomicAdd(work, 1u);
+  idx = __shfl(idx, 0);
+  float xn[DIM];
+  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
   for (;;) {
-    unsigned int idx = 0;
-    if (lane == 0) idx = atomicAdd(work, 1u);
-    idx = __shfl(idx, 0);
     if ((int64_t)idx >= n) break;
     const int64_t gidx = base + (int64_t)idx * stride;
-
     float x[DIM];
-    for (int k = 0; k < DIM; k++) x[k] = pts[(int64_t)idx * DIM + k];
+    for (int k = 0; k < DIM; k++) x[k] = xn[k];
+    unsigned int nidx_l0 = 0;
+    if (lane == 0) nidx_l0 = atomicAdd(work, 1u);
 
     // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
     DIAG_T0(t_fb0);
@@ -2046,12 +2186,15 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
       tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
       atomicAdd(&s_hist[bucket], 1u);
     }
-    if (!estimate) continue;
+    // the next point: its index (the atomic has returned by now) and coordinates
+    const unsigned int nidx = (unsigned int)__shfl((int)nidx_l0, 0);
+    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
+    if (!estimate) { idx = nidx; continue; }
     c_pts += lane == 0;
     DIAG_ADD(D_FB_SETUP, t_fb0);
     DIAG_COUNT(D_FB_PTS, 1);
     DIAG_T0(t_fb1);
-    build_lhs<DIM>(prm, gidx, strat, partner, lane);
+    build_lhs<DIM>(prm, gidx, strat, partner, reinterpret_cast<char*>(rejL), lane);
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
     const float firstR = 0.99f * smin(dDist, nDist);
@@ -2064,6 +2207,7 @@ __global__ __launch_bounds__(kBlock) void wos_first_ball_kernel(
     DIAG_ADD(D_FB_TOTAL, t_fb0);
     DIAG_MAX(D_FB_MAX, __builtin_amdgcn_s_memtime() - t_fb0);
     wave_sync();
+    idx = nidx;
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
@@ -2502,7 +2646,9 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
   return hipGetLastError();
 }
 
-size_t first_ball_wave_lds_bytes(int lhs_floats) { return (size_t)2 * lhs_floats * sizeof(float) + sizeof(RejLDS); }
+size_t first_ball_wave_lds_bytes(int lhs_floats) {
+  return (size_t)2 * lhs_floats * sizeof(float) + fb_union_bytes(lhs_floats);
+}
 
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 

@@ -1,0 +1,112 @@
+"""Soundness of the certain-reject bound of the Yukawa rejection sampler
+(csrc/wos_kernel.hip rej_quick_bound): for every ball, the exact accept threshold
+T(r) = pdfRadius(r) / bound of rejectionSampleGreensFn (distributions.h:362-383,
+Yukawa members :573-696 (2D), :698-832 (3D)) -- evaluated here with the oracle's
+deterministic math and the kernel's float/double rounding steps -- never exceeds the
+bound, so skipping the radius evaluation when u > bound cannot change a decision.
+CPU only (the oracle library)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+f32 = np.float32
+TWO_PI = 6.283185307179586
+FOUR_PI = 12.566370614359172
+
+
+def _bessel(which, x):
+    L = oracle_lib.lib()
+    L.oracle_bessel.restype = C.c_double
+    L.oracle_bessel.argtypes = [C.c_int, C.c_double, C.c_int]
+    return L.oracle_bessel(which, float(x), 0)
+
+
+def _expf(x):
+    L = oracle_lib.lib()
+    L.oracle_math.restype = C.c_double
+    L.oracle_math.argtypes = [C.c_int, C.c_double, C.c_int]
+    return f32(L.oracle_math(10, float(x), 0))
+
+
+def _bound(R, lam, sl, dim):
+    a, b = (f32(2.2), f32(0.6)) if dim == 2 else (f32(2.0), f32(0.5))
+    sR = f32(np.sqrt(R))
+    if R <= lam:
+        return max(max(f32(a / R), f32(a / lam)), max(f32(b * sR), f32(b * sl)))
+    return max(min(f32(a / R), f32(a / lam)), min(f32(b * sR), f32(b * sl)))
+
+
+def _quick(dim, sl, inv_nb):
+    C_ = f32(0.4670) if dim == 2 else f32(0.3683)
+    q = f32(f32(C_ * inv_nb) / sl)
+    # the kernel disables the shortcut for a non-positive / non-finite bound
+    # (tiny balls, where the float norm cancels to <= 0)
+    return q if (q > 0 and q < f32(3.0e38)) else f32(3.0e38)
+
+
+def _thresholds_2d(R, lam, xs):
+    sl = f32(np.sqrt(f32(lam)))
+    muR = f32(R * sl)
+    A0 = f32(_bessel(2, muR))
+    A1 = f32(_bessel(0, muR))
+    pk = f32(1.0 / (TWO_PI * float(A1)))
+    nrm = f32((1.0 - TWO_PI * float(pk)) / float(lam))
+    bound = _bound(R, f32(lam), sl, 2)
+    out = []
+    for x in xs:
+        r = f32(x * R)
+        mur = f32(r * sl)
+        K0 = f32(_bessel(2, mur))
+        I0 = f32(_bessel(0, mur))
+        ev = f32(float(f32(K0 - f32(f32(I0 * A0) / A1))) / TWO_PI)
+        p = f32(ev / nrm)
+        pdf = f32(1.0 / (TWO_PI * float(r)))
+        out.append(f32(f32(p / pdf) / bound))
+    inv_nb = f32(f32(1.0) / f32(nrm * bound))
+    return np.array(out), _quick(2, sl, inv_nb)
+
+
+def _thresholds_3d(R, lam, xs):
+    sl = f32(np.sqrt(f32(lam)))
+    muR = f32(R * sl)
+    e = _expf(-muR)
+    A0 = e
+    A1 = f32(f32(f32(1.0) - f32(e * e)) / f32(f32(2.0) * e))
+    pk = f32(float(muR) / (FOUR_PI * float(A1)))
+    nrm = f32((1.0 - FOUR_PI * float(pk)) / float(lam))
+    bound = _bound(R, f32(lam), sl, 3)
+    out = []
+    for x in xs:
+        r = f32(x * R)
+        mur = f32(r * sl)
+        em = _expf(-mur)
+        sh = f32(f32(f32(1.0) - f32(em * em)) / f32(f32(2.0) * em))
+        ev = f32(float(f32(em - f32(f32(A0 * sh) / A1))) / (FOUR_PI * float(r)))
+        p = f32(ev / nrm)
+        pdf = f32(1.0 / ((FOUR_PI * float(r)) * float(r)))
+        out.append(f32(f32(p / pdf) / bound))
+    inv_nb = f32(f32(1.0) / f32(nrm * bound))
+    return np.array(out), _quick(3, sl, inv_nb)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+@pytest.mark.parametrize("lam", [50.0, 350.0, 2000.0])
+def test_quick_reject_bound_dominates_exact_threshold(dim, lam):
+    rng = np.random.default_rng(7 + dim)
+    radii = np.concatenate([np.exp(rng.uniform(np.log(1e-4), np.log(3.0), 24)), [1e-3, 0.05, 0.5, 2.0]])
+    # dense near the peak of r K0(mu r) / r e^{-mu r} (x ~ 1 / (mu R)) and over all of (0, 1]
+    for R in radii.astype(np.float32):
+        mu = np.sqrt(lam)
+        peak = min(1.0, 0.6 / (mu * float(R)))
+        xs = np.unique(np.concatenate([np.linspace(1e-4, 1.0, 300), peak * np.linspace(0.5, 1.5, 101)]))
+        xs = xs[(xs > 0) & (xs <= 1.0)].astype(np.float32)
+        T, q = (_thresholds_2d if dim == 2 else _thresholds_3d)(f32(R), f32(lam), xs)
+        T = T[np.isfinite(T)]
+        assert T.size > 0
+        assert T.max() <= q, (dim, lam, float(R), float(T.max()), float(q))
+        # and the bound is useful: within a small factor of the true maximum once mu R >~ 1
+        if mu * R > 2.0 and q < f32(3.0e38):
+            assert q < 1.5 * T.max(), (dim, lam, float(R), float(T.max()), float(q))

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 2
+#define WOS_ABI_VERSION 3
 
 enum {
     WOS_OK = 0,
@@ -77,6 +77,22 @@ typedef struct wos_scene wos_scene;
 int wos_scene_create(const wos_scene_desc *desc, int32_t device, wos_scene **out);
 int wos_scene_destroy(wos_scene *scene);
 
+/* Replaces the source grid (-div u) of an existing scene.  The reference rebuilds
+ * the whole scene every projection to change only this (model_split.py:185-191,
+ * Scene(sceneConfig, div) -> scene.h:54-77 / scene_3d.h:22-40); here geometry
+ * stays resident.  dims as wos_scene_desc.source_dims; `on_device`: `source` is
+ * a device pointer on the scene's device.  The copy is ordered on `stream`
+ * (hipStream_t, NULL = null stream) after any solve still running on another
+ * stream. */
+int wos_scene_set_source(wos_scene *scene, const float *source, const int32_t *dims,
+                         int32_t on_device, void *stream);
+
+/* Scenes share a per-device solve workspace and a cache of prepared geometries
+ * (keyed by content), so the reference's per-step Scene(...) costs neither a
+ * workspace allocation nor a re-preparation.  This releases both for `device`
+ * (-1: every device); live scenes stay valid and the next solve reallocates. */
+int wos_release_caches(int32_t device);
+
 typedef struct wos_scene_info {
     int32_t dim, n_prims, n_silhouettes, n_dprims, device;
     float bbox_min[3], bbox_max[3];
@@ -122,6 +138,10 @@ typedef struct wos_stats {
     double walk_ms;             /* of which: the walks (wos_walk_kernel) -- the dominant kernel */
     double fold_ms;             /* of which: statistics + masked outputs (wos_fold_kernel) */
     uint64_t walk_launches;     /* walk-kernel launches (one per batch of points) */
+    int32_t first_ball_blocks_per_cu;  /* occupancy of the launches (256-thread workgroups per CU) */
+    int32_t walk_blocks_per_cu;
+    int32_t walk_lds_bytes;     /* dynamic LDS per walk-kernel workgroup */
+    int32_t star_grid;          /* 1: the star-radius cell grid was staged */
 } wos_stats;
 
 /* Replaces runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d

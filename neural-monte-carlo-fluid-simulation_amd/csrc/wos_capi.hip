@@ -1,13 +1,25 @@
 // wos_capi.hip -- the extern "C" boundary declared in include/wos.h.
 //
-// Owns device memory for the scene (geometry records + source grid) and a
-// grow-only per-scene workspace (staging buffers for host pointers, counters,
-// work queue).  Errors are reported as status codes + wos_last_error(), never by
-// aborting the process (the reference aborts: config.h:8-11, scene.h:106-109).
+// Device memory lives at three levels, sized for a time-stepper that builds a
+// new Scene(sceneConfig, div) for every projection (model_split.py:191):
+//   * per device (DevCtx, kept for the process): the solve workspace -- walk
+//     tasks, per-point state, PCG32 jump table, counters, staging buffers for
+//     host pointers, timing events.  Shared by every scene on the device, so a
+//     fresh scene costs no workspace allocation;
+//   * per geometry (Geom, shared by content, the 8 most recent kept after their
+//     last scene is gone): the prepared boundary records and the star-radius
+//     grids built for it, so re-creating a scene on the same boundary skips the
+//     preparation and the upload;
+//   * per scene: the source grid (replaceable in place, wos_scene_set_source).
+// Errors are reported as status codes + wos_last_error(), never by aborting the
+// process (the reference aborts: config.h:8-11, scene.h:106-109).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <list>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -41,17 +53,11 @@ hipError_t upload(T** dst, const std::vector<T>& src) {
   return hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
 }
 
-}  // namespace
-
-struct wos_scene {
-  int device = 0;
-  wos::HostScene host;
-  wos::DevScene dev{};
-  float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
-  float* d_source = nullptr;
-  float *d_pgroup = nullptr, *d_sgroup = nullptr;
-  // workspace
-  std::mutex mu;
+// ---- per-device solve workspace ---------------------------------------------
+struct DevCtx {
+  std::mutex mu;  // one solve at a time per device (the workspace is shared)
+  bool ready = false;
+  int num_cus = 0;
   float* d_pts = nullptr;
   float* d_p = nullptr;
   float* d_g = nullptr;
@@ -60,18 +66,183 @@ struct wos_scene {
   size_t ws_points = 0;
   uint64_t* d_jump = nullptr;  // PCG32 jump-ahead table (A_k, C_k), grow-only
   int n_jump = 0;
-  float* d_tasks = nullptr;      // walk-task workspace (DevTasks arrays), grow-only
-  int64_t task_cap = 0;          // tasks
-  int32_t* d_pstate = nullptr;   // per-point state + queue permutation of one batch, then bucket counters
+  float* d_tasks = nullptr;    // walk-task workspace (DevTasks arrays), grow-only
+  int64_t task_cap = 0;
+  int32_t* d_pstate = nullptr; // per-point state + queue permutation of one batch, then bucket counters
   int64_t pstate_cap = 0;
-  unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counter
+  unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counters
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::vector<hipEvent_t> bev;  // per-batch kernel boundary events (4 per batch), grow-only
-  int num_cus = 0;
-  // star-radius cell grid, built on first use for the solver's (precision, minR)
-  wos::StarGrid sgrid;
-  bool sgrid_built = false, sgrid_ok = false;
-  uint32_t* d_sgrid = nullptr;
+  hipEvent_t done = nullptr;   // end of the last enqueued solve
+  hipStream_t last_stream = nullptr;
+  bool inflight = false;       // a solve may still run on last_stream
+  std::vector<hipEvent_t> bev; // per-batch kernel boundary events (4 per batch), grow-only
+};
+
+constexpr int kMaxDevices = 64;
+DevCtx g_ctx[kMaxDevices];  // never destroyed: the HIP runtime may be gone at process exit
+
+void ctx_free(DevCtx& c) {
+  hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
+  hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters);
+  if (c.ev0) hipEventDestroy(c.ev0);
+  if (c.ev1) hipEventDestroy(c.ev1);
+  if (c.done) hipEventDestroy(c.done);
+  for (hipEvent_t e : c.bev) hipEventDestroy(e);
+  c.d_pts = c.d_p = c.d_g = nullptr;
+  c.d_nest = c.d_steps = nullptr;
+  c.ws_points = 0;
+  c.d_jump = nullptr; c.n_jump = 0;
+  c.d_tasks = nullptr; c.task_cap = 0;
+  c.d_pstate = nullptr; c.pstate_cap = 0;
+  c.d_counters = nullptr;
+  c.ev0 = c.ev1 = c.done = nullptr;
+  c.bev.clear();
+  c.last_stream = nullptr;
+  c.inflight = false;
+  c.ready = false;
+}
+
+// caller holds c.mu and has selected the device
+int ctx_ready(DevCtx& c, int device) {
+  if (c.ready) return WOS_OK;
+  HIP_TRY(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, device));
+  HIP_TRY(hipMalloc((void**)&c.d_counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
+  HIP_TRY(hipEventCreate(&c.ev0));
+  HIP_TRY(hipEventCreate(&c.ev1));
+  HIP_TRY(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+  c.ready = true;
+  return WOS_OK;
+}
+
+// order `st` after the last solve enqueued on another stream (the workspace and,
+// for set_source, the source grid may still be in use there)
+hipError_t ctx_order(DevCtx& c, hipStream_t st) {
+  if (c.inflight && c.last_stream != st && c.done) return hipStreamWaitEvent(st, c.done, 0);
+  return hipSuccess;
+}
+
+// ---- prepared geometry, shared by content -----------------------------------
+struct Geom {
+  int device = 0;
+  int dim = 2, double_sided = 0;
+  std::vector<float> v, dv;  // the key: exactly the inputs of prepare_scene
+  std::vector<int32_t> ix, dix;
+  wos::HostScene host;
+  float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
+  float *d_pgroup = nullptr, *d_sgroup = nullptr;
+  std::mutex mu;  // star grids
+  struct Grid {
+    float prec, min_r;
+    bool ok;
+    wos::StarGrid grid;
+    uint32_t* d = nullptr;
+  };
+  std::list<Grid> grids;  // stable addresses (a solve keeps a pointer)
+  ~Geom() {
+    hipSetDevice(device);
+    hipFree(d_prim); hipFree(d_paux); hipFree(d_sil); hipFree(d_dprim); hipFree(d_dpaux);
+    hipFree(d_pgroup); hipFree(d_sgroup);
+    for (Grid& g : grids) hipFree(g.d);
+  }
+};
+
+std::mutex g_geom_mu;
+// most recent first; heap-held and never destroyed (no hipFree during static teardown)
+std::vector<std::shared_ptr<Geom>>& g_geom_lru = *new std::vector<std::shared_ptr<Geom>>();
+constexpr size_t kGeomCacheSize = 8;
+
+template <typename T>
+bool same(const std::vector<T>& a, const T* b, int n) {
+  return a.size() == (size_t)n && (n == 0 || std::memcmp(a.data(), b, (size_t)n * sizeof(T)) == 0);
+}
+
+bool geom_matches(const Geom& g, const wos_scene_desc* d, int device) {
+  const int dim = d->dim;
+  return g.device == device && g.dim == dim && g.double_sided == d->is_double_sided &&
+         same(g.v, d->vertices, d->n_vertices * dim) && same(g.ix, d->prims, d->n_prims * dim) &&
+         same(g.dv, d->dvertices, d->n_dvertices * dim) && same(g.dix, d->dprims, d->n_dprims * dim);
+}
+
+// the prepared geometry of `d` on `device`: from the cache, else prepared + uploaded
+int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
+  {
+    std::lock_guard<std::mutex> lk(g_geom_mu);
+    for (size_t i = 0; i < g_geom_lru.size(); i++)
+      if (geom_matches(*g_geom_lru[i], d, device)) {
+        out = g_geom_lru[i];
+        std::rotate(g_geom_lru.begin(), g_geom_lru.begin() + i, g_geom_lru.begin() + i + 1);
+        return WOS_OK;
+      }
+  }
+  auto g = std::make_shared<Geom>();
+  const int dim = d->dim;
+  g->device = device;
+  g->dim = dim;
+  g->double_sided = d->is_double_sided;
+  if (d->n_vertices > 0) g->v.assign(d->vertices, d->vertices + (size_t)d->n_vertices * dim);
+  if (d->n_prims > 0) g->ix.assign(d->prims, d->prims + (size_t)d->n_prims * dim);
+  if (d->n_dvertices > 0) g->dv.assign(d->dvertices, d->dvertices + (size_t)d->n_dvertices * dim);
+  if (d->n_dprims > 0) g->dix.assign(d->dprims, d->dprims + (size_t)d->n_dprims * dim);
+  wos::HostSceneInput in;
+  in.dim = dim;
+  in.vertices = d->vertices; in.prims = d->prims; in.n_vertices = d->n_vertices; in.n_prims = d->n_prims;
+  in.dvertices = d->dvertices; in.dprims = d->dprims; in.n_dvertices = d->n_dvertices; in.n_dprims = d->n_dprims;
+  in.is_double_sided = d->is_double_sided;
+  std::string err;
+  if (!wos::prepare_scene(in, g->host, err)) return fail(WOS_E_INVALID, "wos_scene_create: " + err);
+  HIP_TRY(upload(&g->d_prim, g->host.prim));
+  HIP_TRY(upload(&g->d_paux, g->host.paux));
+  HIP_TRY(upload(&g->d_sil, g->host.sil));
+  HIP_TRY(upload(&g->d_dprim, g->host.dprim));
+  HIP_TRY(upload(&g->d_dpaux, g->host.dpaux));
+  HIP_TRY(upload(&g->d_pgroup, g->host.pgroup));
+  HIP_TRY(upload(&g->d_sgroup, g->host.sgroup));
+  {
+    std::lock_guard<std::mutex> lk(g_geom_mu);
+    g_geom_lru.insert(g_geom_lru.begin(), g);
+    if (g_geom_lru.size() > kGeomCacheSize) g_geom_lru.pop_back();
+  }
+  out = g;
+  return WOS_OK;
+}
+
+// LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
+constexpr size_t kStarGridBudget = 16 * 1024;
+
+// dynamic LDS a workgroup may use: 160 KB per CU minus the kernels' static LDS
+// (rejection jump table 2 KB, counters, histogram)
+constexpr size_t kLdsDynamicMax = 160 * 1024 - 4096;
+
+bool star_grid_enabled() {
+  const char* e = std::getenv("WOS_STAR_GRID");  // "0": always the cooperative group scan (A/B runs, tests)
+  return !(e && e[0] == '0');
+}
+
+// the star grid of `g` for the solver's silhouette precision and minR (built once)
+int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  for (const Geom::Grid& x : g.grids)
+    if (x.prec == prec && x.min_r == min_r) { *out = &x; return WOS_OK; }
+  Geom::Grid x{prec, min_r, false, {}, nullptr};
+  x.ok = wos::build_star_grid(g.host, prec, min_r, kStarGridBudget, x.grid);
+  if (x.ok) {
+    HIP_TRY(hipMalloc((void**)&x.d, x.grid.words.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(x.d, x.grid.words.data(), x.grid.words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  g.grids.push_back(std::move(x));
+  *out = &g.grids.back();
+  return WOS_OK;
+}
+
+}  // namespace
+
+struct wos_scene {
+  int device = 0;
+  std::shared_ptr<Geom> geom;
+  wos::DevScene dev{};
+  float* d_source = nullptr;
+  size_t source_cap = 0;  // floats
+  std::mutex mu;          // solve vs set_source on the same scene
 };
 
 extern "C" {
@@ -129,83 +300,64 @@ void wos_default_params(wos_solver_params* p) {
   p->seed = 0x5EED0001ULL;
 }
 
-static void scene_release(wos_scene* s) {
-  if (!s) return;
-  hipSetDevice(s->device);
-  hipFree(s->d_prim); hipFree(s->d_paux); hipFree(s->d_sil); hipFree(s->d_dprim); hipFree(s->d_dpaux);
-  hipFree(s->d_source);
-  hipFree(s->d_pgroup); hipFree(s->d_sgroup);
-  hipFree(s->d_pts); hipFree(s->d_p); hipFree(s->d_g); hipFree(s->d_nest); hipFree(s->d_steps);
-  hipFree(s->d_counters);
-  hipFree(s->d_jump);
-  hipFree(s->d_tasks);
-  hipFree(s->d_pstate);
-  hipFree(s->d_sgrid);
-  if (s->ev0) hipEventDestroy(s->ev0);
-  if (s->ev1) hipEventDestroy(s->ev1);
-  for (hipEvent_t e : s->bev) hipEventDestroy(e);
+static int check_source_dims(int dim, const int32_t* dims, size_t* nsrc) {
+  const int nsd = dim == 2 ? 2 : 3;
+  size_t n = 1;
+  for (int k = 0; k < nsd; k++) {
+    if (dims[k] <= 0) return fail(WOS_E_INVALID, "bad source dims");
+    n *= (size_t)dims[k];
+  }
+  *nsrc = n;
+  return WOS_OK;
 }
 
 int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   if (!d || !out) return fail(WOS_E_INVALID, "wos_scene_create: null argument");
   *out = nullptr;
   if (d->dim != 2 && d->dim != 3) return fail(WOS_E_INVALID, "wos_scene_create: dim must be 2 or 3");
-  const int nsd = d->dim == 2 ? 2 : 3;
-  for (int k = 0; k < nsd; k++)
-    if (d->source && d->source_dims[k] <= 0) return fail(WOS_E_INVALID, "wos_scene_create: bad source dims");
+  size_t nsrc = 0;
+  if (d->source && check_source_dims(d->dim, d->source_dims, &nsrc) != WOS_OK)
+    return fail(WOS_E_INVALID, "wos_scene_create: bad source dims");
   if (!(d->absorption >= 0.0f)) return fail(WOS_E_INVALID, "wos_scene_create: absorption must be >= 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(WOS_E_DEVICE, "wos_scene_create: no HIP device available");
-  if (device < 0 || device >= ndev) return fail(WOS_E_INVALID, "wos_scene_create: device index out of range");
-
-  wos::HostSceneInput in;
-  in.dim = d->dim;
-  in.vertices = d->vertices; in.prims = d->prims; in.n_vertices = d->n_vertices; in.n_prims = d->n_prims;
-  in.dvertices = d->dvertices; in.dprims = d->dprims; in.n_dvertices = d->n_dvertices; in.n_dprims = d->n_dprims;
-  in.is_double_sided = d->is_double_sided;
+  if (device < 0 || device >= ndev || device >= kMaxDevices)
+    return fail(WOS_E_INVALID, "wos_scene_create: device index out of range");
+  HIP_TRY(hipSetDevice(device));
+  std::shared_ptr<Geom> geom;
+  int rc = geom_get(d, device, geom);
+  if (rc != WOS_OK) return rc;
   auto* s = new wos_scene();
-  std::string err;
-  if (!wos::prepare_scene(in, s->host, err)) { delete s; return fail(WOS_E_INVALID, "wos_scene_create: " + err); }
   s->device = device;
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = upload(&s->d_prim, s->host.prim);
-  if (e == hipSuccess) e = upload(&s->d_paux, s->host.paux);
-  if (e == hipSuccess) e = upload(&s->d_sil, s->host.sil);
-  if (e == hipSuccess) e = upload(&s->d_dprim, s->host.dprim);
-  if (e == hipSuccess) e = upload(&s->d_dpaux, s->host.dpaux);
-  if (e == hipSuccess) e = upload(&s->d_pgroup, s->host.pgroup);
-  if (e == hipSuccess) e = upload(&s->d_sgroup, s->host.sgroup);
-  size_t nsrc = 0;
+  s->geom = geom;
   if (d->source) {
-    nsrc = (size_t)d->source_dims[0] * d->source_dims[1] * (d->dim == 3 ? d->source_dims[2] : 1);
-    if (e == hipSuccess) e = hipMalloc((void**)&s->d_source, nsrc * sizeof(float));
+    hipError_t e = hipMalloc((void**)&s->d_source, nsrc * sizeof(float));
     if (e == hipSuccess)
       e = hipMemcpy(s->d_source, d->source, nsrc * sizeof(float),
                     d->source_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      hipFree(s->d_source);
+      delete s;
+      return fail(WOS_E_DEVICE, std::string("wos_scene_create: ") + hipGetErrorString(e));
+    }
+    s->source_cap = nsrc;
   }
-  if (e == hipSuccess) e = hipMalloc((void**)&s->d_counters, wos::kNumCounterSlots * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipEventCreate(&s->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&s->ev1);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&s->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (e != hipSuccess) {
-    std::string msg = std::string("wos_scene_create: ") + hipGetErrorString(e);
-    scene_release(s);
-    delete s;
-    return fail(WOS_E_DEVICE, msg);
-  }
+  const wos::HostScene& h = geom->host;
   wos::DevScene& ds = s->dev;
   ds.dim = d->dim;
-  ds.n_prims = s->host.n_prims;
-  ds.n_sil = s->host.n_sil;
-  ds.n_dprims = s->host.n_dprims;
-  ds.prim = s->d_prim; ds.paux = s->d_paux; ds.sil = s->d_sil; ds.dprim = s->d_dprim; ds.dpaux = s->d_dpaux;
+  ds.n_prims = h.n_prims;
+  ds.n_sil = h.n_sil;
+  ds.n_dprims = h.n_dprims;
+  ds.prim = geom->d_prim; ds.paux = geom->d_paux; ds.sil = geom->d_sil;
+  ds.dprim = geom->d_dprim; ds.dpaux = geom->d_dpaux;
   ds.source = s->d_source;
-  ds.pgroup = s->d_pgroup; ds.sgroup = s->d_sgroup;
-  ds.n_pgroups = s->host.n_pgroups; ds.n_sgroups = s->host.n_sgroups;
+  ds.pgroup = geom->d_pgroup; ds.sgroup = geom->d_sgroup;
+  ds.n_pgroups = h.n_pgroups; ds.n_sgroups = h.n_sgroups;
+  const int nsd = d->dim == 2 ? 2 : 3;
   for (int k = 0; k < 3; k++) {
     ds.sdims[k] = d->source ? (k < nsd ? d->source_dims[k] : 1) : 0;
-    ds.pmin[k] = s->host.pmin[k]; ds.pmax[k] = s->host.pmax[k]; ds.ext[k] = s->host.ext[k];
+    ds.pmin[k] = h.pmin[k]; ds.pmax[k] = h.pmax[k]; ds.ext[k] = h.ext[k];
   }
   ds.absorption = d->absorption;
   ds.g_dirichlet = d->dirichlet_value;
@@ -215,63 +367,127 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   return WOS_OK;
 }
 
+int wos_scene_set_source(wos_scene* s, const float* source, const int32_t* dims, int32_t on_device, void* stream) {
+  if (!s || !source || !dims) return fail(WOS_E_INVALID, "wos_scene_set_source: null argument");
+  size_t nsrc = 0;
+  if (check_source_dims(s->dev.dim, dims, &nsrc) != WOS_OK) return fail(WOS_E_INVALID, "wos_scene_set_source: bad source dims");
+  std::lock_guard<std::mutex> lock(s->mu);
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  DevCtx& c = g_ctx[s->device];
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    HIP_TRY(ctx_order(c, st));  // a solve on another stream may still read the old grid
+  }
+  if (nsrc > s->source_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    hipFree(s->d_source);
+    s->d_source = nullptr;
+    s->source_cap = 0;
+    HIP_TRY(hipMalloc((void**)&s->d_source, nsrc * sizeof(float)));
+    s->source_cap = nsrc;
+  }
+  HIP_TRY(hipMemcpyAsync(s->d_source, source, nsrc * sizeof(float),
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  const int nsd = s->dev.dim == 2 ? 2 : 3;
+  s->dev.source = s->d_source;
+  for (int k = 0; k < 3; k++) s->dev.sdims[k] = k < nsd ? dims[k] : 1;
+  return WOS_OK;
+}
+
 int wos_scene_destroy(wos_scene* s) {
   if (!s) return WOS_OK;
-  scene_release(s);
+  {
+    std::lock_guard<std::mutex> lock(s->mu);
+    hipSetDevice(s->device);
+    DevCtx& c = g_ctx[s->device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.inflight) hipEventSynchronize(c.done);  // an async solve may still read the source
+    hipFree(s->d_source);
+  }
   delete s;
+  return WOS_OK;
+}
+
+int wos_release_caches(int32_t device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  for (int dv = 0; dv < std::min(ndev, kMaxDevices); dv++) {
+    if (device >= 0 && dv != device) continue;
+    DevCtx& c = g_ctx[dv];
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.ready) continue;
+    HIP_TRY(hipSetDevice(dv));
+    HIP_TRY(hipDeviceSynchronize());
+    ctx_free(c);
+  }
+  std::lock_guard<std::mutex> lk(g_geom_mu);
+  if (device < 0) {
+    g_geom_lru.clear();
+  } else {
+    g_geom_lru.erase(std::remove_if(g_geom_lru.begin(), g_geom_lru.end(),
+                                    [&](const std::shared_ptr<Geom>& g) { return g->device == device; }),
+                     g_geom_lru.end());
+  }
   return WOS_OK;
 }
 
 int wos_scene_get_info(const wos_scene* s, wos_scene_info* info) {
   if (!s || !info) return fail(WOS_E_INVALID, "wos_scene_get_info: null argument");
-  info->dim = s->host.dim;
-  info->n_prims = s->host.n_prims;
-  info->n_silhouettes = s->host.n_sil;
-  info->n_dprims = s->host.n_dprims;
+  const wos::HostScene& h = s->geom->host;
+  info->dim = h.dim;
+  info->n_prims = h.n_prims;
+  info->n_silhouettes = h.n_sil;
+  info->n_dprims = h.n_dprims;
   info->device = s->device;
-  for (int k = 0; k < 3; k++) { info->bbox_min[k] = s->host.pmin[k]; info->bbox_max[k] = s->host.pmax[k]; }
+  for (int k = 0; k < 3; k++) { info->bbox_min[k] = h.pmin[k]; info->bbox_max[k] = h.pmax[k]; }
   return WOS_OK;
 }
 
-static int ensure_workspace(wos_scene* s, size_t npts) {
-  if (npts <= s->ws_points) return WOS_OK;
-  const int dim = s->host.dim;
-  hipFree(s->d_pts); hipFree(s->d_p); hipFree(s->d_g); hipFree(s->d_nest); hipFree(s->d_steps);
-  s->d_pts = s->d_p = s->d_g = nullptr; s->d_nest = s->d_steps = nullptr; s->ws_points = 0;
-  size_t cap = npts + npts / 4 + 1024;
-  HIP_TRY(hipMalloc((void**)&s->d_pts, cap * dim * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&s->d_p, cap * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&s->d_g, cap * dim * sizeof(float)));
-  HIP_TRY(hipMalloc((void**)&s->d_nest, cap * sizeof(int32_t)));
-  HIP_TRY(hipMalloc((void**)&s->d_steps, cap * sizeof(int32_t)));
-  s->ws_points = cap;
+}  // extern "C"
+
+namespace {
+
+int ensure_workspace(DevCtx& c, int dim, size_t npts) {
+  if (npts <= c.ws_points) return WOS_OK;
+  hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
+  c.d_pts = c.d_p = c.d_g = nullptr; c.d_nest = c.d_steps = nullptr; c.ws_points = 0;
+  const size_t cap = npts + npts / 4 + 1024;
+  HIP_TRY(hipMalloc((void**)&c.d_pts, cap * 3 * sizeof(float)));  // either dimension
+  HIP_TRY(hipMalloc((void**)&c.d_p, cap * sizeof(float)));
+  HIP_TRY(hipMalloc((void**)&c.d_g, cap * 3 * sizeof(float)));
+  HIP_TRY(hipMalloc((void**)&c.d_nest, cap * sizeof(int32_t)));
+  HIP_TRY(hipMalloc((void**)&c.d_steps, cap * sizeof(int32_t)));
+  (void)dim;
+  c.ws_points = cap;
   return WOS_OK;
 }
 
 // walk tasks per batch: 2^24 tasks = 0.8 GB (2D) / 1.0 GB (3D) of workspace
-static constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
+constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
 
-static int ensure_tasks(wos_scene* s, int64_t tasks, int64_t points) {
-  const int tf = wos::task_floats(s->host.dim);
-  if (tasks > s->task_cap) {
-    hipFree(s->d_tasks);
-    s->d_tasks = nullptr; s->task_cap = 0;
-    HIP_TRY(hipMalloc((void**)&s->d_tasks, (size_t)tasks * tf * sizeof(float)));
-    s->task_cap = tasks;
+int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
+  // sized for 3D records so either dimension fits
+  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
+  if (tasks > c.task_cap) {
+    hipFree(c.d_tasks);
+    c.d_tasks = nullptr; c.task_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c.d_tasks, (size_t)tasks * tf * sizeof(float)));
+    c.task_cap = tasks;
   }
-  if (points > s->pstate_cap) {
-    hipFree(s->d_pstate);
-    s->d_pstate = nullptr; s->pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&s->d_pstate, ((size_t)2 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
-    s->pstate_cap = points;
+  if (points > c.pstate_cap) {
+    hipFree(c.d_pstate);
+    c.d_pstate = nullptr; c.pstate_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)2 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
+    c.pstate_cap = points;
   }
   return WOS_OK;
 }
 
 // SoA views into the task workspace for a batch of T tasks
-static wos::DevTasks task_view(wos_scene* s, int dim, int64_t T, int32_t wpp) {
+wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   wos::DevTasks tk{};
-  float* f = s->d_tasks;
+  float* f = c.d_tasks;
   tk.pt = f; f += dim * T;
   tk.thr = f; f += T;
   tk.tsrc = f; f += T;
@@ -281,17 +497,17 @@ static wos::DevTasks task_view(wos_scene* s, int dim, int64_t T, int32_t wpp) {
   tk.sdir = f; f += dim * T;
   tk.total = f; f += T;
   tk.code = (uint32_t*)f;
-  tk.pstate = s->d_pstate;
-  tk.perm = (uint32_t*)(s->d_pstate + s->pstate_cap);
-  tk.hist = (uint32_t*)(s->d_pstate + 2 * s->pstate_cap);
+  tk.pstate = c.d_pstate;
+  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap);
+  tk.hist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap);
   tk.T = T;
   tk.wpp = wpp;
   return tk;
 }
 
 // state_k = A_k * state_0 + C_k for the PCG32 LCG (multiplier kPcgMult, increment kPcgInc)
-static int ensure_jump(wos_scene* s, int k_needed) {
-  if (k_needed <= s->n_jump) return WOS_OK;
+int ensure_jump(DevCtx& c, int k_needed) {
+  if (k_needed <= c.n_jump) return WOS_OK;
   // >= 2 * 1000 + 2: the wave-cooperative rejection sampler jumps up to 1000 iterations ahead
   const int cap = std::max(k_needed, 4096);
   std::vector<uint64_t> t(2 * (size_t)cap);
@@ -301,40 +517,17 @@ static int ensure_jump(wos_scene* s, int k_needed) {
     A = A * wos::kPcgMult;
     Cc = Cc * wos::kPcgMult + wos::kPcgInc;
   }
-  hipFree(s->d_jump);
-  s->d_jump = nullptr; s->n_jump = 0;
-  HIP_TRY(hipMalloc((void**)&s->d_jump, t.size() * sizeof(uint64_t)));
-  HIP_TRY(hipMemcpy(s->d_jump, t.data(), t.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-  s->n_jump = cap;
+  hipFree(c.d_jump);
+  c.d_jump = nullptr; c.n_jump = 0;
+  HIP_TRY(hipMalloc((void**)&c.d_jump, t.size() * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpy(c.d_jump, t.data(), t.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  c.n_jump = cap;
   return WOS_OK;
 }
 
-// dynamic LDS a workgroup may use: 160 KB per CU minus the kernels' static LDS
-// (rejection jump table 2 KB, counters, histogram)
-static constexpr size_t kLdsDynamicMax = 160 * 1024 - 4096;
+}  // namespace
 
-// LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
-static constexpr size_t kStarGridBudget = 16 * 1024;
-
-static bool star_grid_enabled() {
-  const char* e = std::getenv("WOS_STAR_GRID");  // "0": always the cooperative group scan (A/B runs, tests)
-  return !(e && e[0] == '0');
-}
-
-// (re)build the star grid for the solver's silhouette precision and minR
-static int ensure_star_grid(wos_scene* s, float prec, float min_r) {
-  if (s->sgrid_built && s->sgrid.prec == prec && s->sgrid.min_r == min_r) return WOS_OK;
-  hipFree(s->d_sgrid);
-  s->d_sgrid = nullptr;
-  s->sgrid_ok = wos::build_star_grid(s->host, prec, min_r, kStarGridBudget, s->sgrid);
-  s->sgrid_built = true;
-  if (s->sgrid_ok) {
-    HIP_TRY(hipMalloc((void**)&s->d_sgrid, s->sgrid.words.size() * sizeof(uint32_t)));
-    HIP_TRY(hipMemcpy(s->d_sgrid, s->sgrid.words.data(), s->sgrid.words.size() * sizeof(uint32_t),
-                      hipMemcpyHostToDevice));
-  }
-  return WOS_OK;
-}
+extern "C" {
 
 int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
               int64_t index_stride, float* p, float* grad, int32_t* n_est, int32_t* steps, wos_stats* stats,
@@ -348,9 +541,17 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (!(prm->epsilon_shell >= 0.0f) || !(prm->min_star_radius >= 0.0f) || !(prm->silhouette_precision >= 0.0f))
     return fail(WOS_E_INVALID, "wos_solve: negative tolerance");
   std::lock_guard<std::mutex> lock(s->mu);
-  const int dim = s->host.dim;
+  Geom& geom = *s->geom;
+  const wos::HostScene& host = geom.host;
+  const int dim = host.dim;
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
+  DevCtx& c = g_ctx[s->device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  {
+    int rc = ctx_ready(c, s->device);
+    if (rc != WOS_OK) return rc;
+  }
 
   wos::DevParams dp{};
   const bool anti = !prm->disable_gradient_antithetic_variates;
@@ -374,35 +575,36 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   {
     // diagonal draws + shuffle draws of the stratified samples
     const int k_needed = 2 * (2 * dp.n_pairs) * (dim - 1);
-    int rc = ensure_jump(s, k_needed);
+    int rc = ensure_jump(c, k_needed);
     if (rc != WOS_OK) return rc;
-    dp.jump = s->d_jump;
-    dp.n_jump = s->n_jump;
+    dp.jump = c.d_jump;
+    dp.n_jump = c.n_jump;
   }
 
   // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
   // in the first-ball kernel)
   const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
   const int SS = dim == 2 ? wos::kSilStride2 : wos::kSilStride3;
-  const int primAl = (s->host.n_prims * PS + 3) & ~3;
-  const int silAl = (s->host.n_sil * SS + 3) & ~3;
+  const int primAl = (host.n_prims * PS + 3) & ~3;
+  const int silAl = (host.n_sil * SS + 3) & ~3;
   const int geom_floats =
-      primAl + silAl + wos::kGroupStride * s->host.n_pgroups + wos::kSGroupStride * s->host.n_sgroups;
+      primAl + silAl + wos::kGroupStride * host.n_pgroups + wos::kSGroupStride * host.n_sgroups;
   // the walk kernel also stages the star-radius grid (after the silhouette groups)
   wos::DevScene dsc = s->dev;
   dsc.sgrid = nullptr;
   dsc.sgrid_words = dsc.sgrid_off_words = 0;
-  if (star_grid_enabled() && s->host.n_sil > 0) {
-    int rc = ensure_star_grid(s, prm->silhouette_precision, prm->min_star_radius);
+  if (star_grid_enabled() && host.n_sil > 0) {
+    const Geom::Grid* gr = nullptr;
+    int rc = star_grid(geom, prm->silhouette_precision, prm->min_star_radius, &gr);
     if (rc != WOS_OK) return rc;
-    if (s->sgrid_ok) {
-      dsc.sgrid = s->d_sgrid;
-      dsc.sgrid_words = (int32_t)s->sgrid.words.size();
-      dsc.sgrid_off_words = s->sgrid.off_words;
+    if (gr->ok) {
+      dsc.sgrid = gr->d;
+      dsc.sgrid_words = (int32_t)gr->grid.words.size();
+      dsc.sgrid_off_words = gr->grid.off_words;
       for (int k = 0; k < 3; k++) {
-        dsc.sgrid_n[k] = s->sgrid.n[k];
-        dsc.sgrid_min[k] = s->sgrid.gmin[k];
-        dsc.sgrid_inv[k] = s->sgrid.inv[k];
+        dsc.sgrid_n[k] = gr->grid.n[k];
+        dsc.sgrid_min[k] = gr->grid.gmin[k];
+        dsc.sgrid_inv[k] = gr->grid.inv[k];
       }
     }
   }
@@ -422,6 +624,9 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +
                                     std::to_string(std::max(shmem_fb, shmem_walk)) + " bytes)");
 
+  // the shared workspace may still be in use by a solve enqueued on another stream
+  HIP_TRY(ctx_order(c, st));
+
   const float* d_pts = pts;
   float* d_p = p;
   float* d_g = grad;
@@ -429,94 +634,101 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   int32_t* d_steps = steps;
   const bool dev_ptrs = (flags & WOS_PTRS_DEVICE) != 0;
   if (!dev_ptrs && n > 0) {
-    int rc = ensure_workspace(s, (size_t)n);
+    int rc = ensure_workspace(c, dim, (size_t)n);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(s->d_pts, pts, (size_t)n * dim * sizeof(float), hipMemcpyHostToDevice, st));
-    d_pts = s->d_pts; d_p = s->d_p; d_g = s->d_g;
-    d_nest = n_est ? s->d_nest : nullptr;
-    d_steps = steps ? s->d_steps : nullptr;
+    HIP_TRY(hipMemcpyAsync(c.d_pts, pts, (size_t)n * dim * sizeof(float), hipMemcpyHostToDevice, st));
+    d_pts = c.d_pts; d_p = c.d_p; d_g = c.d_g;
+    d_nest = n_est ? c.d_nest : nullptr;
+    d_steps = steps ? c.d_steps : nullptr;
   }
-  HIP_TRY(hipMemsetAsync(s->d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
 
   // points are solved in batches whose walk tasks fit the task workspace
   const int64_t wpp = (int64_t)dp.n_pairs * dp.n_anti;
   const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
-  int grid_fb = 0, grid_walk = 0;
+  int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;
   if (n > 0) {
-    int rc = ensure_tasks(s, batch * wpp, batch);
+    int rc = ensure_tasks(c, dim, batch * wpp, batch);
     if (rc != WOS_OK) return rc;
-    int bpc = 0;
-    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb, &bpc));
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb, &bpc_fb));
     grid_fb = (int)std::min<int64_t>((batch + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
-                                     (int64_t)std::max(1, bpc) * std::max(1, s->num_cus));
-    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc));
-    grid_walk = std::max(1, bpc) * std::max(1, s->num_cus);
+                                     (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
+    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc_walk));
+    grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
-  unsigned int* q_points = (unsigned int*)(s->d_counters + wos::kNumCounters);
-  unsigned int* q_tasks = (unsigned int*)(s->d_counters + wos::kNumCounters + 1);
+  unsigned int* q_points = (unsigned int*)(c.d_counters + wos::kNumCounters);
+  unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kNumCounters + 1);
   const int64_t n_batches = n > 0 ? (n + batch - 1) / batch : 0;
-  while ((int64_t)s->bev.size() < 4 * n_batches) {
+  while ((int64_t)c.bev.size() < 4 * n_batches) {
     hipEvent_t e = nullptr;
     HIP_TRY(hipEventCreate(&e));
-    s->bev.push_back(e);
+    c.bev.push_back(e);
   }
-  HIP_TRY(hipEventRecord(s->ev0, st));
+  HIP_TRY(hipEventRecord(c.ev0, st));
   for (int64_t b0 = 0; b0 < n; b0 += batch) {
-    hipEvent_t* ev = &s->bev[4 * (b0 / batch)];
+    hipEvent_t* ev = &c.bev[4 * (b0 / batch)];
     const int64_t nb = std::min(batch, n - b0);
-    wos::DevTasks tk = task_view(s, dim, nb * wpp, (int32_t)wpp);
+    wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp);
     const int64_t bbase = index_base + b0 * index_stride;
     if (b0 > 0)
-      HIP_TRY(hipMemsetAsync(s->d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
+      HIP_TRY(hipMemsetAsync(c.d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), st));
     HIP_TRY(hipEventRecord(ev[0], st));
-    HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, s->d_counters,
+    HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
                                     q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, st));
     HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(hipEventRecord(ev[1], st));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
-    HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, s->d_counters, q_tasks, walk_grid,
+    HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
                               shmem_walk, geom_floats_walk, st));
     HIP_TRY(hipEventRecord(ev[2], st));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
                              d_steps ? d_steps + b0 : nullptr, st));
     HIP_TRY(hipEventRecord(ev[3], st));
   }
-  HIP_TRY(hipEventRecord(s->ev1, st));
+  HIP_TRY(hipEventRecord(c.ev1, st));
   if (!dev_ptrs && n > 0) {
     HIP_TRY(hipMemcpyAsync(p, d_p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(grad, d_g, (size_t)n * dim * sizeof(float), hipMemcpyDeviceToHost, st));
     if (n_est) HIP_TRY(hipMemcpyAsync(n_est, d_nest, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (steps) HIP_TRY(hipMemcpyAsync(steps, d_steps, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   }
+  HIP_TRY(hipEventRecord(c.done, st));
+  c.last_stream = st;
+  c.inflight = true;
   if ((flags & WOS_ASYNC) && dev_ptrs) return WOS_OK;
   HIP_TRY(hipStreamSynchronize(st));
+  c.inflight = false;
   wos::diag_dump(dim == 2 ? "2d" : "3d");
   if (stats) {
-    unsigned long long c[wos::kNumCounters];
-    HIP_TRY(hipMemcpy(c, s->d_counters, sizeof(c), hipMemcpyDeviceToHost));
-    stats->walk_steps = c[0];
-    stats->wasted_steps = c[1];
-    stats->walks_recorded = c[2];
-    stats->walks_escaped = c[3];
-    stats->walks_max_length = c[4];
-    stats->walks_rr = c[5];
-    stats->walks_dirichlet = c[6];
-    stats->points_estimated = c[7];
-    stats->rejection_iters = c[8];
+    unsigned long long cnt[wos::kNumCounters];
+    HIP_TRY(hipMemcpy(cnt, c.d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
+    stats->walk_steps = cnt[0];
+    stats->wasted_steps = cnt[1];
+    stats->walks_recorded = cnt[2];
+    stats->walks_escaped = cnt[3];
+    stats->walks_max_length = cnt[4];
+    stats->walks_rr = cnt[5];
+    stats->walks_dirichlet = cnt[6];
+    stats->points_estimated = cnt[7];
+    stats->rejection_iters = cnt[8];
     float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    HIP_TRY(hipEventElapsedTime(&ms, c.ev0, c.ev1));
     stats->kernel_ms = ms;
     stats->first_ball_ms = stats->walk_ms = stats->fold_ms = 0.0;
     stats->walk_launches = (uint64_t)n_batches;
     for (int64_t b = 0; b < n_batches; b++) {
-      hipEvent_t* ev = &s->bev[4 * b];
+      hipEvent_t* ev = &c.bev[4 * b];
       float a = 0.0f, w = 0.0f, f = 0.0f;
       HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
       HIP_TRY(hipEventElapsedTime(&w, ev[1], ev[2]));
       HIP_TRY(hipEventElapsedTime(&f, ev[2], ev[3]));
       stats->first_ball_ms += a; stats->walk_ms += w; stats->fold_ms += f;
     }
+    stats->first_ball_blocks_per_cu = bpc_fb;
+    stats->walk_blocks_per_cu = bpc_walk;
+    stats->walk_lds_bytes = (int32_t)shmem_walk;
+    stats->star_grid = dsc.sgrid != nullptr;
   }
   return WOS_OK;
 }

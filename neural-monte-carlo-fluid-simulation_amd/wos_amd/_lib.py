@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 2  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 3  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
@@ -62,7 +62,8 @@ class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_max_length",
         "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [
-        (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)]
+        (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)] + [
+        (n, C.c_int32) for n in ("first_ball_blocks_per_cu", "walk_blocks_per_cu", "walk_lds_bytes", "star_grid")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n))) for n, t in self._fields_}
@@ -71,8 +72,8 @@ class Stats(C.Structure):
 # exported symbols, exactly those declared in include/wos.h
 EXPORTS = (
     "wos_load_obj", "wos_mesh_free", "wos_scene_create", "wos_scene_destroy",
-    "wos_scene_get_info", "wos_default_params", "wos_solve", "wos_selftest_math",
-    "wos_last_error", "wos_abi_version", "wos_device_count",
+    "wos_scene_get_info", "wos_scene_set_source", "wos_release_caches", "wos_default_params", "wos_solve",
+    "wos_selftest_math", "wos_last_error", "wos_abi_version", "wos_device_count",
 )
 
 _lib = None
@@ -96,6 +97,10 @@ def load():
     L.wos_scene_destroy.argtypes = [C.c_void_p]
     L.wos_scene_get_info.restype = C.c_int
     L.wos_scene_get_info.argtypes = [C.c_void_p, C.POINTER(SceneInfo)]
+    L.wos_scene_set_source.restype = C.c_int
+    L.wos_scene_set_source.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_void_p]
+    L.wos_release_caches.restype = C.c_int
+    L.wos_release_caches.argtypes = [C.c_int32]
     L.wos_default_params.restype = None
     L.wos_default_params.argtypes = [C.POINTER(SolverParams)]
     L.wos_solve.restype = C.c_int

@@ -123,6 +123,35 @@ class WosScene:
         self._h = h
         del keep
 
+    def set_source(self, source, stream=None):
+        """Replace the source grid (-div u) in place: the geometry stays resident.
+        `source` is a numpy array or a torch tensor (a CUDA tensor is copied
+        device-to-device on torch's current stream, no host round trip).  Replaces
+        the reference's per-step Scene(sceneConfig, div) (model_split.py:191)."""
+        L = _lib.load()
+        dims = (C.c_int32 * 3)(0, 0, 0)
+        if _is_torch(source) and source.is_cuda:
+            import torch
+            src = source.detach().to(dtype=torch.float32).contiguous()
+            shape = tuple(src.shape)
+            ptr, on_dev = src.data_ptr(), 1
+            if stream is None:
+                stream = torch.cuda.current_stream(src.device).cuda_stream
+        else:
+            if _is_torch(source):
+                source = source.detach().cpu().numpy()
+            src = np.ascontiguousarray(source, dtype=np.float32)
+            shape = src.shape
+            ptr, on_dev = src.ctypes.data, 0
+        if len(shape) != self.dim:
+            raise WosError(f"source grid must be {self.dim}-D, got shape {shape}")
+        for k in range(len(shape)):
+            dims[k] = int(shape[k])
+        check(L.wos_scene_set_source(self._h, ptr, dims, on_dev, stream), "wos_scene_set_source")
+        # the copy is ordered on `stream`: keep the buffer alive until the next replacement
+        self._src_keep = src
+        self.source_shape = tuple(int(x) for x in shape)
+
     @classmethod
     def from_obj(cls, path, dim, source=None, absorption=0.0, flip_orientation=False, normalize=False, **kw):
         v, ix = load_obj(path, dim, flip_orientation, normalize)
@@ -186,6 +215,12 @@ class WosScene:
             self.close()
         except Exception:
             pass
+
+
+def release_caches(device=-1):
+    """Free the per-device solve workspace and the cached prepared geometries
+    (wos_release_caches); live scenes stay valid."""
+    check(_lib.load().wos_release_caches(int(device)), "wos_release_caches")
 
 
 def selftest_math(which, x, device=0):

@@ -89,6 +89,13 @@ class Scene:
         self.bbox = self._scene.info()
         self.last_stats = None
 
+    def set_source(self, source):
+        """Extension: replace the source grid of this scene in place (a CUDA tensor
+        stays on the device), instead of building a new Scene every step."""
+        if not hasattr(source, "shape"):
+            source = np.asarray(source, dtype=np.float32)
+        self._scene.set_source(source)
+
 
 def wost(scene, solverConfig, outputConfig, pts, return_numpy=False):
     """runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d: returns

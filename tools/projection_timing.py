@@ -1,0 +1,79 @@
+"""Wall time of one pressure projection the way the reference's time-stepper issues it
+(src/2d/models/model_split.py:185-202): a fresh zombie_bindings.Scene(sceneConfig, div)
+every step, then wost(scene, solver, output, pts) -> nested lists, then the gradient
+back to the device (model_split.py:272).  Compared with the device-resident hand-off
+(torch CUDA div + points, results stay on the GPU) and with one scene whose source is
+replaced each step.  GPU box only.
+    python3 tools/projection_timing.py [steps]
+"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "neural-monte-carlo-fluid-simulation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import zombie_bindings  # noqa: E402
+from wos_amd import workloads  # noqa: E402
+
+
+def timed(fn, steps):
+    fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        out.append((time.perf_counter() - t0) * 1e3)
+    return float(np.median(out))
+
+
+def projection_timings(steps=10, n_walks=128):
+    cfg = workloads.karman_config(n_walks=n_walks)
+    scene_cfg = dict(cfg["scene"], boundary=cfg["obj"])
+    solver, output = cfg["solver"], cfg["output"]
+    div_np = np.ascontiguousarray(cfg["source"], np.float32)
+    pts_np = np.ascontiguousarray(cfg["points"], np.float32)
+    dev = torch.device("cuda", 0)
+    div_t = torch.from_numpy(div_np).to(dev)
+    pts_t = torch.from_numpy(pts_np).to(dev)
+    res = {"points": int(pts_np.shape[0]), "source_grid": list(div_np.shape), "walks": solver["nWalks"]}
+
+    # (a) the reference's call pattern: div / points on the host, a fresh Scene per
+    # step, nested lists out, grad p copied back to the device
+    def ref_style():
+        sc = zombie_bindings.Scene(scene_cfg, div_t.cpu().numpy())
+        s, p, g = zombie_bindings.wost(sc, solver, output, pts_t.detach().cpu().numpy())
+        s, p, g = np.array(s), np.array(p), np.array(g)
+        return torch.Tensor(g).to(dev)
+    res["ref_style_ms"] = timed(ref_style, steps)
+
+    def scene_only():
+        return zombie_bindings.Scene(scene_cfg, div_np)
+    res["scene_create_ms"] = timed(scene_only, steps)
+
+    # (b) device hand-off: CUDA div + points, fresh Scene per step, outputs stay on device
+    def dev_style():
+        sc = zombie_bindings.Scene(scene_cfg, div_t)
+        return zombie_bindings.wost(sc, solver, output, pts_t)
+    res["device_fresh_scene_ms"] = timed(dev_style, steps)
+
+    # (c) one scene for the whole run, the source replaced in place each step
+    keep = zombie_bindings.Scene(scene_cfg, div_t)
+
+    def dev_reuse():
+        keep.set_source(div_t)
+        return zombie_bindings.wost(keep, solver, output, pts_t)
+    res["device_scene_reuse_ms"] = timed(dev_reuse, steps)
+    st = keep.last_stats
+    res["kernel_ms"] = st["kernel_ms"]
+    res["walk_steps"] = st["walk_steps"]
+    return res
+
+
+if __name__ == "__main__":
+    print(json.dumps(projection_timings(int(sys.argv[1]) if len(sys.argv) > 1 else 10)), flush=True)

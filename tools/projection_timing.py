@@ -75,5 +75,50 @@ def projection_timings(steps=10, n_walks=128):
     return res
 
 
+def pipeline_timings(steps=5, n_points=65536, n_walks=128, vis_resolution=1000):
+    """The whole projection step of the karman example (examples/karman/run.sh:
+    SIREN 2 x 128 sine, vis_resolution 1000, wost.json solver): SIREN divergence on
+    the grid, the solve at the pressure samples, the projection loss + backward --
+    (a) with the reference's host hand-offs, (b) device-resident (wos_amd.projection)."""
+    from wos_amd import projection as pj
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = workloads.karman_config(n_walks=n_walks, n_points=n_points)
+    size = workloads.scene_size(workloads.KARMAN_OBJ)
+    scene_cfg = dict(cfg["scene"], boundary=cfg["obj"])
+    u = pj.Siren(2, 2, 2, 128).to(dev)
+    u_prev = pj.Siren(2, 2, 2, 128).to(dev)
+    samples = torch.from_numpy(cfg["points"]).to(dev)
+    proj = pj.PressureProjector(scene_cfg, cfg["solver"], cfg["output"], samples)
+    n_loss = 128 * 128  # sample_resolution 128 (run.sh)
+    res = {"points": int(samples.shape[0]), "walks": n_walks, "vis_resolution": vis_resolution}
+
+    def host_step():
+        div = proj.source_from_velocity(u_prev, vis_resolution, size).cpu().numpy()
+        sc = zombie_bindings.Scene(scene_cfg, div)
+        s, p, g = zombie_bindings.wost(sc, cfg["solver"], cfg["output"], samples.detach().cpu().numpy())
+        grad_p = torch.Tensor(np.array(g)).to(dev)
+        loss = proj.projection_loss(u, u_prev, grad_p, n_loss)
+        loss.backward()
+
+    def device_step():
+        div = proj.source_from_velocity(u_prev, vis_resolution, size)
+        p, g = proj.solve(div)
+        loss = proj.projection_loss(u, u_prev, g, n_loss)
+        loss.backward()
+
+    def divergence_only():
+        return proj.source_from_velocity(u_prev, vis_resolution, size)
+
+    res["host_handoff_step_ms"] = timed(host_step, steps)
+    res["device_step_ms"] = timed(device_step, steps)
+    res["siren_divergence_ms"] = timed(divergence_only, steps)
+    res["solve_kernel_ms"] = proj.last_stats["kernel_ms"]
+    return res
+
+
 if __name__ == "__main__":
-    print(json.dumps(projection_timings(int(sys.argv[1]) if len(sys.argv) > 1 else 10)), flush=True)
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    print(json.dumps({"scene_handoff": projection_timings(steps),
+                      "pipeline_64k": pipeline_timings(max(3, steps // 2)),
+                      "pipeline_512sq": pipeline_timings(max(3, steps // 2), n_points=512 * 512)}), flush=True)

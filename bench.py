@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--no-projection-wall", action="store_true")
     return ap.parse_args()
 
 
@@ -225,6 +226,19 @@ def main():
             "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
                                 "fold": float(np.mean(fold_ms)), "total": kms},
         }
+        if world == 1 and not a.no_projection_wall:
+            # the metric's second half: wall time of one whole projection call as the
+            # time-stepper issues it (fresh Scene(sceneConfig, div) + wost, model_split.py:185-202)
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from projection_timing import projection_timings
+            pt = projection_timings(steps=3, n_walks=a.walks)
+            line["projection_wall"] = {
+                "device_handoff_ms": pt["device_fresh_scene_ms"],
+                "reference_handoff_ms": pt["ref_style_ms"],
+                "scene_create_ms": pt["scene_create_ms"],
+                "note": "device: Scene(cfg, div CUDA tensor) + wost(CUDA points), outputs on device; reference: "
+                        "div/points via .cpu().numpy(), nested-list outputs, grad p back to the device",
+            }
         if world == 1 and not a.no_cpu_baseline:
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(cfg, threads, a.cpu_budget_s)

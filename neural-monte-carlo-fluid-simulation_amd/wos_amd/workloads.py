@@ -183,6 +183,30 @@ def cube_config(res=128, n_walks=64, src_res=82):
             "output": dict(OUTPUT_BASE, gridRes=100), "source": src, "points": pts, "obj": CUBE_OBJ}
 
 
+ENGINE_OBJ = os.path.join(SCENES, "engine_geometry.obj")
+
+
+def engine_config(n_walks=64, n_points=4096, flip=False, seed=3):
+    """The largest mesh the reference ships: the zombie demo's engine outline
+    (bindings/zombie/demo/scenes/engine/data/geometry.obj, 647 segments in several
+    loops), loaded with normalizeDomain (scene.h:104-145) and used here as an
+    all-Neumann karman-style problem (lambda = 350, the wost.json solver) -- the
+    capacity case for the LDS-staged kernels (beyond the star-grid limit of 255
+    silhouette candidates).  Uniform random points over the bounding box; about
+    half lie inside the fluid region (either orientation)."""
+    from .engine import load_obj
+    v, ix = load_obj(ENGINE_OBJ, 2, flip, True)
+    lo, hi = v.min(0), v.max(0)
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(lo, hi, (n_points, 2)).astype(np.float32)
+    X, Y = np.meshgrid(np.linspace(lo[0], hi[0], 203), np.linspace(lo[1], hi[1], 203), indexing="xy")
+    src = (np.sin(3 * X) * np.cos(2 * Y) + 0.5 * np.cos(5 * X + 1)).astype(np.float32)
+    solver = dict(SOLVER_BASE, nWalks=n_walks)
+    scene = dict(SCENE_BASE, boundary=ENGINE_OBJ, normalizeDomain=True, flipOrientation=flip)
+    return {"name": "engine2d", "dim": 2, "scene": scene, "solver": solver, "output": dict(OUTPUT_BASE),
+            "source": src, "points": pts, "vertices": v, "prims": ix, "absorption": 350.0, "flip": flip}
+
+
 def gear_config(n_teeth=160, n_walks=64, res=24, holes=3, seed=7):
     """Stress scene for the culling / compaction paths (no reference analogue):
     fluid inside a counter-clockwise gear (2*n_teeth segments alternating between

@@ -167,6 +167,18 @@ def test_gear_many_groups_bit_exact(gpu, oracle):
     _compare(oracle, osc, sc, cfg, cfg["points"])
 
 
+@pytest.mark.parametrize("flip", [False, True])
+def test_engine_mesh_bit_exact(gpu, oracle, flip):
+    """the reference's largest mesh (647 segments, zombie engine demo), normalized:
+    more silhouette candidates than the star grid takes, several loops"""
+    cfg = workloads.engine_config(n_walks=64, n_points=2048, flip=flip)
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0, watertight=True)
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0, watertight=True)
+    _, _, s1 = _compare(oracle, osc, sc, cfg, cfg["points"])
+    assert s1["points_estimated"] > 600
+    sc.close()
+
+
 def test_open_box3d_silhouette_edges_bit_exact(gpu, oracle):
     """3D with silhouette edges (one face of the cube removed -> open edges, like the
     karman3d cube): edge silhouette candidates, 3D cone culling, the cooperative

@@ -35,6 +35,9 @@ def scene_for(name):
         cfg = workloads.cube_config(res=res, n_walks=64)
         v, ix = objparse.load(cfg["obj"], 3)
         return cfg, WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    if name == "engine":
+        cfg = workloads.engine_config(n_walks=128, n_points=65536)
+        return cfg, WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
     if name == "gear":
         cfg = workloads.gear_config(res=256)
         return cfg, WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
@@ -42,7 +45,8 @@ def scene_for(name):
 
 
 def main():
-    names = sys.argv[1:] or ["B_karman64k", "B_karman_grid32k", "C_dirichlet512", "D_cube64", "D_cube128", "gear"]
+    names = sys.argv[1:] or ["B_karman64k", "B_karman_grid32k", "C_dirichlet512", "D_cube64", "D_cube128", "gear",
+                              "engine"]
     dev = torch.device("cuda", 0)
     for name in names:
         cfg, sc = scene_for(name)

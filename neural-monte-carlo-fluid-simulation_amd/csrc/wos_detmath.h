@@ -253,6 +253,63 @@ WOS_HD double bessk1(double x) {
          y * (0.1504268e-1 + y * (-0.780353e-2 + y * (0.325614e-2 + y * (-0.68245e-3)))))));
 }
 
+// I and K of order 0 and/or 1 at the same x >= 0, the shared pieces evaluated once:
+// the operations of bessi0 / bessi1 / bessk0 / bessk1 above, operand for operand, so
+// the values are identical -- y and dexp(x)/sqrt(x) of the I's, dlog(x/2) and
+// I0 / I1 reused by the K's for x <= 2, 2/x and dexp(-x)/sqrt(x) of the K's for
+// x > 2.  (The ball update needs all four at mu R; the Green's function, its
+// gradient and the direction-sampled Poisson kernel need one order at mu r.)
+template <bool N0, bool N1>
+WOS_HD void bessel_ik(double x, double* i0, double* k0, double* i1, double* k1) {
+  const double ax = __builtin_fabs(x);
+  double vi0 = 0.0, vi1 = 0.0;
+  if (ax < 3.75) {
+    double y = x / 3.75;
+    y = y * y;
+    if (N0)
+      vi0 = 1.0 + y * (3.5156229 + y * (3.0899424 + y * (1.2067492 + y * (0.2659732 +
+            y * (0.360768e-1 + y * 0.45813e-2)))));
+    if (N1)
+      vi1 = ax * (0.5 + y * (0.87890594 + y * (0.51498869 + y * (0.15084934 + y * (0.2658733e-1 +
+            y * (0.301532e-2 + y * 0.32411e-3))))));
+  } else {
+    const double y = 3.75 / ax;
+    const double e = dexp(ax) / __builtin_sqrt(ax);
+    if (N0)
+      vi0 = e * (0.39894228 + y * (0.1328592e-1 + y * (0.225319e-2 +
+            y * (-0.157565e-2 + y * (0.916281e-2 + y * (-0.2057706e-1 + y * (0.2635537e-1 +
+            y * (-0.1647633e-1 + y * 0.392377e-2))))))));
+    if (N1) {
+      double ans = 0.2282967e-1 + y * (-0.2895312e-1 + y * (0.1787654e-1 - y * 0.420059e-2));
+      ans = 0.39894228 + y * (-0.3988024e-1 + y * (-0.362018e-2 + y * (0.163801e-2 +
+            y * (-0.1031555e-1 + y * ans))));
+      vi1 = ans * e;
+    }
+  }
+  if (N1 && x < 0.0) vi1 = -vi1;
+  if (x <= 2.0) {
+    const double y = x * x / 4.0;
+    const double l = dlog(x / 2.0);
+    if (N0)
+      *k0 = (-l * vi0) + (-0.57721566 + y * (0.42278420 + y * (0.23069756 +
+            y * (0.3488590e-1 + y * (0.262698e-2 + y * (0.10750e-3 + y * 0.74e-5))))));
+    if (N1)
+      *k1 = (l * vi1) + (1.0 / x) * (1.0 + y * (0.15443144 + y * (-0.67278579 +
+            y * (-0.18156897 + y * (-0.1919402e-1 + y * (-0.110404e-2 + y * (-0.4686e-4)))))));
+  } else {
+    const double y = 2.0 / x;
+    const double e = dexp(-x) / __builtin_sqrt(x);
+    if (N0)
+      *k0 = e * (1.25331414 + y * (-0.7832358e-1 + y * (0.2189568e-1 +
+            y * (-0.1062446e-1 + y * (0.587872e-2 + y * (-0.251540e-2 + y * 0.53208e-3))))));
+    if (N1)
+      *k1 = e * (1.25331414 + y * (0.23498619 + y * (-0.3655620e-1 +
+            y * (0.1504268e-1 + y * (-0.780353e-2 + y * (0.325614e-2 + y * (-0.68245e-3)))))));
+  }
+  if (N0) *i0 = vi0;
+  if (N1) *i1 = vi1;
+}
+
 // ---------------------------------------------------------------------------
 // PCG32 (pcg32.h) + counter-based seeding
 // ---------------------------------------------------------------------------

@@ -695,10 +695,12 @@ struct Gfn {
 #if WOS_ABL_FAST_BESSEL
       A0 = k0_fast(muR); A1 = i0_fast(muR); B0 = k1_fast(muR); B1 = i1_fast(muR);
 #else
-      A0 = (float)bessk0((double)muR);
-      A1 = (float)bessi0((double)muR);
-      B0 = (float)bessk1((double)muR);
-      B1 = (float)bessi1((double)muR);
+      double i0, k0, i1, k1;
+      bessel_ik<true, true>((double)muR, &i0, &k0, &i1, &k1);
+      A0 = (float)k0;
+      A1 = (float)i0;
+      B0 = (float)k1;
+      B1 = (float)i1;
 #endif
     } else {
       float expmuR = fexp(-muR);
@@ -719,8 +721,10 @@ struct Gfn {
     }
     float mur = r * sqrtLambda;
     if constexpr (DIM == 2) {
-      float K0mur = (float)bessk0((double)mur);
-      float I0mur = (float)bessi0((double)mur);
+      double i0, k0;
+      bessel_ik<true, false>((double)mur, &i0, &k0, nullptr, nullptr);
+      float K0mur = (float)k0;
+      float I0mur = (float)i0;
       return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
     } else {
       float expmur = fexp(-mur);
@@ -748,8 +752,10 @@ struct Gfn {
     }
     float mur = r * sqrtLambda;
     if constexpr (DIM == 2) {
-      float K1mur = (float)bessk1((double)mur);
-      float I1mur = (float)bessi1((double)mur);
+      double i1, k1;
+      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
+      float K1mur = (float)k1;
+      float I1mur = (float)i1;
       float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
       return (float)((double)Qr / (kTwoPi * (double)r));
     } else {
@@ -802,8 +808,10 @@ struct Gfn {
 #if WOS_ABL_FAST_BESSEL
       float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
 #else
-      float K1mur = (float)bessk1((double)mur);
-      float I1mur = (float)bessi1((double)mur);
+      double i1, k1;
+      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
+      float K1mur = (float)k1;
+      float I1mur = (float)i1;
 #endif
       float Q = K1mur + I1mur * A0 / A1;
       return mur * Q;
@@ -2594,6 +2602,13 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
     case 15: r = (double)__builtin_sqrtf((float)v); break;
     case 16: r = (double)i0_fast((float)v); break;
     case 17: r = (double)k0_fast((float)v); break;
+    // the fused evaluator of the kernels (bessel_ik) must equal 6..9
+    case 18: { double a, b; bessel_ik<true, false>(v, &r, &a, nullptr, nullptr); (void)b; } break;
+    case 19: { double a; bessel_ik<false, true>(v, nullptr, nullptr, &r, &a); } break;
+    case 20: { double a; bessel_ik<true, false>(v, &a, &r, nullptr, nullptr); } break;
+    case 21: { double a; bessel_ik<false, true>(v, nullptr, nullptr, &a, &r); } break;
+    case 22: { double a, b, c; bessel_ik<true, true>(v, &a, &r, &b, &c); } break;
+    case 23: { double a, b, c; bessel_ik<true, true>(v, &a, &b, &c, &r); } break;
     default: r = __builtin_nan("");
   }
   out[i] = r;

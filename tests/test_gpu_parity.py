@@ -45,6 +45,17 @@ def test_bessel_bit_exact(gpu, oracle, which):
     np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
+@pytest.mark.parametrize("which,ref", [(18, 0), (19, 1), (20, 2), (21, 3), (22, 2), (23, 3)])
+def test_fused_bessel_bit_exact(gpu, oracle, which, ref):
+    """bessel_ik (one evaluation of the shared exp/log/sqrt pieces for I0, I1, K0, K1,
+    as the ball update and the Green's function use it) == the separate A&S functions"""
+    rng = np.random.default_rng(which)
+    x = np.concatenate([rng.uniform(1e-4, 4.0, 5000), rng.uniform(3.7, 120.0, 5000), [2.0, 3.75, 1e-3, 1.9999999]])
+    got = selftest_math(which, x)
+    want = np.array([oracle.lib().oracle_bessel(ref, float(v), 0) for v in x])
+    np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 @pytest.mark.parametrize("which", [10, 11, 12, 13, 14])
 def test_math_float_bit_exact(gpu, oracle, which):
     rng = np.random.default_rng(which)

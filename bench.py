@@ -79,6 +79,21 @@ def measured_traffic(points, walks):
     return best
 
 
+def measured_issue():
+    """Vector-instruction issue of the walk kernel from the committed rocprofv3 SQ
+    pass (tools/collect_sq.py -> profiles/*walk_sq.json), if any."""
+    prof = os.path.join(REPO, "profiles")
+    best = None
+    if os.path.isdir(prof):
+        for f in sorted(os.listdir(prof)):
+            if f.endswith("walk_sq.json"):
+                try:
+                    best = json.load(open(os.path.join(prof, f)))
+                except (OSError, ValueError):
+                    continue
+    return best
+
+
 def cpu_baseline(cfg, n_threads, budget_s):
     """The CPU oracle restatement (oracle/, C + pthreads) timed on this host on a
     bounded, strided sample of the same workload -- a reported baseline only."""
@@ -223,9 +238,15 @@ def main():
                          "algorithmic_bytes_per_launch": wbytes,
                          "traffic_source": tr["source"] if tr else None,
                          "projection_achieved_GBps": pbytes / (kms * 1e-3) / 1e9},
+            "valu_issue": None,
             "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
                                 "fold": float(np.mean(fold_ms)), "total": kms},
         }
+        sq = measured_issue()
+        if sq:
+            line["valu_issue"] = {"kernel": sq["kernel"], "frac": sq["valu_issue_frac"],
+                                  "wait_any_frac": sq["wait_any_frac"], "wait_inst_frac": sq["wait_inst_frac"],
+                                  "source": sq["source"]}
         if world == 1 and not a.no_projection_wall:
             # the metric's second half: wall time of one whole projection call as the
             # time-stepper issues it (fresh Scene(sceneConfig, div) + wost, model_split.py:185-202)

@@ -206,8 +206,13 @@ int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
   return WOS_OK;
 }
 
-// LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
-constexpr size_t kStarGridBudget = 16 * 1024;
+// LDS budget of the star-radius grid (staged by every walk-kernel workgroup);
+// WOS_STAR_GRID_BUDGET (bytes) overrides it for A/B runs
+size_t star_grid_budget() {
+  const char* e = std::getenv("WOS_STAR_GRID_BUDGET");
+  if (e && *e) return (size_t)std::strtoul(e, nullptr, 10);
+  return 16 * 1024;
+}
 
 // dynamic LDS a workgroup may use: 160 KB per CU minus the kernels' static LDS
 // (rejection jump table 2 KB, counters, histogram)
@@ -224,7 +229,7 @@ int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
   for (const Geom::Grid& x : g.grids)
     if (x.prec == prec && x.min_r == min_r) { *out = &x; return WOS_OK; }
   Geom::Grid x{prec, min_r, false, {}, nullptr};
-  x.ok = wos::build_star_grid(g.host, prec, min_r, kStarGridBudget, x.grid);
+  x.ok = wos::build_star_grid(g.host, prec, min_r, star_grid_budget(), x.grid);
   if (x.ok) {
     HIP_TRY(hipMalloc((void**)&x.d, x.grid.words.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(x.d, x.grid.words.data(), x.grid.words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));

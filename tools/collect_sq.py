@@ -1,0 +1,63 @@
+"""Instruction issue of the walk kernel from rocprofv3 SQ counters (GPU box): one
+--pmc pass (8 SQ counters) over `bench.py --steps 2 --warmup 1`, averaged over the
+wos_walk_kernel dispatches and written to gpurun_out/<tag>_walk_sq.json (copy it to
+profiles/ to have bench.py report it as roofline.valu).
+
+The path is bound by neither HBM nor MFMA: the meaningful ceiling
+is the vector-instruction issue rate.  valu_issue_frac = SQ_INSTS_VALU x 4 cycles
+(a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles) / (kernel time x
+2.4 GHz x 256 CUs x 4 SIMDs), the kernel time from the same pass's dispatch
+timestamps; the SQ_WAIT_* split says how much of a wave's life is spent parked on
+memory / LDS waits (s_waitcnt) versus stalled at issue.
+    python3 tools/collect_sq.py [tag]
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
+OUT = os.path.join(REPO, "gpurun_out", f"{TAG}_sq")
+COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+            "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
+CLOCK_HZ, SIMDS = 2.4e9, 256 * 4
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc", *COUNTERS, "-d", OUT, "-o", "sq", "--output-format", "csv", "--",
+           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+           "--no-projection-wall"]
+    subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
+                   stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=300)
+    per, dur = {}, {}
+    for f in glob.glob(os.path.join(OUT, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "wos_walk_kernel" not in r["Kernel_Name"]:
+                continue
+            d = r["Dispatch_Id"]
+            per.setdefault(d, {}).setdefault(r["Counter_Name"], 0.0)
+            per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+            dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    if not per:
+        raise SystemExit(f"no wos_walk_kernel records under {OUT}")
+    n = len(per)
+    mean = {c: sum(p.get(c, 0.0) for p in per.values()) / n for c in COUNTERS}
+    t = sum(dur.values()) / n
+    res = {"kernel": "wos_walk_kernel", "dispatches": n, "kernel_s": t, "counters": mean,
+           "valu_issue_frac": mean["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS),
+           "wait_any_frac": mean["SQ_WAIT_ANY"] / mean["SQ_WAVE_CYCLES"],
+           "wait_inst_frac": mean["SQ_WAIT_INST_ANY"] / mean["SQ_WAVE_CYCLES"],
+           "active_frac": mean["SQ_ACTIVE_INST_ANY"] / mean["SQ_WAVE_CYCLES"],
+           "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass), bench.py --steps 2 --warmup 1; "
+                     "VALU issue = INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs)"}
+    path = os.path.join(REPO, "gpurun_out", f"{TAG}_walk_sq.json")
+    json.dump(res, open(path, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -66,6 +66,8 @@ def main():
                           "walk_ms": st["walk_ms"], "fold_ms": st["fold_ms"], "walk_steps": st["walk_steps"],
                           "wasted_steps": st["wasted_steps"], "steps_per_s": st["walk_steps"] / (st["kernel_ms"] * 1e-3),
                           "rejection_iters": st["rejection_iters"],
+                          "walk_blocks_per_cu": st["walk_blocks_per_cu"], "fb_blocks_per_cu": st["first_ball_blocks_per_cu"],
+                          "walk_lds_bytes": st["walk_lds_bytes"], "star_grid": st["star_grid"],
                           "finite": bool(torch.isfinite(p).all().item() and torch.isfinite(g).all().item())}),
               flush=True)
         sc.close()

@@ -950,8 +950,12 @@ __device__ __forceinline__ float k1_fast(float x) {
 // a 1e-3 margin (far above the A&S polynomial error and the float rounding of the
 // exact path), so u above the bound is the exact test's reject without evaluating
 // r at all.  A non-positive or non-finite bound disables the shortcut.
+#ifndef WOS_QUICK_REJ
+#define WOS_QUICK_REJ 1
+#endif
 template <int DIM>
 __device__ __forceinline__ float rej_quick_bound(float sqrtL, float invNB) {
+  if (!WOS_QUICK_REJ) return 3.0e38f;
   const float C = DIM == 2 ? 0.4670f : 0.3683f;
   const float q = C * invNB / sqrtL;
   return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
@@ -1056,7 +1060,10 @@ __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0
 // The jump constants of the first kRejJumpLds rejection iterations (draw 2j) are
 // staged in LDS by every kernel that samples (stage_rej_jump); later iterations
 // (P ~ 1e-4 per sample) read the global table.
-constexpr int kRejJumpLds = 128;
+#ifndef WOS_REJ_JUMP_LDS
+#define WOS_REJ_JUMP_LDS 128
+#endif
+constexpr int kRejJumpLds = WOS_REJ_JUMP_LDS > 0 ? WOS_REJ_JUMP_LDS : 1;
 __shared__ unsigned long long s_rej_jump[2 * kRejJumpLds];
 
 __device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
@@ -1065,7 +1072,7 @@ __device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
 
 // stream state before rejection iteration j (draw 2j) from stream start s0
 __device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0, int j) {
-  if (j < kRejJumpLds) return s_rej_jump[2 * j] * s0 + s_rej_jump[2 * j + 1];
+  if (WOS_REJ_JUMP_LDS > 0 && j < kRejJumpLds) return s_rej_jump[2 * j] * s0 + s_rej_jump[2 * j + 1];
   return jump_state(prm, s0, 2 * j);
 }
 
@@ -2267,6 +2274,13 @@ constexpr unsigned int kTaskGrab = 256;  // tasks a wave takes from the global q
 #ifndef WOS_PRIO
 #define WOS_PRIO 0
 #endif
+// 1: the staged ring also carries each task's record (pt, throughput, source total,
+// Dirichlet distance), loaded one iteration ahead; 0 (default, measured faster on
+// every config: the staged records cost registers the step needs): only the task
+// index and its point's state are staged, the record is loaded at hand-out
+#ifndef WOS_TASK_RING
+#define WOS_TASK_RING 0
+#endif
 #ifndef WOS_DRAIN
 #define WOS_DRAIN 0
 #endif
@@ -2337,10 +2351,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
       if (mine) {
         s_t = pidx * wpp + (q - qp * wpp);
         s_ok = tk.pstate[pidx] & kPtEstimate;
-        for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
-        s_thr = tk.thr[s_t];
-        s_tsrc = tk.tsrc[s_t];
-        s_dd = tk.dd[s_t];
+        if (WOS_TASK_RING) {
+          for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
+          s_thr = tk.thr[s_t];
+          s_tsrc = tk.tsrc[s_t];
+          s_dd = tk.dd[s_t];
+        }
       }
       S += take;
       wq += (uint32_t)take;
@@ -2368,9 +2384,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
         const int src = (head + (rank < take ? rank : 0)) & (kWave - 1);
         const uint32_t v_t = (uint32_t)__shfl((int)s_t, src);
         const uint32_t v_ok = (uint32_t)__shfl((int)s_ok, src);
-        float v_pt[DIM];
-        for (int kk = 0; kk < DIM; kk++) v_pt[kk] = __shfl(s_pt[kk], src);
-        const float v_thr = __shfl(s_thr, src), v_tsrc = __shfl(s_tsrc, src), v_dd = __shfl(s_dd, src);
+        float v_pt[DIM], v_thr = 0.0f, v_tsrc = 0.0f, v_dd = 0.0f;
+        if (WOS_TASK_RING) {
+          for (int kk = 0; kk < DIM; kk++) v_pt[kk] = __shfl(s_pt[kk], src);
+          v_thr = __shfl(s_thr, src);
+          v_tsrc = __shfl(s_tsrc, src);
+          v_dd = __shfl(s_dd, src);
+        } else if (t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
+          for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];
+          v_thr = tk.thr[v_t];
+          v_tsrc = tk.tsrc[v_t];
+          v_dd = tk.dd[v_t];
+        }
         if (t < 0 && rank < take) {
           t = (int64_t)v_t;
           if (!v_ok) {  // point outside the domain: no walks

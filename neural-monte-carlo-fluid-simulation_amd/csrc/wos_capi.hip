@@ -75,7 +75,9 @@ struct DevCtx {
   hipEvent_t done = nullptr;   // end of the last enqueued solve
   hipStream_t last_stream = nullptr;
   bool inflight = false;       // a solve may still run on last_stream
-  std::vector<hipEvent_t> bev; // per-batch kernel boundary events (4 per batch), grow-only
+  std::vector<hipEvent_t> bev; // per-chunk kernel boundary events (4 per chunk), grow-only
+  hipStream_t aux[wos::kMaxPipes] = {};  // pipelines 1.. (pipeline 0 is the caller's stream)
+  hipEvent_t fork = nullptr, join[wos::kMaxPipes] = {};
 };
 
 constexpr int kMaxDevices = 64;
@@ -88,6 +90,14 @@ void ctx_free(DevCtx& c) {
   if (c.ev1) hipEventDestroy(c.ev1);
   if (c.done) hipEventDestroy(c.done);
   for (hipEvent_t e : c.bev) hipEventDestroy(e);
+  for (int i = 0; i < wos::kMaxPipes; i++) {
+    if (c.aux[i]) hipStreamDestroy(c.aux[i]);
+    if (c.join[i]) hipEventDestroy(c.join[i]);
+    c.aux[i] = nullptr;
+    c.join[i] = nullptr;
+  }
+  if (c.fork) hipEventDestroy(c.fork);
+  c.fork = nullptr;
   c.d_pts = c.d_p = c.d_g = nullptr;
   c.d_nest = c.d_steps = nullptr;
   c.ws_points = 0;
@@ -110,6 +120,11 @@ int ctx_ready(DevCtx& c, int device) {
   HIP_TRY(hipEventCreate(&c.ev0));
   HIP_TRY(hipEventCreate(&c.ev1));
   HIP_TRY(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+  for (int i = 1; i < wos::kMaxPipes; i++) {
+    HIP_TRY(hipStreamCreateWithFlags(&c.aux[i], hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c.join[i], hipEventDisableTiming));
+  }
   c.ready = true;
   return WOS_OK;
 }
@@ -483,16 +498,20 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
   if (points > c.pstate_cap) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)2 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc((void**)&c.d_pstate,
+                      ((size_t)2 * points + 2 * wos::kCostBuckets * wos::kMaxPipes) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
 }
 
-// SoA views into the task workspace for a batch of T tasks
-wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
+// SoA views into the task workspace for a chunk of T tasks: pipeline `pipe` owns
+// tasks [pipe * task_slice, ...) and points [pipe * point_slice, ...) of the workspace
+wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, int64_t task_slice,
+                        int64_t point_slice) {
   wos::DevTasks tk{};
-  float* f = c.d_tasks;
+  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
+  float* f = c.d_tasks + (size_t)pipe * task_slice * tf;
   tk.pt = f; f += dim * T;
   tk.thr = f; f += T;
   tk.tsrc = f; f += T;
@@ -502,9 +521,9 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   tk.sdir = f; f += dim * T;
   tk.total = f; f += T;
   tk.code = (uint32_t*)f;
-  tk.pstate = c.d_pstate;
-  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap);
-  tk.hist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap);
+  tk.pstate = c.d_pstate + pipe * point_slice;
+  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap + pipe * point_slice);
+  tk.hist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
   tk.T = T;
   tk.wpp = wpp;
   return tk;
@@ -648,49 +667,69 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   }
   HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
 
-  // points are solved in batches whose walk tasks fit the task workspace
+  // Points are solved in chunks whose walk tasks fit the task workspace.  With
+  // WOS_SPLIT = S > 1 the chunks are dealt round-robin to S pipelines (the caller's
+  // stream + S-1 internal streams, each with its own workspace slice and queues), so
+  // one chunk's first balls run in the long-walk tail of another chunk's walk kernel.
   const int64_t wpp = (int64_t)dp.n_pairs * dp.n_anti;
-  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
+  int pipes = 1;
+  if (const char* e = std::getenv("WOS_SPLIT")) pipes = std::max(1, std::min(wos::kMaxPipes, std::atoi(e)));
+  const int64_t slice_tasks = kMaxBatchTasks / pipes;
+  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, slice_tasks / wpp));
+  if (pipes > 1 && n > 0) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, (n + pipes - 1) / pipes));
+  const int64_t n_chunks = n > 0 ? (n + chunk - 1) / chunk : 0;
+  if (n_chunks < pipes) pipes = (int)std::max<int64_t>(1, n_chunks);
   int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;
   if (n > 0) {
-    int rc = ensure_tasks(c, dim, batch * wpp, batch);
+    int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
     if (rc != WOS_OK) return rc;
     HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb, &bpc_fb));
-    grid_fb = (int)std::min<int64_t>((batch + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
+    grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
     HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
-  unsigned int* q_points = (unsigned int*)(c.d_counters + wos::kNumCounters);
-  unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kNumCounters + 1);
-  const int64_t n_batches = n > 0 ? (n + batch - 1) / batch : 0;
-  while ((int64_t)c.bev.size() < 4 * n_batches) {
+  while ((int64_t)c.bev.size() < 4 * n_chunks) {
     hipEvent_t e = nullptr;
     HIP_TRY(hipEventCreate(&e));
     c.bev.push_back(e);
   }
   HIP_TRY(hipEventRecord(c.ev0, st));
-  for (int64_t b0 = 0; b0 < n; b0 += batch) {
-    hipEvent_t* ev = &c.bev[4 * (b0 / batch)];
-    const int64_t nb = std::min(batch, n - b0);
-    wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp);
+  if (pipes > 1) {
+    HIP_TRY(hipEventRecord(c.fork, st));
+    for (int i = 1; i < pipes; i++) HIP_TRY(hipStreamWaitEvent(c.aux[i], c.fork, 0));
+  }
+  for (int64_t k = 0; k < n_chunks; k++) {
+    const int pipe = (int)(k % pipes);
+    hipStream_t ps = pipe == 0 ? st : c.aux[pipe];
+    const int64_t b0 = k * chunk;
+    hipEvent_t* ev = &c.bev[4 * k];
+    const int64_t nb = std::min(chunk, n - b0);
+    wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp, pipe, chunk * wpp, chunk);
     const int64_t bbase = index_base + b0 * index_stride;
-    if (b0 > 0)
-      HIP_TRY(hipMemsetAsync(c.d_counters + wos::kNumCounters, 0, 2 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), st));
-    HIP_TRY(hipEventRecord(ev[0], st));
+    unsigned long long* qslot = c.d_counters + wos::kNumCounters + 2 * pipe;
+    unsigned int* q_points = (unsigned int*)qslot;
+    unsigned int* q_tasks = (unsigned int*)(qslot + 1);
+    if (k >= pipes) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), ps));
+    HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), ps));
+    HIP_TRY(hipEventRecord(ev[0], ps));
     HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
-                                    q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, st));
-    HIP_TRY(wos::launch_lpt_order(tk, nb, st));
-    HIP_TRY(hipEventRecord(ev[1], st));
+                                    q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, ps));
+    HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
+    HIP_TRY(hipEventRecord(ev[1], ps));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
     HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
-                              shmem_walk, geom_floats_walk, st));
-    HIP_TRY(hipEventRecord(ev[2], st));
+                              shmem_walk, geom_floats_walk, ps));
+    HIP_TRY(hipEventRecord(ev[2], ps));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
-                             d_steps ? d_steps + b0 : nullptr, st));
-    HIP_TRY(hipEventRecord(ev[3], st));
+                             d_steps ? d_steps + b0 : nullptr, ps));
+    HIP_TRY(hipEventRecord(ev[3], ps));
   }
+  for (int i = 1; i < pipes; i++) {
+    HIP_TRY(hipEventRecord(c.join[i], c.aux[i]));
+    HIP_TRY(hipStreamWaitEvent(st, c.join[i], 0));
+  }
+  const int64_t n_batches = n_chunks;
   HIP_TRY(hipEventRecord(c.ev1, st));
   if (!dev_ptrs && n > 0) {
     HIP_TRY(hipMemcpyAsync(p, d_p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));

@@ -71,7 +71,7 @@ __device__ __forceinline__ void wave_sync() {
 // Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_NUM };
+       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_NUM };
 // slots holding maxima (folded with atomicMax)
 __host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 __device__ unsigned long long g_diag[D_NUM];
@@ -1183,10 +1183,13 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
     }
     int j0 = 0, jacc = -1;
     bool done = !coop;
+    DIAG_COUNT(D_RCALLS, 1);
+    DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
     for (;;) {
       const uint64_t pend = __ballot(!done);
       if (pend == 0) break;
       const int nact = __popcll(pend);
+      DIAG_COUNT(D_RGENS, 1);
       // B consecutive iterations per unfinished lane, at least kRejBmin (fewer
       // generations -- each costs three wave syncs and the owners' scan -- for a
       // few iterations evaluated past an accept)
@@ -1212,8 +1215,10 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
             const uint64_t st = rej_state(prm, L->s0[owner], j);
             const float u = draw_float(st);
             int dcs = 0;
+            DIAG_LANE(D_RITEMS);
             if (u > L->qb[owner]) {
               // certain reject: the radius draw is not needed
+              DIAG_LANE(D_RQUICK);
             } else if constexpr (DIM == 2) {
               const float x = draw_float(st * kPcgMult + kPcgInc);
               dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
@@ -1226,7 +1231,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
                                         L->bound[owner]);
             }
             if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
-            else if (dcs < 0) atomicOr(&L->und[owner], 1u << b);
+            else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
           }
         }
       }
@@ -2711,6 +2716,10 @@ void diag_dump(const char* tag) {
   const double fp = (double)(d[D_FB_PTS] ? d[D_FB_PTS] : 1);
   fprintf(stderr, "[diag %s] first-ball: points %llu cycles/point: setup %.0f lhs %.0f balls %.0f total %.0f\n", tag,
           d[D_FB_PTS], d[D_FB_SETUP] / fp, d[D_FB_LHS] / fp, d[D_FB_BALLS] / fp, d[D_FB_TOTAL] / fp);
+  fprintf(stderr, "[diag %s] rejection: calls %llu, lanes/call %.1f, generations/call %.2f, items/call %.1f, quick-rejected %.1f%%, undecided %.3f%%\n",
+          tag, d[D_RCALLS], (double)d[D_RLANES] / (d[D_RCALLS] ? d[D_RCALLS] : 1), (double)d[D_RGENS] / (d[D_RCALLS] ? d[D_RCALLS] : 1),
+          (double)d[D_RITEMS] / (d[D_RCALLS] ? d[D_RCALLS] : 1), 100.0 * d[D_RQUICK] / (d[D_RITEMS] ? d[D_RITEMS] : 1),
+          100.0 * d[D_RUND] / (d[D_RITEMS] ? d[D_RITEMS] : 1));
   fprintf(stderr, "[diag %s] max cycles/point (first balls) %llu, longest walk %llu steps, longest walk-kernel wave %llu cycles\n",
           tag, d[D_FB_MAX], d[D_WMAXLEN], d[D_WAVEMAX]);
   fprintf(stderr, "[diag %s] star calls %llu: groups visited/call %.2f, candidates/call %.2f, exact/call %.2f\n", tag,

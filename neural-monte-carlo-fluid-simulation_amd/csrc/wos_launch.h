@@ -7,8 +7,11 @@ namespace wos {
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlockHost = 4;
 constexpr int kNumCounters = 9;
-// queue slots after the counters: [kNumCounters] point queue, [kNumCounters + 1] task queue
-constexpr int kNumCounterSlots = kNumCounters + 2;
+// at most this many chunks of points are in flight on concurrent streams (pipelines)
+constexpr int kMaxPipes = 4;
+// queue slots after the counters: per pipeline i, [kNumCounters + 2i] point queue,
+// [kNumCounters + 2i + 1] task queue
+constexpr int kNumCounterSlots = kNumCounters + 2 * kMaxPipes;
 
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,

@@ -8,6 +8,7 @@ do not need the oracle (determinism, shard invariance, finiteness, agreement of
 aggregate statistics with an oracle subset).
 """
 import numpy as np
+import torch
 import pytest
 
 import objparse
@@ -252,6 +253,43 @@ def test_karman_full_size_properties(gpu, oracle):
     np.testing.assert_array_equal(po, p1[sub])
     np.testing.assert_array_equal(go, g1[sub])
     assert s1["walks_recorded"] > 0.9 * 128 * pts.shape[0]
+
+
+@pytest.mark.parametrize("which", ["C_dirichlet512", "D_cube128"])
+def test_full_size_configs_properties(gpu, oracle, which):
+    """BASELINE configs C (Dirichlet obstacle, 512^2 points x 256 walks) and D (cube,
+    128^3 points x 64 walks) at full size: determinism, shard invariance (the strided
+    half solved alone), finiteness, the Dirichlet maximum principle bound, and the
+    oracle on a sparse strided subset, bit for bit."""
+    if which == "C_dirichlet512":
+        cfg = workloads.dirichlet_obstacle_config(n_walks=256, res=512)
+        kw = dict(dvertices=cfg["dvertices"], dprims=cfg["dprims"], dirichlet_value=1.0, watertight=True)
+        osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+        sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+        stride = 4099
+    else:
+        cfg = workloads.cube_config(res=128, n_walks=64)
+        osc, sc = _pair(cfg, oracle, dim=3)
+        stride = 32771
+    pts = np.ascontiguousarray(cfg["points"])
+    prm = solver_params(cfg["solver"], cfg["output"])
+    x = torch.from_numpy(pts).to(torch.device("cuda", 0))
+    p1, g1, s1 = sc.solve(x, prm)
+    p2, g2, _ = sc.solve(x, prm)
+    p1, g1, p2, g2 = (t.cpu().numpy() for t in (p1, g1, p2, g2))
+    np.testing.assert_array_equal(p1.view(np.uint32), p2.view(np.uint32))
+    np.testing.assert_array_equal(g1.view(np.uint32), g2.view(np.uint32))
+    assert np.isfinite(p1).all() and np.isfinite(g1).all()
+    pe, ge, _ = sc.solve(x[1::2].contiguous(), prm, index_base=1, index_stride=2)
+    np.testing.assert_array_equal(pe.cpu().numpy().view(np.uint32), p1[1::2].view(np.uint32))
+    np.testing.assert_array_equal(ge.cpu().numpy().view(np.uint32), g1[1::2].view(np.uint32))
+    sub = np.arange(0, pts.shape[0], stride)
+    prm_o = oracle.make_params(cfg["solver"], cfg["output"], math_mode=0)
+    po, go, _, _, _ = oracle.solve(osc, prm_o, pts[sub], index_base=0, index_stride=stride)
+    assert_bits_equal(p1[sub], po)
+    assert_bits_equal(g1[sub], go)
+    assert s1["walk_steps"] > 0 and s1["points_estimated"] > 0.5 * pts.shape[0]
+    sc.close()
 
 
 @pytest.mark.parametrize("name", ["karman_small", "taylorgreen_small", "box_dirichlet_small", "cube_small"])

@@ -24,6 +24,11 @@
 
 namespace wos {
 
+// 1: the star-grid candidate lists of all lanes are evaluated wave-cooperatively;
+// 0: each lane scans its own cell list sequentially
+#ifndef WOS_CELL_COOP
+#define WOS_CELL_COOP 1
+#endif
 #ifndef WOS_ABL_NO_SIL
 #define WOS_ABL_NO_SIL 0
 #endif
@@ -1739,13 +1744,22 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
       }
     }
   }
-  // lanes inside the star grid scan their cell's short list; the rest (no grid,
-  // outside it) share the wave-cooperative group scan below
+  // lanes inside the star grid take their cell's short candidate list; the rest
+  // (no grid, outside it) share the wave-cooperative group scan below
+  int c_beg = 0, c_end = 0;
+  bool use_cell = false;
   if (need && G.sgrid != nullptr) {
     const int cell = star_cell<DIM>(sc, x);
     if (cell >= 0) {
-      result = star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
-      need = false;
+      if (!WOS_CELL_COOP) {
+        result = star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
+        need = false;
+      } else {
+        const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
+        c_beg = off[cell];
+        c_end = off[cell + 1];
+        use_cell = true;
+      }
     }
   }
   if (__ballot(need) == 0) return result;
@@ -1757,10 +1771,47 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     L->brk[lane] = 0xFFFFFFFFu;
     L->best[lane] = ~0ull;
   }
+  if (WOS_CELL_COOP && __ballot(use_cell) != 0) {
+    // the (lane, candidate) pairs of all cell lists, spread over the wave in windows
+    // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
+    // the longest list; accepted candidates fold into the owner like the group scan
+    const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
+    const uint32_t cnt = use_cell ? (uint32_t)(c_end - c_beg) : 0u;
+    uint32_t incl = cnt;
+    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
+      const uint32_t v = __shfl_up(incl, dlt);
+      if (lane >= dlt) incl += v;
+    }
+    const uint32_t total = __shfl(incl, kWave - 1);
+    const uint32_t first = incl - cnt;
+    constexpr uint32_t kWin = kWave * kStarChunk;
+    for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
+      for (uint32_t i = 0; i < cnt; i++) {
+        const uint32_t q = first + i;
+        if (q >= w0 && q < w0 + kWin) L->list[q - w0] = ((uint32_t)lane << 26) | (uint32_t)lst[c_beg + i];
+      }
+      wave_sync();
+      const uint32_t items = (total - w0) < kWin ? (total - w0) : kWin;
+      for (uint32_t k = lane; k < items; k += kWave) {
+        const uint32_t e = L->list[k];
+        const int owner = (int)(e >> 26);
+        const int sidx = (int)(e & 0x3FFFFFFu);
+        float xo[DIM];
+        for (int q = 0; q < DIM; q++) xo[q] = L->qx[q][owner];
+        float d2;
+        if (star_candidate<DIM>(G, sidx, xo, L->r2[owner], L->flip[owner] != 0u, prec, &d2)) {
+          atomicMin(&L->best[owner], ((unsigned long long)__float_as_uint(d2) << 32) | (0xFFFFFFFFu - (uint32_t)sidx));
+          if (d2 <= L->minR2[owner]) atomicMin(&L->brk[owner], (uint32_t)sidx);
+        }
+      }
+      wave_sync();
+    }
+  }
+  const bool scan_groups = need && !use_cell;
   const int nsg = sc.n_sgroups, ns = sc.n_sil;
-  for (int g0 = 0; g0 < nsg; g0 += kStarChunk) {
+  for (int g0 = 0; g0 < nsg && __ballot(scan_groups) != 0; g0 += kStarChunk) {
     uint32_t mask = 0;
-    if (need) {
+    if (scan_groups) {
       const int gn = (nsg - g0) < kStarChunk ? (nsg - g0) : kStarChunk;
       for (int j = 0; j < gn; j++) {
         const float* B = G.sgroup + (g0 + j) * kSGroupStride;

@@ -144,7 +144,7 @@ struct Geom {
   std::vector<int32_t> ix, dix;
   wos::HostScene host;
   float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
-  float *d_pgroup = nullptr, *d_sgroup = nullptr;
+  float *d_pgroup = nullptr, *d_sgroup = nullptr, *d_dgroup = nullptr;
   std::mutex mu;  // star grids
   struct Grid {
     float prec, min_r;
@@ -156,7 +156,7 @@ struct Geom {
   ~Geom() {
     hipSetDevice(device);
     hipFree(d_prim); hipFree(d_paux); hipFree(d_sil); hipFree(d_dprim); hipFree(d_dpaux);
-    hipFree(d_pgroup); hipFree(d_sgroup);
+    hipFree(d_pgroup); hipFree(d_sgroup); hipFree(d_dgroup);
     for (Grid& g : grids) hipFree(g.d);
   }
 };
@@ -211,6 +211,7 @@ int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
   HIP_TRY(upload(&g->d_dprim, g->host.dprim));
   HIP_TRY(upload(&g->d_dpaux, g->host.dpaux));
   HIP_TRY(upload(&g->d_pgroup, g->host.pgroup));
+  HIP_TRY(upload(&g->d_dgroup, g->host.dgroup));
   HIP_TRY(upload(&g->d_sgroup, g->host.sgroup));
   {
     std::lock_guard<std::mutex> lk(g_geom_mu);
@@ -372,8 +373,8 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   ds.prim = geom->d_prim; ds.paux = geom->d_paux; ds.sil = geom->d_sil;
   ds.dprim = geom->d_dprim; ds.dpaux = geom->d_dpaux;
   ds.source = s->d_source;
-  ds.pgroup = geom->d_pgroup; ds.sgroup = geom->d_sgroup;
-  ds.n_pgroups = h.n_pgroups; ds.n_sgroups = h.n_sgroups;
+  ds.pgroup = geom->d_pgroup; ds.sgroup = geom->d_sgroup; ds.dgroup = geom->d_dgroup;
+  ds.n_pgroups = h.n_pgroups; ds.n_sgroups = h.n_sgroups; ds.n_dgroups = h.n_dgroups;
   const int nsd = d->dim == 2 ? 2 : 3;
   for (int k = 0; k < 3; k++) {
     ds.sdims[k] = d->source ? (k < nsd ? d->source_dims[k] : 1) : 0;
@@ -632,7 +633,9 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
       }
     }
   }
-  int geom_floats_walk = geom_floats + ((dsc.sgrid_words + 3) & ~3);
+  // ... and the Dirichlet primitives with their culling boxes (after the grid)
+  const int dir_floats = ((host.n_dprims * PS + 3) & ~3) + wos::kGroupStride * host.n_dgroups;
+  int geom_floats_walk = geom_floats + ((dsc.sgrid_words + 3) & ~3) + dir_floats;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   const size_t shmem_fb =
       (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
@@ -641,8 +644,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (dsc.sgrid != nullptr && shmem_walk > kLdsDynamicMax) {  // no room: the group scan alone
     dsc.sgrid = nullptr;
     dsc.sgrid_words = dsc.sgrid_off_words = 0;
-    geom_floats_walk = geom_floats;
-    shmem_walk = (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+    geom_floats_walk = geom_floats + dir_floats;
+    shmem_walk = (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
   }
   if (std::max(shmem_fb, shmem_walk) > kLdsDynamicMax)
     return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +

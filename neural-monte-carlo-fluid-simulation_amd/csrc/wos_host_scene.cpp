@@ -257,6 +257,13 @@ bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
     add_box(out.pgroup, pts);
     out.n_pgroups++;
   }
+  for (int g0 = 0; g0 < out.n_dprims; g0 += kGroup) {
+    std::vector<const float*> pts;
+    for (int p = g0; p < std::min(out.n_dprims, g0 + kGroup); p++)
+      for (int c = 0; c < in.dim; c++) pts.push_back(dir.v[dir.ix[p][c]].x);
+    add_box(out.dgroup, pts);
+    out.n_dgroups++;
+  }
   const int SS = in.dim == 2 ? kSilStride2 : kSilStride3;
   for (int g0 = 0; g0 < out.n_sil; g0 += kGroup) {
     const int g1 = std::min(out.n_sil, g0 + kGroup);

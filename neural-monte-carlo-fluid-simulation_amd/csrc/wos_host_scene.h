@@ -26,8 +26,8 @@ struct HostScene {
   int dim = 2;
   int n_prims = 0, n_sil = 0, n_dprims = 0;
   std::vector<float> prim, paux, sil, dprim, dpaux;
-  std::vector<float> pgroup, sgroup;  // culling boxes (kGroupStride floats each)
-  int n_pgroups = 0, n_sgroups = 0;
+  std::vector<float> pgroup, sgroup, dgroup;  // culling boxes (kGroupStride floats each)
+  int n_pgroups = 0, n_sgroups = 0, n_dgroups = 0;
   float pmin[3] = {0, 0, 0}, pmax[3] = {0, 0, 0}, ext[3] = {0, 0, 0};
 };
 

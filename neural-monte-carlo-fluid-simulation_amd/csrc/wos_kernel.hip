@@ -287,6 +287,42 @@ __device__ __forceinline__ float bbox_far_dist(const DevScene& sc, const float* 
 }
 
 // per-lane (non-cooperative) closest distance to the Dirichlet boundary
+// Squared distance from x to a padded group box: below the computed distance of
+// every member (the padding dwarfs the rounding of both), so skipping a group whose
+// bound exceeds the running minimum never skips the scan's result.
+template <int DIM>
+__device__ __forceinline__ float box_dist2(const float* B, const float* x) {
+  float d2 = 0.0f;
+  for (int k = 0; k < DIM; k++) {
+    const float e = smax(smax(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
+    d2 += e * e;
+  }
+  return d2;
+}
+
+// computeDistToDirichlet (fcpw_scene_loader.h:299-315) over the Dirichlet
+// primitives in LDS, groups of kGroup culled by their boxes: the sequential `<=`
+// scan's result (the last primitive attaining the minimum computed d^2), as
+// dirichlet_dist_lane, without visiting groups that cannot attain it.
+template <int DIM>
+__device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, const float* dgroup,
+                                       const float* x) {
+  if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
+  constexpr int PS = Layout<DIM>::prim;
+  float sr2 = kFltMax, best = kFltMax;
+  for (int gi = 0; gi < sc.n_dgroups; gi++) {
+    if (box_dist2<DIM>(dgroup + gi * kGroupStride, x) > sr2) continue;
+    const int p1 = (gi + 1) * kGroup < sc.n_dprims ? (gi + 1) * kGroup : sc.n_dprims;
+    for (int p = gi * kGroup; p < p1; p++) {
+      float pt[DIM], t0, t1;
+      float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
+      float d2 = d * d;
+      if (d2 <= sr2) { sr2 = d2; best = d; }
+    }
+  }
+  return best;
+}
+
 template <int DIM>
 __device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
   if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
@@ -368,6 +404,8 @@ struct LGeom {
   const float* sgroup;
   const uint32_t* sgrid;  // star-radius cell grid (u16 offsets | u8 lists), nullptr if none
   int sgrid_off_words;
+  const float* dprim;     // Dirichlet primitives + their culling boxes (walk kernel)
+  const float* dgroup;
 };
 
 // Certain rejection of a whole group for a ray segment [o, o + rt*dir]: slab
@@ -1453,7 +1491,8 @@ __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParam
 
 // after the source sample (walk_on_stars.h:270-327)
 template <int DIM>
-__device__ __forceinline__ int walk_step_tail(const DevScene& sc, const DevParams& prm, float& dirichletDist,
+__device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G, const DevParams& prm,
+                                              float& dirichletDist,
                                               Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, const float* dir,
                                               bool hit, const Hit& ip, const float* sp) {
   if (!prm.ignore_source) {
@@ -1475,7 +1514,7 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const DevParam
   st.walkLength++;
   if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
   if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
-  dirichletDist = dirichlet_dist_lane<DIM>(sc, st.pt);
+  dirichletDist = dirichlet_dist_culled<DIM>(sc, G.dprim, G.dgroup, st.pt);
   return -1;
 }
 
@@ -2156,6 +2195,11 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
   uint32_t* gw = reinterpret_cast<uint32_t*>(smem + primAl + silAl + pgN + sgN);
   G.sgrid = (with_sil && sc.sgrid != nullptr) ? gw : nullptr;
   G.sgrid_off_words = sc.sgrid_off_words;
+  const int sgridAl = sc.sgrid != nullptr ? ((sc.sgrid_words + 3) & ~3) : 0;
+  const int dpN = sc.n_dprims * PS, dpAl = (dpN + 3) & ~3, dgN = sc.n_dgroups * kGroupStride;
+  float* dbase = smem + primAl + silAl + pgN + sgN + sgridAl;
+  G.dprim = with_sil ? dbase : sc.dprim;
+  G.dgroup = with_sil ? dbase + dpAl : sc.dgroup;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
   if (with_sil) {
     for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
@@ -2163,6 +2207,8 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
     for (int i = threadIdx.x; i < sgN; i += kBlock) smem[primAl + silAl + pgN + i] = sc.sgroup[i];
     if (sc.sgrid != nullptr)
       for (int i = threadIdx.x; i < sc.sgrid_words; i += kBlock) gw[i] = sc.sgrid[i];
+    for (int i = threadIdx.x; i < dpN; i += kBlock) dbase[i] = sc.dprim[i];
+    for (int i = threadIdx.x; i < dgN; i += kBlock) dbase[dpAl + i] = sc.dgroup[i];
   }
   return G;
 }
@@ -2528,7 +2574,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
     if (!prm.ignore_source)
       sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, &c_iters, false, rejL, lane);
     DIAG_ADD(D_SAMPLE, t_smp);
-    if (live) code = walk_step_tail<DIM>(sc, prm, ddist, ws, g, st, dir, hit, ip, sp);
+    if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
     DIAG_ADD(D_STEP, t_step);
     if (t >= 0 && code >= 0) {
       const bool recorded = code == WC_DIRICHLET || code == WC_RR;

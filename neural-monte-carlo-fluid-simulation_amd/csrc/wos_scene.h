@@ -50,7 +50,8 @@ struct DevScene {
   const float* source;
   const float* pgroup;   // n_pgroups boxes over consecutive Neumann primitives
   const float* sgroup;   // n_sgroups boxes over consecutive silhouette candidates
-  int32_t n_pgroups, n_sgroups;
+  const float* dgroup;   // n_dgroups boxes over consecutive Dirichlet primitives
+  int32_t n_pgroups, n_sgroups, n_dgroups;
   int32_t sdims[3];
   float pmin[3], pmax[3], ext[3];
   float absorption;

@@ -2176,7 +2176,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
     }
     tk.thr[t] = throughput;
     tk.tsrc[t] = totalSource;
-    tk.dd[t] = dirichlet_dist_lane<DIM>(sc, g.ySurf);
+    tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
   }
 }
 

@@ -76,7 +76,7 @@ __device__ __forceinline__ void wave_sync() {
 // Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_NUM };
+       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_MID, D_END, D_TAIL, D_NUM };
 // slots holding maxima (folded with atomicMax)
 __host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 __device__ unsigned long long g_diag[D_NUM];
@@ -301,23 +301,34 @@ __device__ __forceinline__ float box_dist2(const float* B, const float* x) {
 }
 
 // computeDistToDirichlet (fcpw_scene_loader.h:299-315) over the Dirichlet
-// primitives in LDS, groups of kGroup culled by their boxes: the sequential `<=`
-// scan's result (the last primitive attaining the minimum computed d^2), as
-// dirichlet_dist_lane, without visiting groups that cannot attain it.
+// primitives, groups of kGroup culled by their boxes.  The sequential `<=` scan
+// returns d of the highest-index primitive attaining the minimum computed d^2;
+// here the group with the smallest box bound is evaluated first (a tight running
+// minimum), then every other group whose bound does not exceed it, keeping
+// (min d^2, highest index) -- the same primitive, hence the same d.
 template <int DIM>
 __device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, const float* dgroup,
                                        const float* x) {
   if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
   constexpr int PS = Layout<DIM>::prim;
+  const int ng = sc.n_dgroups;
+  int g0 = 0;
+  float lb0 = kFltMax;
+  for (int gi = 0; gi < ng; gi++) {
+    const float lb = box_dist2<DIM>(dgroup + gi * kGroupStride, x);
+    if (lb < lb0) { lb0 = lb; g0 = gi; }
+  }
   float sr2 = kFltMax, best = kFltMax;
-  for (int gi = 0; gi < sc.n_dgroups; gi++) {
-    if (box_dist2<DIM>(dgroup + gi * kGroupStride, x) > sr2) continue;
+  int bestp = -1;
+  for (int k = 0; k < ng; k++) {
+    const int gi = k == 0 ? g0 : (k <= g0 ? k - 1 : k);
+    if (k > 0 && box_dist2<DIM>(dgroup + gi * kGroupStride, x) > sr2) continue;
     const int p1 = (gi + 1) * kGroup < sc.n_dprims ? (gi + 1) * kGroup : sc.n_dprims;
     for (int p = gi * kGroup; p < p1; p++) {
       float pt[DIM], t0, t1;
-      float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
-      float d2 = d * d;
-      if (d2 <= sr2) { sr2 = d2; best = d; }
+      const float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
+      const float d2 = d * d;
+      if (d2 < sr2 || (d2 == sr2 && p > bestp)) { sr2 = d2; best = d; bestp = p; }
     }
   }
   return best;
@@ -2557,7 +2568,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
     const bool live = t >= 0 && code < 0;
     float dir[DIM], org[DIM], starR = 0.0f;
     for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
+    DIAG_T0(t_mid);
     if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org);
+    DIAG_ADD(D_MID, t_mid);
     Hit ip;
     DIAG_T0(t_ray);
 #if WOS_RAY_WAVE
@@ -2567,14 +2580,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
                      ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
 #endif
     DIAG_ADD(D_RAY, t_ray);
+    DIAG_T0(t_end);
     if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
+    DIAG_ADD(D_END, t_end);
     float sp[DIM], pdf_unused;
     for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
     DIAG_T0(t_smp);
     if (!prm.ignore_source)
       sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, &c_iters, false, rejL, lane);
     DIAG_ADD(D_SAMPLE, t_smp);
+    DIAG_T0(t_tail);
     if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
+    DIAG_ADD(D_TAIL, t_tail);
     DIAG_ADD(D_STEP, t_step);
     if (t >= 0 && code >= 0) {
       const bool recorded = code == WC_DIRICHLET || code == WC_RR;
@@ -2813,6 +2830,9 @@ void diag_dump(const char* tag) {
   const double fp = (double)(d[D_FB_PTS] ? d[D_FB_PTS] : 1);
   fprintf(stderr, "[diag %s] first-ball: points %llu cycles/point: setup %.0f lhs %.0f balls %.0f total %.0f\n", tag,
           d[D_FB_PTS], d[D_FB_SETUP] / fp, d[D_FB_LHS] / fp, d[D_FB_BALLS] / fp, d[D_FB_TOTAL] / fp);
+  fprintf(stderr, "[diag %s] step parts cycles/iter: mid (ball update) %.0f  end %.0f  tail %.0f\n", tag,
+          (double)d[D_MID] / (d[D_ITERS] ? d[D_ITERS] : 1), (double)d[D_END] / (d[D_ITERS] ? d[D_ITERS] : 1),
+          (double)d[D_TAIL] / (d[D_ITERS] ? d[D_ITERS] : 1));
   fprintf(stderr, "[diag %s] rejection: calls %llu, lanes/call %.1f, generations/call %.2f, items/call %.1f, quick-rejected %.1f%%, undecided %.3f%%\n",
           tag, d[D_RCALLS], (double)d[D_RLANES] / (d[D_RCALLS] ? d[D_RCALLS] : 1), (double)d[D_RGENS] / (d[D_RCALLS] ? d[D_RCALLS] : 1),
           (double)d[D_RITEMS] / (d[D_RCALLS] ? d[D_RCALLS] : 1), 100.0 * d[D_RQUICK] / (d[D_RITEMS] ? d[D_RITEMS] : 1),

@@ -141,7 +141,9 @@ typedef struct wos_stats {
     int32_t first_ball_blocks_per_cu;  /* occupancy of the launches (256-thread workgroups per CU) */
     int32_t walk_blocks_per_cu;
     int32_t walk_lds_bytes;     /* dynamic LDS per walk-kernel workgroup */
-    int32_t star_grid;          /* 1: the star-radius cell grid was staged */
+    int32_t star_grid;          /* 1: the star-radius cell grid was used */
+    int32_t geom_global;        /* 1: geometry read from global memory (too large for LDS) */
+    int32_t reserved;
 } wos_stats;
 
 /* Replaces runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d

@@ -647,9 +647,23 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     geom_floats_walk = geom_floats + dir_floats;
     shmem_walk = (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
   }
-  if (std::max(shmem_fb, shmem_walk) > kLdsDynamicMax)
-    return fail(WOS_E_CAPACITY, "wos_solve: scene + nWalks exceed the LDS budget of the staged kernels (" +
-                                    std::to_string(std::max(shmem_fb, shmem_walk)) + " bytes)");
+  // scenes beyond the LDS budget (or WOS_GEOM_GLOBAL=1): geometry read from global
+  // memory through L2, LDS for the per-wave scratch only
+  wos::DevScene dfb = s->dev;
+  int geom_floats_fb = geom_floats;
+  size_t shmem_fb_launch = shmem_fb;
+  const char* gg = std::getenv("WOS_GEOM_GLOBAL");
+  if ((gg && gg[0] == '1') || std::max(shmem_fb, shmem_walk) > kLdsDynamicMax) {
+    dfb.geom_global = 1;
+    dsc.geom_global = 1;
+    geom_floats_fb = 0;
+    geom_floats_walk = 0;
+    shmem_fb_launch = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
+    shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+    if (std::max(shmem_fb_launch, shmem_walk) > kLdsDynamicMax)
+      return fail(WOS_E_CAPACITY, "wos_solve: nWalks exceed the LDS budget of the first-ball kernel (" +
+                                      std::to_string(shmem_fb_launch) + " bytes)");
+  }
 
   // the shared workspace may still be in use by a solve enqueued on another stream
   HIP_TRY(ctx_order(c, st));
@@ -686,7 +700,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (n > 0) {
     int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb, &bpc_fb));
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb_launch, &bpc_fb));
     grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
     HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc_walk));
@@ -716,8 +730,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     if (k >= pipes) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), ps));
     HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), ps));
     HIP_TRY(hipEventRecord(ev[0], ps));
-    HIP_TRY(wos::launch_first_balls(dim, s->dev, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
-                                    q_points, grid_fb, shmem_fb, geom_floats, lhs_floats, ps));
+    HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
+                                    q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, ps));
     HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
     HIP_TRY(hipEventRecord(ev[1], ps));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
@@ -776,6 +790,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     stats->walk_blocks_per_cu = bpc_walk;
     stats->walk_lds_bytes = (int32_t)shmem_walk;
     stats->star_grid = dsc.sgrid != nullptr;
+    stats->geom_global = dsc.geom_global;
   }
   return WOS_OK;
 }

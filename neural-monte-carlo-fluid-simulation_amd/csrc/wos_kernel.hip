@@ -2199,6 +2199,17 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
   const int primAl = (primN + 3) & ~3, silAl = (silN + 3) & ~3;
   const int pgN = sc.n_pgroups * kGroupStride, sgN = sc.n_sgroups * kSGroupStride;
   LGeom G;
+  if (sc.geom_global) {  // too large for LDS: the same records, read through L2
+    G.prim = sc.prim;
+    G.sil = sc.sil;
+    G.pgroup = sc.pgroup;
+    G.sgroup = sc.sgroup;
+    G.sgrid = with_sil ? sc.sgrid : nullptr;
+    G.sgrid_off_words = sc.sgrid_off_words;
+    G.dprim = sc.dprim;
+    G.dgroup = sc.dgroup;
+    return G;
+  }
   G.prim = smem;
   G.sil = smem + primAl;
   G.pgroup = smem + primAl + silAl;
@@ -2246,14 +2257,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
   __shared__ uint32_t s_hist[kCostBuckets];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  stage_geometry<DIM>(sc, smem, false);
+  const LGeom Gfb = stage_geometry<DIM>(sc, smem, false);
   stage_rej_jump(prm);
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
-  const float* Lprim = smem;
+  const float* Lprim = Gfb.prim;
   float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
   int* partner = (int*)(strat + lhs_floats);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);

@@ -52,6 +52,9 @@ struct DevScene {
   const float* sgroup;   // n_sgroups boxes over consecutive silhouette candidates
   const float* dgroup;   // n_dgroups boxes over consecutive Dirichlet primitives
   int32_t n_pgroups, n_sgroups, n_dgroups;
+  // 1: the kernels read the geometry records from global memory (L2) instead of
+  // staging them in LDS -- scenes too large for the LDS budget (set per solve)
+  int32_t geom_global;
   int32_t sdims[3];
   float pmin[3], pmax[3], ext[3];
   float absorption;

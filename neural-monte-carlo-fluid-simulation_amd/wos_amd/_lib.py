@@ -63,7 +63,8 @@ class Stats(C.Structure):
         "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_max_length",
         "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [
         (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)] + [
-        (n, C.c_int32) for n in ("first_ball_blocks_per_cu", "walk_blocks_per_cu", "walk_lds_bytes", "star_grid")]
+        (n, C.c_int32) for n in ("first_ball_blocks_per_cu", "walk_blocks_per_cu", "walk_lds_bytes", "star_grid",
+                                 "geom_global", "reserved")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n))) for n, t in self._fields_}

@@ -255,6 +255,46 @@ def test_karman_full_size_properties(gpu, oracle):
     assert s1["walks_recorded"] > 0.9 * 128 * pts.shape[0]
 
 
+@pytest.mark.parametrize("scene", ["karman", "gear", "cube", "dirichlet"])
+def test_geometry_from_global_memory_bit_exact(gpu, oracle, scene, monkeypatch):
+    """WOS_GEOM_GLOBAL=1: the kernels read the geometry records through L2 instead of
+    staging them in LDS (the path of scenes too large for LDS) -- same results."""
+    monkeypatch.setenv("WOS_GEOM_GLOBAL", "1")
+    if scene == "karman":
+        cfg = workloads.karman_config(n_walks=64)
+        osc, sc = _pair(cfg, oracle)
+        pts = cfg["points"][:512]
+    elif scene == "gear":
+        cfg = workloads.gear_config(n_walks=32, res=16)
+        osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+        sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+        pts = cfg["points"]
+    elif scene == "cube":
+        cfg = workloads.cube_config(res=8, n_walks=32)
+        osc, sc = _pair(cfg, oracle, dim=3)
+        pts = cfg["points"]
+    else:
+        cfg = workloads.dirichlet_obstacle_config(n_walks=64, res=16)
+        kw = dict(dvertices=cfg["dvertices"], dprims=cfg["dprims"], dirichlet_value=1.0, watertight=True)
+        osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+        sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+        pts = cfg["points"]
+    _, _, st = _compare(oracle, osc, sc, cfg, pts)
+    assert st["geom_global"] == 1
+    sc.close()
+
+
+def test_mesh_beyond_lds_bit_exact(gpu, oracle):
+    """a 12 000-segment boundary (192 KB of records: more than a CU's LDS) runs with
+    the geometry in global memory and matches the oracle"""
+    cfg = workloads.gear_config(n_teeth=6000, n_walks=16, res=6)
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], watertight=True)
+    _, _, st = _compare(oracle, osc, sc, cfg, cfg["points"])
+    assert st["geom_global"] == 1 and st["points_estimated"] > 0
+    sc.close()
+
+
 @pytest.mark.parametrize("which", ["C_dirichlet512", "D_cube128"])
 def test_full_size_configs_properties(gpu, oracle, which):
     """BASELINE configs C (Dirichlet obstacle, 512^2 points x 256 walks) and D (cube,

@@ -3,7 +3,7 @@
 #   tools/ab.sh "old ring1 ring4" "B_karman64k D_cube64"
 # Each (variant, config) runs twice in its own process; prints one JSON line per run.
 cd "$(dirname "$0")/.."
-for rnd in 1 2; do
+for rnd in $(seq 1 ${ROUNDS:-2}); do
   for v in $1; do
     for c in $2; do
       echo -n "$v "

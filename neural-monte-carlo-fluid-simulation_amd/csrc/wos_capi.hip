@@ -700,10 +700,10 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (n > 0) {
     int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, shmem_fb_launch, &bpc_fb));
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb));
     grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
-    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, shmem_walk, &bpc_walk));
+    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
   while ((int64_t)c.bev.size() < 4 * n_chunks) {

@@ -2192,14 +2192,14 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
 }
 
 // LDS image: prims | silhouettes | prim groups | silhouette groups (each block 16-B aligned)
-template <int DIM>
+template <int DIM, bool GG>
 __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
   constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
   const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
   const int primAl = (primN + 3) & ~3, silAl = (silN + 3) & ~3;
   const int pgN = sc.n_pgroups * kGroupStride, sgN = sc.n_sgroups * kSGroupStride;
   LGeom G;
-  if (sc.geom_global) {  // too large for LDS: the same records, read through L2
+  if constexpr (GG) {  // too large for LDS: the same records, read through L2
     G.prim = sc.prim;
     G.sil = sc.sil;
     G.pgroup = sc.pgroup;
@@ -2248,7 +2248,7 @@ enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
 #ifndef WOS_FB_WAVES_PER_EU
 #define WOS_FB_WAVES_PER_EU 1
 #endif
-template <int DIM>
+template <int DIM, bool GG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
@@ -2257,7 +2257,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
   __shared__ uint32_t s_hist[kCostBuckets];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const LGeom Gfb = stage_geometry<DIM>(sc, smem, false);
+  const LGeom Gfb = stage_geometry<DIM, GG>(sc, smem, false);
   stage_rej_jump(prm);
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
 #if WOS_DIAG
@@ -2412,14 +2412,14 @@ constexpr unsigned int kTaskGrab = 256;  // tasks a wave takes from the global q
 #ifndef WOS_WALK_WAVES_PER_EU
 #define WOS_WALK_WAVES_PER_EU 4
 #endif
-template <int DIM>
+template <int DIM, bool GG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK_WAVES_PER_EU))) void wos_walk_kernel(
     const DevScene sc, const DevParams prm, const DevTasks tk, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int s_ctr[C_NUM];
   const int lane = threadIdx.x & (kWave - 1);
-  const LGeom G = stage_geometry<DIM>(sc, smem, true);
+  const LGeom G = stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
   // per-wave scratch shared by the star and ray queries (used one after the other)
   char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + (threadIdx.x / kWave) * walk_scratch_bytes<DIM>();
@@ -2718,16 +2718,26 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   if (steps_out) steps_out[i] = (int32_t)steps;
 }
 
-template __global__ void wos_first_ball_kernel<2>(const DevScene, const DevParams, const float*, int64_t, int64_t,
-                                                  int64_t, const DevTasks, unsigned long long*, unsigned int*, int,
-                                                  int);
-template __global__ void wos_first_ball_kernel<3>(const DevScene, const DevParams, const float*, int64_t, int64_t,
-                                                  int64_t, const DevTasks, unsigned long long*, unsigned int*, int,
-                                                  int);
-template __global__ void wos_walk_kernel<2>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                            unsigned long long*, unsigned int*, int);
-template __global__ void wos_walk_kernel<3>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                            unsigned long long*, unsigned int*, int);
+template __global__ void wos_first_ball_kernel<2, false>(const DevScene, const DevParams, const float*, int64_t,
+                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
+                                                           unsigned int*, int, int);
+template __global__ void wos_walk_kernel<2, false>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                                     unsigned long long*, unsigned int*, int);
+template __global__ void wos_first_ball_kernel<2, true>(const DevScene, const DevParams, const float*, int64_t,
+                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
+                                                           unsigned int*, int, int);
+template __global__ void wos_walk_kernel<2, true>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                                     unsigned long long*, unsigned int*, int);
+template __global__ void wos_first_ball_kernel<3, false>(const DevScene, const DevParams, const float*, int64_t,
+                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
+                                                           unsigned int*, int, int);
+template __global__ void wos_walk_kernel<3, false>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                                     unsigned long long*, unsigned int*, int);
+template __global__ void wos_first_ball_kernel<3, true>(const DevScene, const DevParams, const float*, int64_t,
+                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
+                                                           unsigned int*, int, int);
+template __global__ void wos_walk_kernel<3, true>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
+                                                     unsigned long long*, unsigned int*, int);
 template __global__ void wos_fold_kernel<2>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
                                             int32_t*);
 template __global__ void wos_fold_kernel<3>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
@@ -2777,12 +2787,15 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                               unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
                               hipStream_t s) {
-  if (dim == 2)
-    hipLaunchKernelGGL(wos_first_ball_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride,
-                       tk, counters, work, geom_floats, lhs_floats);
-  else
-    hipLaunchKernelGGL(wos_first_ball_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride,
-                       tk, counters, work, geom_floats, lhs_floats);
+#define WOS_LAUNCH_FB(D, G)                                                                                  \
+  hipLaunchKernelGGL((wos_first_ball_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, \
+                     tk, counters, work, geom_floats, lhs_floats)
+  if (dim == 2) {
+    if (sc.geom_global) WOS_LAUNCH_FB(2, true); else WOS_LAUNCH_FB(2, false);
+  } else {
+    if (sc.geom_global) WOS_LAUNCH_FB(3, true); else WOS_LAUNCH_FB(3, false);
+  }
+#undef WOS_LAUNCH_FB
   return hipGetLastError();
 }
 
@@ -2796,12 +2809,15 @@ hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s) {
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                         int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
                         int geom_floats, hipStream_t s) {
-  if (dim == 2)
-    hipLaunchKernelGGL(wos_walk_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters,
-                       tqueue, geom_floats);
-  else
-    hipLaunchKernelGGL(wos_walk_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters,
-                       tqueue, geom_floats);
+#define WOS_LAUNCH_WALK(D, G)                                                                                   \
+  hipLaunchKernelGGL((wos_walk_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters, \
+                     tqueue, geom_floats)
+  if (dim == 2) {
+    if (sc.geom_global) WOS_LAUNCH_WALK(2, true); else WOS_LAUNCH_WALK(2, false);
+  } else {
+    if (sc.geom_global) WOS_LAUNCH_WALK(3, true); else WOS_LAUNCH_WALK(3, false);
+  }
+#undef WOS_LAUNCH_WALK
   return hipGetLastError();
 }
 
@@ -2822,12 +2838,19 @@ size_t first_ball_wave_lds_bytes(int lhs_floats) {
 
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
-hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks) {
-  if (which == 0)
-    return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2>, kBlock, shmem)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3>, kBlock, shmem);
-  return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2>, kBlock, shmem)
-                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3>, kBlock, shmem);
+hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks) {
+  if (which == 0) {
+    if (dim == 2)
+      return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, true>, kBlock, shmem)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, false>, kBlock, shmem);
+    return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, true>, kBlock, shmem)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, false>, kBlock, shmem);
+  }
+  if (dim == 2)
+    return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, true>, kBlock, shmem)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, false>, kBlock, shmem);
+  return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3, true>, kBlock, shmem)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3, false>, kBlock, shmem);
 }
 
 void diag_dump(const char* tag) {

@@ -28,8 +28,8 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
 size_t first_ball_wave_lds_bytes(int lhs_floats);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
-// which: 0 first-ball kernel, 1 walk kernel
-hipError_t occupancy_blocks_per_cu(int which, int dim, size_t shmem, int* blocks);
+// which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry)
+hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
 }  // namespace wos

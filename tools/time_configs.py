@@ -30,9 +30,9 @@ def scene_for(name):
         cfg = workloads.dirichlet_obstacle_config(n_walks=256, res=512)
         return cfg, WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"],
                              dvertices=cfg["dvertices"], dprims=cfg["dprims"], dirichlet_value=1.0, watertight=True)
-    if name.startswith("D_cube"):
+    if name.startswith("D_cube") or name.startswith("E_cube"):
         res = int(name.split("_cube")[1])
-        cfg = workloads.cube_config(res=res, n_walks=64)
+        cfg = workloads.cube_config(res=res, n_walks=64 if name[0] == "D" else 128)
         v, ix = objparse.load(cfg["obj"], 3)
         return cfg, WosScene(v, ix, cfg["source"], 350.0, watertight=True)
     if name == "engine":

@@ -49,6 +49,9 @@ namespace wos {
 #ifndef WOS_ABL_CONST_SRC
 #define WOS_ABL_CONST_SRC 0
 #endif
+#ifndef WOS_ABL_FB
+#define WOS_ABL_FB 0
+#endif
 #ifndef WOS_ABL_NO_STATS
 #define WOS_ABL_NO_STATS 0
 #endif
@@ -2091,7 +2094,12 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   // Bessel constants are evaluated once (identical values either way)
   Gfn<DIM> g0;
   g0.init(yuk0, sc.absorption);
+#if WOS_ABL_FB == 1
+  { const bool y = g0.yukawa; g0.yukawa = false; g0.update_ball(x, firstR); g0.yukawa = y;
+    g0.muR = firstR * g0.sqrtLambda; g0.A0 = 0.5f; g0.A1 = 1.5f; g0.B0 = 0.3f; g0.B1 = 0.7f; }
+#else
   g0.update_ball(x, firstR);
+#endif
   for (int a = 0; a < prm.n_anti; a++) {
     const int64_t t = t0 + a;
     Gfn<DIM> g = g0;
@@ -2117,7 +2125,11 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       totalSource += throughput * contrib;
       firstSource = contrib;
       float gr[DIM];
+#if WOS_ABL_FB == 2
+      for (int k = 0; k < DIM; k++) gr[k] = (g.yVol[k] - g.c[k]) * 0.5f;
+#else
       g.gradient(gr);
+#endif
       float den = sourcePdf * gnorm;
       for (int k = 0; k < DIM; k++) sdir[k] = gr[k] / den;
     }

@@ -116,7 +116,14 @@ def cpu_baseline(cfg, n_threads, budget_s):
     t0 = time.perf_counter()
     _, _, _, _, st = oracle_lib.solve(osc, prm, sample, index_base=0, index_stride=stride)
     dt = time.perf_counter() - t0
+    # one core on a smaller strided subset (BASELINE.md asks for both)
+    prm1 = oracle_lib.make_params(cfg["solver"], cfg["output"], math_mode=0, n_threads=1)
+    s1 = max(1, pts.shape[0] // 1024)
+    t1 = time.perf_counter()
+    _, _, _, _, st1 = oracle_lib.solve(osc, prm1, pts[::s1], index_base=0, index_stride=s1)
+    dt1 = time.perf_counter() - t1
     return {
+        "value_1core": st1["walk_steps"] / dt1,
         "value": st["walk_steps"] / dt,
         "unit": "walk-steps/s",
         "cores": n_threads,

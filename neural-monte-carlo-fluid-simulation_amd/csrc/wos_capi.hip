@@ -77,6 +77,7 @@ struct DevCtx {
   bool inflight = false;       // a solve may still run on last_stream
   std::vector<hipEvent_t> bev; // per-chunk kernel boundary events (4 per chunk), grow-only
   hipStream_t aux[wos::kMaxPipes] = {};  // pipelines 1.. (pipeline 0 is the caller's stream)
+  float* d_rejtab = nullptr;   // rejection bound table, 2D then 3D (DevParams::rej_tab)
   hipEvent_t fork = nullptr, join[wos::kMaxPipes] = {};
 };
 
@@ -85,7 +86,8 @@ DevCtx g_ctx[kMaxDevices];  // never destroyed: the HIP runtime may be gone at p
 
 void ctx_free(DevCtx& c) {
   hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
-  hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters);
+  hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters); hipFree(c.d_rejtab);
+  c.d_rejtab = nullptr;
   if (c.ev0) hipEventDestroy(c.ev0);
   if (c.ev1) hipEventDestroy(c.ev1);
   if (c.done) hipEventDestroy(c.done);
@@ -112,9 +114,25 @@ void ctx_free(DevCtx& c) {
   c.ready = false;
 }
 
+// the rejection bound tables (host, computed once per process)
+const std::vector<float>& rejection_tables() {
+  static std::once_flag once;
+  static std::vector<float> t(2 * wos::kRejTabBins);
+  std::call_once(once, [] {
+    wos::rejection_bound_table(2, t.data());
+    wos::rejection_bound_table(3, t.data() + wos::kRejTabBins);
+  });
+  return t;
+}
+
 // caller holds c.mu and has selected the device
 int ctx_ready(DevCtx& c, int device) {
   if (c.ready) return WOS_OK;
+  {
+    const std::vector<float>& t = rejection_tables();
+    HIP_TRY(hipMalloc((void**)&c.d_rejtab, t.size() * sizeof(float)));
+    HIP_TRY(hipMemcpy(c.d_rejtab, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipMalloc((void**)&c.d_counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
   HIP_TRY(hipEventCreate(&c.ev0));
@@ -604,6 +622,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     if (rc != WOS_OK) return rc;
     dp.jump = c.d_jump;
     dp.n_jump = c.n_jump;
+    const char* rt = std::getenv("WOS_REJ_TABLE");  // "0": the scene-independent bound only (A/B)
+    dp.rej_tab = (rt && rt[0] == '0') ? nullptr : c.d_rejtab;
   }
 
   // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners

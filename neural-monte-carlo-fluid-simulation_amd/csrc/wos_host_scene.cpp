@@ -501,6 +501,57 @@ bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget
 }
 
 // ---------------------------------------------------------------------------
+// rejection bound table (wos_host_scene.h)
+// ---------------------------------------------------------------------------
+namespace {
+
+double yukawa_q(int dim, double s, double x) {
+  if (dim == 2) {
+    const double k0s = bessk0(s), i0s = bessi0(s);
+    return bessk0(s * x) - k0s / i0s * bessi0(s * x);
+  }
+  const double sx = s * x;
+  const double sh = 0.5 * (std::exp(sx) - std::exp(-sx));
+  const double shs = 0.5 * (std::exp(s) - std::exp(-s));
+  return std::exp(-sx) - std::exp(-s) * sh / shs;
+}
+
+double yukawa_f(int dim, double s) {
+  // max over x in (0, 1] of x * Q_s(x): coarse grid, then golden-section on the
+  // bracket of the best sample (x Q_s(x) is unimodal)
+  const int n = 256;
+  double best = 0.0;
+  int bi = 1;
+  for (int i = 1; i <= n; i++) {
+    const double x = (double)i / n;
+    const double v = x * yukawa_q(dim, s, x);
+    if (v > best) { best = v; bi = i; }
+  }
+  double a = (double)(bi - 1) / n, b = (double)std::min(bi + 1, n) / n;
+  if (a <= 0.0) a = 1e-9;
+  const double g = 0.5 * (std::sqrt(5.0) - 1.0);
+  double c = b - g * (b - a), d = a + g * (b - a);
+  double fc = c * yukawa_q(dim, s, c), fd = d * yukawa_q(dim, s, d);
+  for (int it = 0; it < 60; it++) {
+    if (fc > fd) { b = d; d = c; fd = fc; c = b - g * (b - a); fc = c * yukawa_q(dim, s, c); }
+    else { a = c; c = d; fc = fd; d = a + g * (b - a); fd = d * yukawa_q(dim, s, d); }
+  }
+  return std::max(best, std::max(fc, fd));
+}
+
+}  // namespace
+
+void rejection_bound_table(int dim, float* tab) {
+  for (int k = 0; k < kRejTabBins; k++) {
+    const double lo = std::max(1e-6, ((double)k / kRejTabScale) * ((double)k / kRejTabScale));
+    const double hi = ((double)(k + 1) / kRejTabScale) * ((double)(k + 1) / kRejTabScale);
+    double m = 0.0;
+    for (int j = 0; j <= 15; j++) m = std::max(m, yukawa_f(dim, lo + (hi - lo) * j / 15.0));
+    tab[k] = (float)(1.02 * m);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // OBJ parsing
 // ---------------------------------------------------------------------------
 static int parse_face_index(const std::string& token) {  // scene_loader.inl:29-44

@@ -52,6 +52,18 @@ struct StarGrid {
 // does not fit budget_bytes at a useful resolution (the kernel then scans groups)
 bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget_bytes, StarGrid& out);
 
+// Upper bounds for the Yukawa rejection test (wos_kernel.hip rej_quick_bound): the
+// accept threshold of rejectionSampleGreensFn at radius r = x R is
+// T = R * x * Q_s(x) / (norm * bound) with s = mu R and
+//   Q_s(x) = K0(s x) - K0(s) / I0(s) * I0(s x)                 (2D)
+//   Q_s(x) = e^{-s x} - e^{-s} sinh(s x) / sinh(s)             (3D),
+// so T <= R * F(s) / (norm * bound) with F(s) = max_x x Q_s(x).  tab[k] >= F(s) for
+// every s of bin k (k = floor(kRejTabScale * sqrt(s))): the maximum over 16 values
+// of s across the bin, each maximised over x on a grid refined around its peak,
+// times 1.02 (the bins are narrow and F is smooth: the margin dwarfs both
+// discretisations and the float rounding of the kernel's exact test).
+void rejection_bound_table(int dim, float* tab);
+
 bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err);
 bool load_obj(const std::string& path, int dim, bool flip, bool normalize_domain, std::vector<float>& verts,
               std::vector<int32_t>& prims, std::string& err);

@@ -1007,14 +1007,25 @@ __device__ __forceinline__ float k1_fast(float x) {
 // a 1e-3 margin (far above the A&S polynomial error and the float rounding of the
 // exact path), so u above the bound is the exact test's reject without evaluating
 // r at all.  A non-positive or non-finite bound disables the shortcut.
+// Tighter, per ball: T(r) <= R F(mu R) / (norm bound) with F(s) = max_x x Q_s(x)
+// tabulated by bins of s with a 2 % margin (DevParams::rej_tab, wos_host_scene.h
+// rejection_bound_table) -- the subtracted term is kept, so the bound follows the
+// real peak of the threshold (tests/test_rejection_bounds.py checks both bounds).
 #ifndef WOS_QUICK_REJ
 #define WOS_QUICK_REJ 1
 #endif
 template <int DIM>
-__device__ __forceinline__ float rej_quick_bound(float sqrtL, float invNB) {
+__device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, float muR, float sqrtL, float invNB) {
   if (!WOS_QUICK_REJ) return 3.0e38f;
   const float C = DIM == 2 ? 0.4670f : 0.3683f;
-  const float q = C * invNB / sqrtL;
+  float q = C * invNB / sqrtL;
+  if (prm.rej_tab != nullptr && muR >= 0.0f) {
+    const int k = (int)(kRejTabScale * __builtin_sqrtf(muR));
+    if (k < kRejTabBins) {
+      const float qt = R * prm.rej_tab[(DIM == 3 ? kRejTabBins : 0) + k] * invNB;
+      q = qt < q ? qt : q;
+    }
+  }
   return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
 }
 
@@ -1050,7 +1061,7 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
   const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
   const float rho = g.A0 / g.A1;
   const float invNB = 1.0f / (nrm * bound);
-  const float quick = g.yukawa ? rej_quick_bound<DIM>(g.sqrtLambda, invNB) : 3.0e38f;
+  const float quick = g.yukawa ? rej_quick_bound<DIM>(DevParams{}, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
   int iter = 0;
   do {
     float u = s.nextf();
@@ -1107,6 +1118,13 @@ constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
 #endif
 template <int DIM>
 constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3;
+static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16, "RejLDS::surv holds 64 * 16 items");
+// 1: screen a generation's items with the certain-reject bound, then evaluate the
+// survivors compacted over the wave; 0 (default): every lane evaluates its own
+// items (the screen + compaction measured 15-20 % slower on karman / cube / C)
+#ifndef WOS_REJ_COMPACT
+#define WOS_REJ_COMPACT 0
+#endif
 
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
@@ -1139,6 +1157,9 @@ struct RejLDS {
   float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
   float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
   float qb[kWave];                 // certain-reject bound (rej_quick_bound)
+#if WOS_REJ_COMPACT
+  uint16_t surv[kWave * 16];       // items that passed the certain-reject screen (one generation)
+#endif
   float nrm[kWave], bound[kWave];
   uint32_t base[kWave], acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
@@ -1225,7 +1246,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
-      L->qb[lane] = rej_quick_bound<DIM>(g.sqrtLambda, 1.0f / (nrm * bound));
+      L->qb[lane] = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, 1.0f / (nrm * bound));
       if constexpr (DIM == 2) {
         L->c0[lane] = g.A0 / g.A1;
         L->c1[lane] = 1.0f / (nrm * bound);
@@ -1262,6 +1283,57 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         L->und[lane] = 0u;
       }
       wave_sync();
+#if WOS_REJ_COMPACT
+      // phase A: the certain-reject screen of every item (its first draw only);
+      // phase B: the survivors, compacted, evaluated densely by the whole wave
+      uint32_t keep = 0;
+      for (int q = 0; q < per; q++) {
+        const int item = lane * per + q;
+        const int orank = item / B, b = item - orank * B;
+        if (orank < nact) {
+          const int owner = (int)L->owner_of[orank];
+          const int j = (int)L->base[owner] + b;
+          DIAG_LANE(D_RITEMS);
+          if (j < kRejMax) {
+            if (!(draw_float(rej_state(prm, L->s0[owner], j)) > L->qb[owner])) keep |= 1u << q;
+            else DIAG_LANE(D_RQUICK);
+          }
+        }
+      }
+      {
+        const uint32_t kc = (uint32_t)__popc(keep);
+        uint32_t incl = kc;
+        for (int dlt = 1; dlt < kWave; dlt <<= 1) {
+          const uint32_t v = __shfl_up(incl, dlt);
+          if (lane >= dlt) incl += v;
+        }
+        const uint32_t total = __shfl(incl, kWave - 1);
+        uint32_t pos = incl - kc;
+        for (uint32_t m = keep; m; m &= m - 1) L->surv[pos++] = (uint16_t)(lane * per + __builtin_ctz(m));
+        wave_sync();
+        for (uint32_t k = lane; k < total; k += kWave) {
+          const int item = (int)L->surv[k];
+          const int orank = item / B, b = item - orank * B;
+          const int owner = (int)L->owner_of[orank];
+          const int j = (int)L->base[owner] + b;
+          const uint64_t st = rej_state(prm, L->s0[owner], j);
+          const float u = draw_float(st);
+          const float x = draw_float(st * kPcgMult + kPcgInc);
+          int dcs;
+          if constexpr (DIM == 2) {
+            dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
+          } else {
+            const float rr = x * L->R[owner];
+            dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
+            if (dcs < 0)
+              dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
+                                      L->bound[owner]);
+          }
+          if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
+          else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
+        }
+      }
+#else
       for (int q = 0; q < per; q++) {
         const int item = lane * per + q;
         const int orank = item / B, b = item - orank * B;
@@ -1292,6 +1364,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           }
         }
       }
+#endif
       wave_sync();
       if (!done) {
         const uint32_t acc = L->acc[lane], und = L->und[lane];

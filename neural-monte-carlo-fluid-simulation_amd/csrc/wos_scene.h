@@ -92,7 +92,14 @@ struct DevParams {
   // per-point stratified samples in parallel.  n_jump entries.
   const uint64_t* jump;
   int32_t n_jump;
+  // certain-reject bounds of the Yukawa rejection threshold by bin of s = mu R
+  // (wos_host_scene.h rejection_bound_table), kRejTabBins floats; nullptr: none
+  const float* rej_tab;
 };
+
+// bins of the rejection bound table: bin = floor(kRejTabScale * sqrt(mu R))
+constexpr int kRejTabBins = 96;
+constexpr float kRejTabScale = 8.0f;
 
 // Walk-task workspace of one batch of points, SoA over T = n_points * wpp tasks
 // (task t = point * wpp + pair * n_anti + member).  Written by the first-ball

@@ -2264,6 +2264,10 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
     }
     if (!active) continue;
+#if WOS_ABL_FB == 5
+    if (firstSource == 12345.0f) tk.first[t] = throughput + totalSource + bdir[0] + sdir[0];
+    continue;
+#endif
     tk.first[t] = firstSource;
     for (int k = 0; k < DIM; k++) {
       tk.bdir[k * T + t] = bdir[k];
@@ -2330,6 +2334,10 @@ __device__ __forceinline__ void flush_counter(unsigned long long* counters, int 
 enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
 
 // ---- kernel 1: point setup + first balls ----------------------------------
+#ifndef WOS_PT_GRAB
+#define WOS_PT_GRAB 2
+#endif
+constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the first-ball kernel
 #ifndef WOS_FB_WAVES_PER_EU
 #define WOS_FB_WAVES_PER_EU 1
 #endif
@@ -2361,9 +2369,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
   // point queue, one point ahead: the next index is taken (and its coordinates
   // loaded) while the current point is processed, so neither the queue atomic nor
   // the point load sits on a point's critical path
-  unsigned int idx = 0;
-  if (lane == 0) idx = atomicAdd(work, 1u);
-  idx = __shfl(idx, 0);
+  // Points are taken kPtGrab at a time (one queue atomic per chunk: a single-address
+  // atomic per point serialises at ~13 ns, which had bounded the whole kernel);
+  // kPtGrab = 0: static round-robin over the waves of the grid.
+  const unsigned int nwaves = gridDim.x * (kBlock / kWave);
+  const unsigned int wave_id = blockIdx.x * (kBlock / kWave) + wave;
+  unsigned int idx = 0, cend = 0;
+  if (kPtGrab == 0) {
+    idx = wave_id;
+  } else {
+    if (lane == 0) idx = atomicAdd(work, kPtGrab);
+    idx = __shfl(idx, 0);
+    cend = idx + kPtGrab;
+  }
   float xn[DIM];
   for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
   for (;;) {
@@ -2371,8 +2389,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
     const int64_t gidx = base + (int64_t)idx * stride;
     float x[DIM];
     for (int k = 0; k < DIM; k++) x[k] = xn[k];
+    const bool grab = kPtGrab != 0 && idx + 1 >= cend;  // wave-uniform
     unsigned int nidx_l0 = 0;
-    if (lane == 0) nidx_l0 = atomicAdd(work, 1u);
+    if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
 
     // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
     DIAG_T0(t_fb0);
@@ -2411,14 +2430,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
       atomicAdd(&s_hist[bucket], 1u);
     }
     // the next point: its index (the atomic has returned by now) and coordinates
-    const unsigned int nidx = (unsigned int)__shfl((int)nidx_l0, 0);
+    unsigned int nidx, ncend = cend;
+    if (kPtGrab == 0) {
+      nidx = idx + nwaves;
+    } else if (grab) {
+      nidx = (unsigned int)__shfl((int)nidx_l0, 0);
+      ncend = nidx + kPtGrab;
+    } else {
+      nidx = idx + 1;
+    }
     for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
-    if (!estimate) { idx = nidx; continue; }
+    if (!estimate) { idx = nidx; cend = ncend; continue; }
     c_pts += lane == 0;
     DIAG_ADD(D_FB_SETUP, t_fb0);
     DIAG_COUNT(D_FB_PTS, 1);
     DIAG_T0(t_fb1);
+#if WOS_ABL_FB == 3
+    for (int i = lane; i < 2 * npairs * (DIM - 1); i += kWave) strat[i] = (i + 0.5f) / (2 * npairs * (DIM - 1));
+    wave_sync();
+#else
     build_lhs<DIM>(prm, gidx, strat, partner, reinterpret_cast<char*>(rejL), lane);
+#endif
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
     const float firstR = 0.99f * smin(dDist, nDist);
@@ -2432,6 +2464,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
     DIAG_MAX(D_FB_MAX, __builtin_amdgcn_s_memtime() - t_fb0);
     wave_sync();
     idx = nidx;
+    cend = ncend;
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
@@ -2475,7 +2508,10 @@ __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk,
 }
 
 // ---- kernel 2: walks ---------------------------------------------------------
-constexpr unsigned int kTaskGrab = 256;  // tasks a wave takes from the global queue at once
+#ifndef WOS_TASK_GRAB
+#define WOS_TASK_GRAB 128
+#endif
+constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
 
 // experiments (0 = off): WOS_PRIO=n raises the wave priority with the age of its
 // oldest walk (steps / n); WOS_DRAIN=n stops handing tasks to a wave whose oldest

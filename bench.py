@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-projection-wall", action="store_true")
+    ap.add_argument("--blocking", action="store_true",
+                    help="wait for every solve before enqueueing the next (default: the next projection is "
+                         "enqueued while the previous one runs; its stats are read after)")
     return ap.parse_args()
 
 
@@ -165,15 +168,16 @@ def main():
     send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=dev)
 
     def step():
-        p, g, st = scene.solve(x, params, index_base=rank, index_stride=world)
+        """Enqueue one projection (+ the all-gather); returns its stats ticket."""
+        p, g, st = scene.solve(x, params, index_base=rank, index_stride=world, sync=a.blocking)
         if world > 1:
             send[:n_local, 0] = p
             send[:n_local, 1:] = g
             dist.all_gather_into_tensor(gather_buf, send)
-        return st
+        return st["ticket"]
 
     for _ in range(a.warmup):
-        step()
+        scene.solve_stats(step())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -181,8 +185,13 @@ def main():
     t0 = time.perf_counter()
     steps_rec = steps_all = 0
     kernel_ms, walk_ms, fb_ms, fold_ms, walk_kernel_steps, launches = [], [], [], [], 0, 0
-    for _ in range(a.steps):
-        st = step()
+    # one projection in flight behind the one whose counters are read (device counters,
+    # copied per solve; wos_solve_stats waits only for that solve)
+    tickets = [step()]
+    for k in range(a.steps):
+        if k + 1 < a.steps:
+            tickets.append(step())
+        st = scene.solve_stats(tickets[k])
         steps_rec += st["walk_steps"]
         steps_all += st["walk_steps"] + st["wasted_steps"]
         kernel_ms.append(st["kernel_ms"])
@@ -235,6 +244,7 @@ def main():
                        "points": n_all, "walks_per_point": a.walks, "source_grid": list(cfg["source"].shape),
                        "parallelism": f"points sharded by stride over {world} GPU(s) + 1 RCCL all-gather"},
             "projection_ms": elapsed / a.steps * 1e3,
+            "enqueue": "blocking" if a.blocking else "pipelined (next projection enqueued before the previous one's stats are read)",
             "kernel_ms": kms,
             "walk_steps_per_projection": steps_rec / a.steps,
             "wasted_steps_per_projection": (steps_all - steps_rec) / a.steps,

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 3
+#define WOS_ABI_VERSION 4
 
 enum {
     WOS_OK = 0,
@@ -33,7 +33,8 @@ enum {
 
 /* flags for wos_solve */
 #define WOS_PTRS_DEVICE 0x1u   /* pts/p/grad/n_est/steps are device pointers on the scene's device */
-#define WOS_ASYNC       0x2u   /* enqueue on `stream` and return; stats are not filled */
+#define WOS_ASYNC       0x2u   /* with WOS_PTRS_DEVICE: enqueue on `stream` and return; only
+                                  stats->ticket is filled (read the rest with wos_solve_stats) */
 
 /* A boundary mesh: 2D line segments (dim=2) or 3D triangles (dim=3). */
 typedef struct wos_mesh {
@@ -144,6 +145,7 @@ typedef struct wos_stats {
     int32_t star_grid;          /* 1: the star-radius cell grid was used */
     int32_t geom_global;        /* 1: geometry read from global memory (too large for LDS) */
     int32_t reserved;
+    uint64_t ticket;            /* id of this solve on its device (for wos_solve_stats) */
 } wos_stats;
 
 /* Replaces runWalkOnStars_sampled (demo.cpp:119-205) / runWalkOnStars_3d
@@ -159,6 +161,13 @@ int wos_solve(wos_scene *scene, const wos_solver_params *params,
               const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
               float *p, float *grad, int32_t *n_est, int32_t *steps,
               wos_stats *stats, void *stream, uint32_t flags);
+
+/* Statistics of an earlier solve on the scene's device, by stats->ticket: waits for
+ * that solve to finish, then fills *stats.  A time-stepper can enqueue the projection
+ * (WOS_ASYNC) and keep queueing device work behind it, as the reference's caller does
+ * with its training loop after wost() (model_split.py:272-283).  The last 16 solves
+ * per device are held; older tickets return WOS_E_INVALID.  No reference analogue. */
+int wos_solve_stats(wos_scene *scene, uint64_t ticket, wos_stats *stats);
 
 /* Device self-test of the deterministic math used by the kernel (for the
  * GPU-vs-oracle parity tests): which = 0 exp, 1 log, 2 sin, 3 cos, 4 atan,

@@ -54,6 +54,19 @@ hipError_t upload(T** dst, const std::vector<T>& src) {
 }
 
 // ---- per-device solve workspace ---------------------------------------------
+// Timing events + a pinned copy of the counters of one enqueued solve, so a solve
+// enqueued with WOS_ASYNC can report its statistics later (wos_solve_stats) while
+// the next solves are already queued behind it.
+struct StatSlot {
+  uint64_t ticket = 0;                  // 0: empty
+  unsigned long long* h_cnt = nullptr;  // pinned host copy of the kNumCounters counters
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  std::vector<hipEvent_t> bev;          // per-chunk kernel boundary events (4 per chunk), grow-only
+  int64_t n_batches = 0;
+  int32_t bpc_fb = 0, bpc_walk = 0, walk_lds = 0, star_grid = 0, geom_global = 0;
+};
+constexpr int kStatSlots = 16;
+
 struct DevCtx {
   std::mutex mu;  // one solve at a time per device (the workspace is shared)
   bool ready = false;
@@ -71,11 +84,11 @@ struct DevCtx {
   int32_t* d_pstate = nullptr; // per-point state + queue permutation of one batch, then bucket counters
   int64_t pstate_cap = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counters
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  StatSlot slot[kStatSlots];   // ring indexed by ticket % kStatSlots
+  uint64_t next_ticket = 1;
   hipEvent_t done = nullptr;   // end of the last enqueued solve
   hipStream_t last_stream = nullptr;
   bool inflight = false;       // a solve may still run on last_stream
-  std::vector<hipEvent_t> bev; // per-chunk kernel boundary events (4 per chunk), grow-only
   hipStream_t aux[wos::kMaxPipes] = {};  // pipelines 1.. (pipeline 0 is the caller's stream)
   float* d_rejtab = nullptr;   // rejection bound table, 2D then 3D (DevParams::rej_tab)
   hipEvent_t fork = nullptr, join[wos::kMaxPipes] = {};
@@ -88,10 +101,15 @@ void ctx_free(DevCtx& c) {
   hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
   hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters); hipFree(c.d_rejtab);
   c.d_rejtab = nullptr;
-  if (c.ev0) hipEventDestroy(c.ev0);
-  if (c.ev1) hipEventDestroy(c.ev1);
+  for (StatSlot& q : c.slot) {
+    if (q.ev0) hipEventDestroy(q.ev0);
+    if (q.ev1) hipEventDestroy(q.ev1);
+    if (q.done) hipEventDestroy(q.done);
+    for (hipEvent_t e : q.bev) hipEventDestroy(e);
+    if (q.h_cnt) hipHostFree(q.h_cnt);
+    q = StatSlot{};
+  }
   if (c.done) hipEventDestroy(c.done);
-  for (hipEvent_t e : c.bev) hipEventDestroy(e);
   for (int i = 0; i < wos::kMaxPipes; i++) {
     if (c.aux[i]) hipStreamDestroy(c.aux[i]);
     if (c.join[i]) hipEventDestroy(c.join[i]);
@@ -107,8 +125,7 @@ void ctx_free(DevCtx& c) {
   c.d_tasks = nullptr; c.task_cap = 0;
   c.d_pstate = nullptr; c.pstate_cap = 0;
   c.d_counters = nullptr;
-  c.ev0 = c.ev1 = c.done = nullptr;
-  c.bev.clear();
+  c.done = nullptr;
   c.last_stream = nullptr;
   c.inflight = false;
   c.ready = false;
@@ -135,8 +152,12 @@ int ctx_ready(DevCtx& c, int device) {
   }
   HIP_TRY(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, device));
   HIP_TRY(hipMalloc((void**)&c.d_counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
-  HIP_TRY(hipEventCreate(&c.ev0));
-  HIP_TRY(hipEventCreate(&c.ev1));
+  for (StatSlot& q : c.slot) {
+    HIP_TRY(hipHostMalloc((void**)&q.h_cnt, wos::kNumCounters * sizeof(unsigned long long)));
+    HIP_TRY(hipEventCreate(&q.ev0));
+    HIP_TRY(hipEventCreate(&q.ev1));
+    HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+  }
   HIP_TRY(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
   for (int i = 1; i < wos::kMaxPipes; i++) {
@@ -568,6 +589,40 @@ int ensure_jump(DevCtx& c, int k_needed) {
   return WOS_OK;
 }
 
+// statistics of the solve held by slot q (its done event has completed)
+int fill_stats(const StatSlot& q, wos_stats* stats) {
+  *stats = wos_stats{};
+  const unsigned long long* cnt = q.h_cnt;
+  stats->walk_steps = cnt[0];
+  stats->wasted_steps = cnt[1];
+  stats->walks_recorded = cnt[2];
+  stats->walks_escaped = cnt[3];
+  stats->walks_max_length = cnt[4];
+  stats->walks_rr = cnt[5];
+  stats->walks_dirichlet = cnt[6];
+  stats->points_estimated = cnt[7];
+  stats->rejection_iters = cnt[8];
+  float ms = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&ms, q.ev0, q.ev1));
+  stats->kernel_ms = ms;
+  stats->walk_launches = (uint64_t)q.n_batches;
+  for (int64_t b = 0; b < q.n_batches; b++) {
+    const hipEvent_t* ev = &q.bev[4 * b];
+    float a = 0.0f, w = 0.0f, f = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&w, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&f, ev[2], ev[3]));
+    stats->first_ball_ms += a; stats->walk_ms += w; stats->fold_ms += f;
+  }
+  stats->first_ball_blocks_per_cu = q.bpc_fb;
+  stats->walk_blocks_per_cu = q.bpc_walk;
+  stats->walk_lds_bytes = q.walk_lds;
+  stats->star_grid = q.star_grid;
+  stats->geom_global = q.geom_global;
+  stats->ticket = q.ticket;
+  return WOS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -726,12 +781,21 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
-  while ((int64_t)c.bev.size() < 4 * n_chunks) {
+  const uint64_t ticket = c.next_ticket++;
+  StatSlot& q = c.slot[ticket % kStatSlots];
+  while ((int64_t)q.bev.size() < 4 * n_chunks) {
     hipEvent_t e = nullptr;
     HIP_TRY(hipEventCreate(&e));
-    c.bev.push_back(e);
+    q.bev.push_back(e);
   }
-  HIP_TRY(hipEventRecord(c.ev0, st));
+  q.ticket = ticket;
+  q.n_batches = n_chunks;
+  q.bpc_fb = bpc_fb;
+  q.bpc_walk = bpc_walk;
+  q.walk_lds = (int32_t)shmem_walk;
+  q.star_grid = dsc.sgrid != nullptr;
+  q.geom_global = dsc.geom_global;
+  HIP_TRY(hipEventRecord(q.ev0, st));
   if (pipes > 1) {
     HIP_TRY(hipEventRecord(c.fork, st));
     for (int i = 1; i < pipes; i++) HIP_TRY(hipStreamWaitEvent(c.aux[i], c.fork, 0));
@@ -740,7 +804,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     const int pipe = (int)(k % pipes);
     hipStream_t ps = pipe == 0 ? st : c.aux[pipe];
     const int64_t b0 = k * chunk;
-    hipEvent_t* ev = &c.bev[4 * k];
+    hipEvent_t* ev = &q.bev[4 * k];
     const int64_t nb = std::min(chunk, n - b0);
     wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp, pipe, chunk * wpp, chunk);
     const int64_t bbase = index_base + b0 * index_stride;
@@ -766,53 +830,48 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     HIP_TRY(hipEventRecord(c.join[i], c.aux[i]));
     HIP_TRY(hipStreamWaitEvent(st, c.join[i], 0));
   }
-  const int64_t n_batches = n_chunks;
-  HIP_TRY(hipEventRecord(c.ev1, st));
+  HIP_TRY(hipEventRecord(q.ev1, st));
+  HIP_TRY(hipMemcpyAsync(q.h_cnt, c.d_counters, wos::kNumCounters * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
   if (!dev_ptrs && n > 0) {
     HIP_TRY(hipMemcpyAsync(p, d_p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(grad, d_g, (size_t)n * dim * sizeof(float), hipMemcpyDeviceToHost, st));
     if (n_est) HIP_TRY(hipMemcpyAsync(n_est, d_nest, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (steps) HIP_TRY(hipMemcpyAsync(steps, d_steps, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   }
+  HIP_TRY(hipEventRecord(q.done, st));
   HIP_TRY(hipEventRecord(c.done, st));
   c.last_stream = st;
   c.inflight = true;
-  if ((flags & WOS_ASYNC) && dev_ptrs) return WOS_OK;
+  if ((flags & WOS_ASYNC) && dev_ptrs) {
+    if (stats) {
+      *stats = wos_stats{};
+      stats->ticket = ticket;
+    }
+    return WOS_OK;
+  }
   HIP_TRY(hipStreamSynchronize(st));
   c.inflight = false;
   wos::diag_dump(dim == 2 ? "2d" : "3d");
   if (stats) {
-    unsigned long long cnt[wos::kNumCounters];
-    HIP_TRY(hipMemcpy(cnt, c.d_counters, sizeof(cnt), hipMemcpyDeviceToHost));
-    stats->walk_steps = cnt[0];
-    stats->wasted_steps = cnt[1];
-    stats->walks_recorded = cnt[2];
-    stats->walks_escaped = cnt[3];
-    stats->walks_max_length = cnt[4];
-    stats->walks_rr = cnt[5];
-    stats->walks_dirichlet = cnt[6];
-    stats->points_estimated = cnt[7];
-    stats->rejection_iters = cnt[8];
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, c.ev0, c.ev1));
-    stats->kernel_ms = ms;
-    stats->first_ball_ms = stats->walk_ms = stats->fold_ms = 0.0;
-    stats->walk_launches = (uint64_t)n_batches;
-    for (int64_t b = 0; b < n_batches; b++) {
-      hipEvent_t* ev = &c.bev[4 * b];
-      float a = 0.0f, w = 0.0f, f = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-      HIP_TRY(hipEventElapsedTime(&w, ev[1], ev[2]));
-      HIP_TRY(hipEventElapsedTime(&f, ev[2], ev[3]));
-      stats->first_ball_ms += a; stats->walk_ms += w; stats->fold_ms += f;
-    }
-    stats->first_ball_blocks_per_cu = bpc_fb;
-    stats->walk_blocks_per_cu = bpc_walk;
-    stats->walk_lds_bytes = (int32_t)shmem_walk;
-    stats->star_grid = dsc.sgrid != nullptr;
-    stats->geom_global = dsc.geom_global;
+    int rc = fill_stats(q, stats);
+    if (rc != WOS_OK) return rc;
   }
   return WOS_OK;
+}
+
+int wos_solve_stats(wos_scene* s, uint64_t ticket, wos_stats* stats) {
+  if (!s || !stats) return fail(WOS_E_INVALID, "wos_solve_stats: null scene/stats");
+  std::lock_guard<std::mutex> lock(s->mu);
+  HIP_TRY(hipSetDevice(s->device));
+  DevCtx& c = g_ctx[s->device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  StatSlot& q = c.slot[ticket % kStatSlots];
+  if (ticket == 0 || q.ticket != ticket)
+    return fail(WOS_E_INVALID, "wos_solve_stats: unknown ticket (more than " + std::to_string(kStatSlots) +
+                                   " solves were enqueued on this device after it)");
+  HIP_TRY(hipEventSynchronize(q.done));
+  return fill_stats(q, stats);
 }
 
 int wos_selftest_math(int32_t which, const double* x, double* out, int64_t n, int32_t device) {

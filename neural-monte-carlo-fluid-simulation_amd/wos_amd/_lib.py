@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 3  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 4  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
@@ -64,7 +64,7 @@ class Stats(C.Structure):
         "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [
         (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)] + [
         (n, C.c_int32) for n in ("first_ball_blocks_per_cu", "walk_blocks_per_cu", "walk_lds_bytes", "star_grid",
-                                 "geom_global", "reserved")]
+                                 "geom_global", "reserved")] + [("ticket", C.c_uint64)]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n))) for n, t in self._fields_}
@@ -74,6 +74,7 @@ class Stats(C.Structure):
 EXPORTS = (
     "wos_load_obj", "wos_mesh_free", "wos_scene_create", "wos_scene_destroy",
     "wos_scene_get_info", "wos_scene_set_source", "wos_release_caches", "wos_default_params", "wos_solve",
+    "wos_solve_stats",
     "wos_selftest_math", "wos_last_error", "wos_abi_version", "wos_device_count",
 )
 
@@ -108,6 +109,8 @@ def load():
     L.wos_solve.argtypes = [C.c_void_p, C.POINTER(SolverParams), C.c_void_p, C.c_int64, C.c_int64,
                             C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                             C.POINTER(Stats), C.c_void_p, C.c_uint32]
+    L.wos_solve_stats.restype = C.c_int
+    L.wos_solve_stats.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(Stats)]
     L.wos_selftest_math.restype = C.c_int
     L.wos_selftest_math.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
     L.wos_last_error.restype = C.c_char_p

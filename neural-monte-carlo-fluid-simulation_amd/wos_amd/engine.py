@@ -167,7 +167,9 @@ class WosScene:
     def solve(self, pts, params=None, *, index_base=0, index_stride=1, counts=False, stream=None,
               sync=True):
         """Solve at query points.  Returns (p [N], grad [N,dim], stats dict[, n_est, steps])
-        as numpy arrays for host input, torch tensors for GPU tensor input."""
+        as numpy arrays for host input, torch tensors for GPU tensor input.  With GPU tensors
+        and sync=False the solve is only enqueued on the stream: the stats dict then holds
+        just "ticket"; solve_stats(ticket) waits for that solve and returns the full dict."""
         L = _lib.load()
         params = params if params is not None else solver_params()
         st = Stats()
@@ -204,6 +206,12 @@ class WosScene:
         if counts:
             out = out + (ne, sp)
         return out
+
+    def solve_stats(self, ticket):
+        """Statistics of an enqueued solve (wos_solve_stats); blocks until it has finished."""
+        st = Stats()
+        check(_lib.load().wos_solve_stats(self._h, int(ticket), C.byref(st)), "wos_solve_stats")
+        return st.as_dict()
 
     def close(self):
         if getattr(self, "_h", None):

@@ -128,3 +128,32 @@ def test_streams_are_ordered(gpu):
     assert np.array_equal(pb.cpu().numpy().view(np.uint32), pb_ref.view(np.uint32))
     a.close()
     b.close()
+
+
+def test_async_solves_report_their_own_stats(gpu):
+    """WOS_ASYNC + wos_solve_stats: several solves enqueued back to back (different
+    point sets) each report the statistics of a blocking solve of the same points,
+    and give the same bit-exact outputs."""
+    cfg, v, ix, pts = _cfg()
+    dev = torch.device("cuda", 0)
+    prm = solver_params(cfg["solver"], cfg["output"])
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    sets = [torch.from_numpy(np.ascontiguousarray(pts[k * 256:(k + 1) * 256 + 64 * k])).to(dev) for k in range(3)]
+    want = []
+    for x in sets:
+        p, g, st = sc.solve(x, prm)
+        want.append((p.cpu().numpy().view(np.uint32), g.cpu().numpy().view(np.uint32), st))
+    enq = [sc.solve(x, prm, sync=False) for x in sets]
+    for (p, g, st0), (pw, gw, stw) in zip(enq, want):
+        assert set(k for k, v in st0.items() if v) <= {"ticket"} and st0["ticket"] > 0
+        st = sc.solve_stats(st0["ticket"])
+        assert np.array_equal(p.cpu().numpy().view(np.uint32), pw)
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), gw)
+        for k in ("walk_steps", "wasted_steps", "walks_recorded", "points_estimated", "rejection_iters"):
+            assert st[k] == stw[k], k
+        assert st["kernel_ms"] > 0 and st["walk_ms"] > 0
+    with pytest.raises(Exception):
+        sc.solve_stats(0)
+    with pytest.raises(Exception):
+        sc.solve_stats(enq[-1][2]["ticket"] + 1000)
+    sc.close()

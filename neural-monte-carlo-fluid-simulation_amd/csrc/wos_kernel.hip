@@ -1151,6 +1151,17 @@ __device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0,
   return jump_state(prm, s0, 2 * j);
 }
 
+// floor(item / B) for item < 2048, 1 <= B <= 32, with m = ceil(2^16 / B): writing
+// item = qB + r, item*m/2^16 = q + (r + item*e/2^16)/B with e = mB - 2^16 < B, and
+// item*e < 2^16, so the floor is q.  (A runtime u32 division is ~20 VALU ops per item.)
+#ifndef WOS_FASTDIV
+#define WOS_FASTDIV 1
+#endif
+__device__ __forceinline__ int rej_div(int item, int B, uint32_t mB) {
+  if (!WOS_FASTDIV) return item / B;
+  return (int)(((uint32_t)item * mB) >> 16);
+}
+
 struct RejLDS {
   unsigned long long s0[kWave];
   float R[kWave], sqrtL[kWave];
@@ -1274,6 +1285,8 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       int B = kWave / nact;
       B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > 32 ? 32 : B);
       const int items = nact * B, per = (items + kWave - 1) / kWave;
+      // item / B as a multiply-shift (exact: item < 2048, B <= 32, see rej_div)
+      const uint32_t mB = (65536u + (uint32_t)B - 1u) / (uint32_t)B;
       if (!done) {
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
@@ -1289,7 +1302,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       uint32_t keep = 0;
       for (int q = 0; q < per; q++) {
         const int item = lane * per + q;
-        const int orank = item / B, b = item - orank * B;
+        const int orank = rej_div(item, B, mB), b = item - orank * B;
         if (orank < nact) {
           const int owner = (int)L->owner_of[orank];
           const int j = (int)L->base[owner] + b;
@@ -1313,7 +1326,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         wave_sync();
         for (uint32_t k = lane; k < total; k += kWave) {
           const int item = (int)L->surv[k];
-          const int orank = item / B, b = item - orank * B;
+          const int orank = rej_div(item, B, mB), b = item - orank * B;
           const int owner = (int)L->owner_of[orank];
           const int j = (int)L->base[owner] + b;
           const uint64_t st = rej_state(prm, L->s0[owner], j);
@@ -1336,7 +1349,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
 #else
       for (int q = 0; q < per; q++) {
         const int item = lane * per + q;
-        const int orank = item / B, b = item - orank * B;
+        const int orank = rej_div(item, B, mB), b = item - orank * B;
         if (orank < nact) {
           const int owner = (int)L->owner_of[orank];
           const int j = (int)L->base[owner] + b;
@@ -2556,6 +2569,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
 
   const uint32_t T = (uint32_t)tk.T;
   const uint32_t wpp = (uint32_t)tk.wpp;
+  // x / wpp as a shift when walks-per-point is a power of two (every shipped config)
+  const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
+  auto divw = [&](uint32_t x) -> uint32_t { return wsh >= 0 ? x >> wsh : x / wpp; };
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
   uint32_t c_iters = 0;
 
@@ -2583,15 +2599,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
         if (c >= T) { exhausted = true; break; }
         wq = c;
         we = (T - c) < G_win ? T : c + G_win;
-        wp0 = c / wpp;
-        const uint32_t np = (we - 1) / wpp - wp0 + 1;
+        wp0 = divw(c);
+        const uint32_t np = divw(we - 1) - wp0 + 1;
         wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
       }
       const int avail = (int)(we - wq);
       const int take = (kWave - S) < avail ? (kWave - S) : avail;
       const int pos = ((lane - head) & (kWave - 1)) - S;
       const bool mine = pos >= 0 && pos < take;
-      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = q / wpp;
+      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = divw(q);
       const uint32_t pidx = (uint32_t)__shfl((int)wperm, (int)(qp - wp0));  // queue position -> permuted point
       if (mine) {
         s_t = pidx * wpp + (q - qp * wpp);
@@ -2647,8 +2663,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
             tk.code[t] = 0u;
             t = -1;
           } else {
-            const uint32_t pidx = v_t / wpp;
-            const uint32_t w = (v_t - pidx * wpp) / (uint32_t)prm.n_anti;
+            const uint32_t pidx = divw(v_t);
+            const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
             for (int kk = 0; kk < DIM; kk++) { st.pt[kk] = v_pt[kk]; st.n[kk] = 0.0f; st.prevDir[kk] = 0.0f; }
             // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
             // and every step rewrites them before that can happen

@@ -172,7 +172,9 @@ int wos_solve_stats(wos_scene *scene, uint64_t ticket, wos_stats *stats);
 /* Device self-test of the deterministic math used by the kernel (for the
  * GPU-vs-oracle parity tests): which = 0 exp, 1 log, 2 sin, 3 cos, 4 atan,
  * 5 sqrt, 6 bessi0, 7 bessi1, 8 bessk0, 9 bessk1 (double); 10 expf, 11 logf,
- * 12 sinf, 13 cosf, 14 cbrtf (float in, float out widened to double). */
+ * 12 sinf, 13 cosf, 14 cbrtf (float in, float out widened to double); 15 sqrtf,
+ * 16 i0_fast, 17 k0_fast, 18-23 the fused double evaluator, 24/25 I0/K0 of the fused
+ * float pair of the rejection fast path. */
 int wos_selftest_math(int32_t which, const double *x, double *out, int64_t n, int32_t device);
 
 const char *wos_last_error(void);

@@ -998,6 +998,45 @@ __device__ __forceinline__ float k1_fast(float x) {
          y * (0.1504268e-1f + y * (-0.780353e-2f + y * (0.325614e-2f + y * (-0.68245e-3f)))))));
 }
 
+// K0 and I0 of the rejection fast path at one argument: the polynomials of
+// k0_fast / i0_fast, with I0 and x^-1/2 shared (k0_fast at x <= 2 re-evaluates I0) and
+// the divisions by / of x as reciprocal products.  The reciprocals add ~1 ulp to y,
+// far inside the 8e-6 band the decisions are certified with (the GPU self-test checks
+// the <= 2e-6 error against the double-precision A&S functions).
+#ifndef WOS_FUSED_K0I0
+#define WOS_FUSED_K0I0 1
+#endif
+__device__ __forceinline__ void k0i0_fast(float x, float* k0, float* i0) {
+  if (!WOS_FUSED_K0I0) { *k0 = k0_fast(x); *i0 = i0_fast(x); return; }
+  const float rs = __builtin_amdgcn_rsqf(x);
+  const float rx = __builtin_amdgcn_rcpf(x);
+  float iv;
+  if (x < 3.75f) {
+    float y = x * 0.266666681f;
+    y = y * y;
+    iv = 1.0f + y * (3.5156229f + y * (3.0899424f + y * (1.2067492f + y * (0.2659732f + y * (0.360768e-1f +
+         y * 0.45813e-2f)))));
+  } else {
+    const float y = 3.75f * rx;
+    const float poly = 0.39894228f + y * (0.1328592e-1f + y * (0.225319e-2f + y * (-0.157565e-2f + y * (0.916281e-2f +
+                       y * (-0.2057706e-1f + y * (0.2635537e-1f + y * (-0.1647633e-1f + y * 0.392377e-2f)))))));
+    iv = exp_fast(x) * rs * poly;
+  }
+  float kv;
+  if (x <= 2.0f) {
+    const float y = x * x * 0.25f;
+    kv = (-__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * iv +
+         (-0.57721566f + y * (0.42278420f + y * (0.23069756f + y * (0.3488590e-1f + y * (0.262698e-2f +
+          y * (0.10750e-3f + y * 0.74e-5f))))));
+  } else {
+    const float y = 2.0f * rx;
+    kv = exp_fast(-x) * rs * (1.25331414f + y * (-0.7832358e-1f + y * (0.2189568e-1f +
+         y * (-0.1062446e-1f + y * (0.587872e-2f + y * (-0.251540e-2f + y * 0.53208e-3f))))));
+  }
+  *k0 = kv;
+  *i0 = iv;
+}
+
 // Certain-reject bound of the Yukawa rejection test.  The test accepts iff
 // u < T(r) = (K0(mu r) - rho I0(mu r)) r / (norm bound) (2D) or
 // (e^{-mu r} - rho sinh(mu r)) r / (norm bound) (3D), with rho = A0/A1 > 0 and the
@@ -1072,7 +1111,9 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
       decided = 0;
     } else if (fast) {
       const float mur = g.r * g.sqrtLambda;
-      const float k0 = k0_fast(mur), ip = i0_fast(mur) * rho;
+      float k0, i0v;
+      k0i0_fast(mur, &k0, &i0v);
+      const float ip = i0v * rho;
       const float c = g.r * invNB;
       const float Tf = (k0 - ip) * c;
       const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
@@ -1190,7 +1231,9 @@ __device__ __forceinline__ void rej_draws(const DevParams& prm, uint64_t s0, int
 // fast decision of one iteration: 1 accept, 0 reject, -1 undecided (see sample_volume)
 __device__ __forceinline__ int rej_fast_decide(float u, float r, float sqrtL, float rho, float invNB) {
   const float mur = r * sqrtL;
-  const float k0 = k0_fast(mur), ip = i0_fast(mur) * rho;
+  float k0, i0v;
+  k0i0_fast(mur, &k0, &i0v);
+  const float ip = i0v * rho;
   const float c = r * invNB;
   const float Tf = (k0 - ip) * c;
   const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
@@ -2911,6 +2954,9 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
     case 21: { double a; bessel_ik<false, true>(v, nullptr, nullptr, &a, &r); } break;
     case 22: { double a, b, c; bessel_ik<true, true>(v, &a, &r, &b, &c); } break;
     case 23: { double a, b, c; bessel_ik<true, true>(v, &a, &b, &c, &r); } break;
+    // the fused float pair of the rejection fast path (k0i0_fast): 24 I0, 25 K0
+    case 24: { float k, i; k0i0_fast((float)v, &k, &i); r = (double)i; } break;
+    case 25: { float k, i; k0i0_fast((float)v, &k, &i); r = (double)k; } break;
     default: r = __builtin_nan("");
   }
   out[i] = r;

@@ -342,7 +342,7 @@ def test_gpu_matches_golden_fixture(gpu, name):
     assert_bits_equal(g, ref["grad"])
 
 
-@pytest.mark.parametrize("which,ref_which", [(16, 0), (17, 2)])
+@pytest.mark.parametrize("which,ref_which", [(16, 0), (17, 2), (24, 0), (25, 2)])
 def test_fast_bessel_error_within_certified_band(gpu, oracle, which, ref_which):
     """The float Bessel approximations of the rejection fast path must stay well inside
     the 8e-6 relative band the kernel certifies its decisions with."""

@@ -2338,7 +2338,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
 
 // LDS image: prims | silhouettes | prim groups | silhouette groups (each block 16-B aligned)
 template <int DIM, bool GG>
-__device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
+__device__ __forceinline__ LGeom geometry_view(const DevScene& sc, float* smem, bool with_sil, bool copy) {
   constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
   const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
   const int primAl = (primN + 3) & ~3, silAl = (silN + 3) & ~3;
@@ -2367,6 +2367,7 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
   float* dbase = smem + primAl + silAl + pgN + sgN + sgridAl;
   G.dprim = with_sil ? dbase : sc.dprim;
   G.dgroup = with_sil ? dbase + dpAl : sc.dgroup;
+  if (!copy) return G;
   for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
   if (with_sil) {
     for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
@@ -2378,6 +2379,34 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
     for (int i = threadIdx.x; i < dgN; i += kBlock) dbase[dpAl + i] = sc.dgroup[i];
   }
   return G;
+}
+
+template <int DIM, bool GG>
+__device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
+  return geometry_view<DIM, GG>(sc, smem, with_sil, true);
+}
+
+// Kernel parameters re-read inside a loop: the view goes through an opaque copy of
+// the pointer to the kernarg block, so every use in an iteration is a scalar load
+// (scalar-cache hit) instead of a value held in SGPRs for the whole kernel.  The
+// walk kernel's loop-invariant scene / parameter / task fields and the constants
+// hoisted next to them otherwise overflow the SGPR file, whose spills into VGPR
+// lanes then push the VGPRs into scratch.
+#ifndef WOS_KVIEW
+#define WOS_KVIEW 1
+#endif
+// The walk kernel's parameters as they lie in the kernarg segment (the ABI lays the
+// arguments out like the members of this struct: declaration order, natural alignment).
+struct WalkKernArgs {
+  DevScene sc;
+  DevParams prm;
+  DevTasks tk;
+};
+using KernArgsPtr = const __attribute__((address_space(4))) WalkKernArgs*;
+__device__ __forceinline__ KernArgsPtr kernargs_opaque() {
+  KernArgsPtr q = (KernArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  if (WOS_KVIEW) asm volatile("" : "+s"(q));
+  return q;
 }
 
 __device__ __forceinline__ void flush_counter(unsigned long long* counters, int slot, uint32_t v, int lane) {
@@ -2591,15 +2620,19 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 #endif
 template <int DIM, bool GG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK_WAVES_PER_EU))) void wos_walk_kernel(
-    const DevScene sc, const DevParams prm, const DevTasks tk, int64_t base, int64_t stride,
+    const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int s_ctr[C_NUM];
+  const DevScene& sc = sc_arg;
+  const DevParams& prm = prm_arg;
+  const DevTasks& tk = tk_arg;
   const int lane = threadIdx.x & (kWave - 1);
-  const LGeom G = stage_geometry<DIM, GG>(sc, smem, true);
+  const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
   // per-wave scratch shared by the star and ray queries (used one after the other)
-  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + (threadIdx.x / kWave) * walk_scratch_bytes<DIM>();
+  const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // wave-uniform: SGPR address
+  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();
   StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
   RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
@@ -2633,7 +2666,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
   uint32_t s_t = 0, s_ok = 0;  // staged task index, its point is estimated
   float s_pt[DIM], s_thr = 0.0f, s_tsrc = 0.0f, s_dd = 0.0f;
   for (int k = 0; k < DIM; k++) s_pt[k] = 0.0f;
-  auto refill = [&]() {
+  auto refill = [&](const DevTasks& tk) {
     while (S < kWave && !exhausted) {
       if (wq >= we) {
         unsigned int c = 0;
@@ -2666,7 +2699,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
       wq += (uint32_t)take;
     }
   };
-  refill();
+  refill(tk);
   int64_t t = -1;           // this lane's task
   int wmax = 0;             // longest live walk of the wave (steps), wave-uniform
   WalkState<DIM> st;
@@ -2677,6 +2710,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
 
   for (;;) {
     DIAG_T0(t_loop);
+    // per-iteration views of the kernel parameters and of the staged geometry (see kview)
+    KernArgsPtr ka = kernargs_opaque();
+    const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
+    const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
+    const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
+    const LGeom G = WOS_KVIEW ? geometry_view<DIM, GG>(sc, smem, true, false) : G0;
     // ---- hand staged tasks to idle lanes (uniform control flow)
     {
       const uint64_t need = __ballot(t < 0);
@@ -2729,7 +2768,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
     }
     if (__ballot(t >= 0) == 0) {
       if (S == 0 && exhausted) break;  // queue drained and every lane idle
-      refill();
+      refill(tk);
       continue;
     }
 #if WOS_PRIO || WOS_DRAIN
@@ -2797,7 +2836,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
                 1u);
       t = -1;
     }
-    refill();
+    refill(tk);
     DIAG_ADD(D_LOOP, t_loop);
   }
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Benchmark: WoS walk-steps/sec + pressure-projection wall-time per step,
-2D karman 64k points x 128 walks (BASELINE.json configs[1] / metric).
+"""Benchmark: WoS walk-steps/sec + pressure-projection wall-time per step
+(BASELINE.json metric), default workload config B: karman 2D, 64k points x 128 walks.
 
 One "step" = one pressure projection: the walk-on-stars solve over every query
 point (inputs already resident in HBM) followed, for N>1 GPUs, by the single
@@ -8,16 +8,23 @@ RCCL all-gather of [p, grad] that hands every rank the full field.  Points are
 sharded by stride across ranks (no data-path collective during the solve); the
 RNG is keyed by the global point index so results do not depend on N.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|B_grid|C|D|E|A]
+                    [--scaling weak|strong]
     torchrun --nproc-per-node N bench.py --gpus N ...   (multi-GPU, RCCL)
+
+Scaling: "weak" (default for B) gives every rank one 64k-point batch of an
+N x 64k projection; "strong" (default for the grid configs C, D, E -- BASELINE's
+8-GPU configs are fixed-size problems) shards the config's fixed point set.
 
 Prints ONE JSON line on rank 0.  `value` counts the ball steps of recorded walks
 (the first ball + every walk() iteration, walk_on_stars.h:523,182); steps of
 dropped walks (escaped / over max length) are reported separately as wasted.
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -27,17 +34,21 @@ sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-FP64_VECTOR_PEAK_TFLOPS = 78.6  # dense FP64 vector peak (spec)
+# MI355X_MICROARCH.md chip table (spec, dense)
+HBM_PEAK_GBS = 8000.0
+FP32_VECTOR_PEAK_TFLOPS = 157.3
+FP64_VECTOR_PEAK_TFLOPS = 78.6
+LIB = os.path.join(PKG, "lib", "libwos_hip.so")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--walks", type=int, default=128)
-    ap.add_argument("--points", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="B", help="A, B, B_grid, C, D or E (SURVEY.md section 8(d))")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"])
+    ap.add_argument("--points", type=int, default=65536, help="config B: random points per rank (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
@@ -46,6 +57,13 @@ def parse():
                     help="wait for every solve before enqueueing the next (default: the next projection is "
                          "enqueued while the previous one runs; its stats are read after)")
     return ap.parse_args()
+
+
+def lib_sha16():
+    try:
+        return hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 def algorithmic_bytes(n_points, dim, total_steps, grid_elems):
@@ -64,37 +82,43 @@ def walk_kernel_bytes(walk_kernel_steps, grid_elems):
     return 4 * walk_kernel_steps + 4 * grid_elems
 
 
-def measured_traffic(points, walks):
-    """HBM bytes per walk-kernel launch from the committed rocprofv3 PMC passes
-    (tools/collect_traffic.py -> profiles/*walk_traffic.json), if they were taken
-    on this configuration; else None."""
+def algorithmic_flops_per_step(n_sil, n_prims, rej_iters_per_step):
+    """F ~ 20 S_sil + 15 N_prim + I_rej x 60 (FP64) + 250 (FP64 ball
+    Bessels + Poisson kernel) per walk step, S_sil / N_prim the scene's silhouette
+    candidates / Neumann primitives (the brute-force query cost of fcpw's Baseline,
+    baseline.inl:60-260), I_rej the measured rejection iterations per step."""
+    f32 = 20.0 * n_sil + 15.0 * n_prims
+    f64 = 60.0 * rej_iters_per_step + 250.0
+    return f32, f64
+
+
+def committed_profile(suffix, cfg_name):
+    """A committed rocprofv3 profile (profiles/*<suffix>) of THIS library build on this
+    configuration: stamped with the sha of libwos_hip.so it was measured on; a stale
+    profile (kernel changed since) is not reported."""
     prof = os.path.join(REPO, "profiles")
+    sha = lib_sha16()
     best = None
-    if os.path.isdir(prof):
+    if os.path.isdir(prof) and sha:
         for f in sorted(os.listdir(prof)):
-            if f.endswith("walk_traffic.json"):
+            if f.endswith(suffix):
                 try:
                     d = json.load(open(os.path.join(prof, f)))
                 except (OSError, ValueError):
                     continue
-                if d.get("points") == points and d.get("walks") == walks:
-                    best = d
+                if d.get("lib_sha16") == sha and d.get("config", "B") == cfg_name:
+                    best = dict(d, file=f)
     return best
 
 
-def measured_issue():
-    """Vector-instruction issue of the walk kernel from the committed rocprofv3 SQ
-    pass (tools/collect_sq.py -> profiles/*walk_sq.json), if any."""
-    prof = os.path.join(REPO, "profiles")
-    best = None
-    if os.path.isdir(prof):
-        for f in sorted(os.listdir(prof)):
-            if f.endswith("walk_sq.json"):
-                try:
-                    best = json.load(open(os.path.join(prof, f)))
-                except (OSError, ValueError):
-                    continue
-    return best
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or None
 
 
 def cpu_baseline(cfg, n_threads, budget_s):
@@ -102,38 +126,46 @@ def cpu_baseline(cfg, n_threads, budget_s):
     bounded, strided sample of the same workload -- a reported baseline only."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
-    import objparse
-    v, ix = objparse.load(cfg["obj"], 2)
-    osc = oracle_lib.OracleScene(v, ix, cfg["source"], float(cfg["scene"]["absorptionCoeff"]))
-    prm = oracle_lib.make_params(cfg["solver"], cfg["output"], math_mode=0, n_threads=n_threads)
+    osc = oracle_lib.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"],
+                                 **cfg["scene_kw"])
     pts = cfg["points"]
+    n = pts.shape[0]
+
+    def run(sample_stride, threads, cap_pts=None):
+        sample = pts[::sample_stride]
+        if cap_pts is not None:
+            sample = sample[:cap_pts]
+        prm = oracle_lib.make_params(cfg["solver"], cfg["output"], math_mode=0, n_threads=threads)
+        t0 = time.perf_counter()
+        _, _, _, _, st = oracle_lib.solve(osc, prm, sample, index_base=0, index_stride=sample_stride)
+        return time.perf_counter() - t0, st, sample.shape[0]
+
     # calibrate on a small slice, then size the sample to ~budget_s of wall time
-    stride = max(1, pts.shape[0] // 512)
-    t0 = time.perf_counter()
-    _, _, _, _, st = oracle_lib.solve(osc, prm, pts[::stride], index_base=0, index_stride=stride)
-    dt = time.perf_counter() - t0
-    per_pt = dt / max(1, pts[::stride].shape[0])
-    n_sample = int(min(pts.shape[0], max(512, budget_s / max(per_pt, 1e-9))))
-    stride = max(1, pts.shape[0] // n_sample)
-    sample = pts[::stride]
-    t0 = time.perf_counter()
-    _, _, _, _, st = oracle_lib.solve(osc, prm, sample, index_base=0, index_stride=stride)
-    dt = time.perf_counter() - t0
-    # one core on a smaller strided subset (BASELINE.md asks for both)
-    prm1 = oracle_lib.make_params(cfg["solver"], cfg["output"], math_mode=0, n_threads=1)
-    s1 = max(1, pts.shape[0] // 1024)
-    t1 = time.perf_counter()
-    _, _, _, _, st1 = oracle_lib.solve(osc, prm1, pts[::s1], index_base=0, index_stride=s1)
-    dt1 = time.perf_counter() - t1
+    stride = max(1, n // 512)
+    dt, st, m = run(stride, n_threads)
+    per_pt = dt / max(1, m)
+    n_sample = int(min(n, max(256, budget_s / max(per_pt, 1e-9))))
+    stride = max(1, n // n_sample)
+    dt, st, m = run(stride, n_threads)
+    # one core on a smaller strided subset (BASELINE.md asks for both), ~budget/4
+    s1 = max(1, int(n / max(16, (budget_s / 4) / max(per_pt * n_threads, 1e-9))))
+    dt1, st1, m1 = run(s1, 1)
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     return {
-        "value_1core": st1["walk_steps"] / dt1,
         "value": st["walk_steps"] / dt,
         "unit": "walk-steps/s",
         "cores": n_threads,
         "kind": "port",
-        "sample": f"{sample.shape[0]} of {pts.shape[0]} karman points (stride {stride}), {cfg['solver']['nWalks']} "
-                  f"walks/pt, oracle/wos_oracle.c det math, {dt:.2f} s wall",
-        "projection_s_extrapolated": dt * pts.shape[0] / sample.shape[0],
+        "sample": f"{m} of {n} points of config {cfg['config_name']} (stride {stride}), "
+                  f"{cfg['solver']['nWalks']} walks/pt, oracle/wos_oracle.c det math, {dt:.2f} s wall on "
+                  f"{n_threads} threads",
+        "value_1core": st1["walk_steps"] / dt1,
+        "sample_1core": f"{m1} points (stride {s1}), {dt1:.2f} s wall",
+        "host_cpus_visible": ncpu,
+        "cpu_share": os.environ.get("OMP_NUM_THREADS"),
+        "cpu_model": cpu_model(),
+        "projection_s_extrapolated": dt * n / m,
+        "wasted_steps_per_s": st["wasted_steps"] / dt,
     }
 
 
@@ -142,6 +174,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    scaling = a.scaling or ("weak" if a.config == "B" else "strong")
+    if scaling == "weak" and a.config != "B":
+        raise SystemExit("weak scaling is defined for config B (random points per rank); use --scaling strong")
     import torch
     import torch.distributed as dist
     from wos_amd import WosScene, solver_params, workloads
@@ -150,13 +185,13 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    # weak scaling: every rank owns one 64k-point batch of a world*64k global projection
-    cfg = workloads.karman_config(n_walks=a.walks, n_points=a.points * world)
+    cfg = workloads.config_by_name(a.config, n_points=a.points * world if scaling == "weak" else None)
     pts_all = cfg["points"]
     n_all = pts_all.shape[0]
-    dim = 2
-    scene = WosScene.from_obj(cfg["obj"], 2, torch.from_numpy(cfg["source"]).to(dev),
-                              float(cfg["scene"]["absorptionCoeff"]), watertight=True, device=local_rank)
+    dim = cfg["dim"]
+    scene = WosScene(cfg["vertices"], cfg["prims"], torch.from_numpy(cfg["source"]).to(dev), cfg["absorption"],
+                     watertight=True, device=local_rank, **cfg["scene_kw"])
+    info = scene.info()
     params = solver_params(cfg["solver"], cfg["output"])
 
     # stride sharding keyed by global index (load balance: near-wall points are slower)
@@ -183,7 +218,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps_rec = steps_all = 0
+    steps_rec = steps_all = rej_iters = 0
     kernel_ms, walk_ms, fb_ms, fold_ms, walk_kernel_steps, launches = [], [], [], [], 0, 0
     # one projection in flight behind the one whose counters are read (device counters,
     # copied per solve; wos_solve_stats waits only for that solve)
@@ -194,6 +229,7 @@ def main():
         st = scene.solve_stats(tickets[k])
         steps_rec += st["walk_steps"]
         steps_all += st["walk_steps"] + st["wasted_steps"]
+        rej_iters += st["rejection_iters"]
         kernel_ms.append(st["kernel_ms"])
         walk_ms.append(st["walk_ms"])
         fb_ms.append(st["first_ball_ms"])
@@ -221,11 +257,20 @@ def main():
         kms = float(np.mean(kernel_ms))
         # dominant kernel: wos_walk_kernel, timed with HIP events on the solve's stream
         wms = float(np.sum(walk_ms) / max(1, launches))
-        wbytes = walk_kernel_bytes(walk_kernel_steps / max(1, launches), cfg["source"].size)
+        wk_steps_launch = walk_kernel_steps / max(1, launches)
+        wbytes = walk_kernel_bytes(wk_steps_launch, cfg["source"].size)
         achieved = wbytes / (wms * 1e-3) / 1e9
-        steps_per_launch = steps_all / a.steps / world
-        pbytes = algorithmic_bytes(n_local, dim, steps_per_launch, cfg["source"].size)
-        tr = measured_traffic(a.points, a.walks)
+        local_steps_all = steps_all / world  # rank 0's share (stride sharding: balanced)
+        pbytes = algorithmic_bytes(n_local, dim, local_steps_all / a.steps, cfg["source"].size)
+        tr = committed_profile("walk_traffic.json", a.config)
+        sq = committed_profile("walk_sq.json", a.config)
+        # FLOP roofline of the walk kernel (the meaningful one: SURVEY.md 8(d))
+        f32, f64 = algorithmic_flops_per_step(info["n_silhouettes"], info["n_prims"],
+                                              rej_iters / max(1.0, local_steps_all))
+        wk_flops32, wk_flops64 = f32 * wk_steps_launch, f64 * wk_steps_launch
+        t_need = wk_flops32 / (FP32_VECTOR_PEAK_TFLOPS * 1e12) + wk_flops64 / (FP64_VECTOR_PEAK_TFLOPS * 1e12)
+        achieved_tf = (wk_flops32 + wk_flops64) / (wms * 1e-3) / 1e12
+        mixed_peak = (wk_flops32 + wk_flops64) / max(t_need, 1e-30) / 1e12
         line = {
             "metric": "WoS walk-steps/sec + pressure-projection wall-time per step, 2D karman 64k pts",
             "value": steps_rec / elapsed,
@@ -235,41 +280,48 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": "karman2d: geometry_1cyl_long_open.obj, lambda=350, RR 0.99, "
-                                   f"{n_all} random query pts ({world} x 256^2 minus cylinder), {a.walks} walks/pt",
-                       "points": n_all, "walks_per_point": a.walks, "source_grid": list(cfg["source"].shape),
+            "config": {"workload": cfg["desc"], "name": a.config, "points": n_all,
+                       "walks_per_point": cfg["solver"]["nWalks"], "source_grid": list(cfg["source"].shape),
                        "parallelism": f"points sharded by stride over {world} GPU(s) + 1 RCCL all-gather"},
             "projection_ms": elapsed / a.steps * 1e3,
             "enqueue": "blocking" if a.blocking else "pipelined (next projection enqueued before the previous one's stats are read)",
             "kernel_ms": kms,
             "walk_steps_per_projection": steps_rec / a.steps,
             "wasted_steps_per_projection": (steps_all - steps_rec) / a.steps,
+            "lib_sha16": lib_sha16(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": tr["bytes_per_launch"] if tr else None,
                          "kernel": "wos_walk_kernel", "kernel_ms": wms,
                          "algorithmic_bytes_per_launch": wbytes,
-                         "traffic_source": tr["source"] if tr else None,
+                         "walk_kernel_steps_per_launch": wk_steps_launch,
+                         "traffic_source": (f"{tr['file']}: {tr['source']}" if tr else
+                                            "no committed PMC profile of this library build on this config"),
                          "projection_achieved_GBps": pbytes / (kms * 1e-3) / 1e9},
+            "flop_roofline": {"bound": "valu", "achieved": achieved_tf, "peak": mixed_peak, "unit": "TFLOP/s",
+                              "frac": t_need / (wms * 1e-3), "kernel": "wos_walk_kernel",
+                              "flops_per_step_fp32": f32, "flops_per_step_fp64": f64,
+                              "peaks": {"fp32": FP32_VECTOR_PEAK_TFLOPS, "fp64": FP64_VECTOR_PEAK_TFLOPS},
+                              "model": "SURVEY.md 8(d): 20 S_sil + 15 N_prim (fp32) + 60 I_rej + 250 (fp64) per "
+                                       "step; frac = (F32/P32 + F64/P64) / kernel time"},
             "valu_issue": None,
             "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
                                 "fold": float(np.mean(fold_ms)), "total": kms},
         }
-        sq = measured_issue()
         if sq:
             line["valu_issue"] = {"kernel": sq["kernel"], "frac": sq["valu_issue_frac"],
                                   "wait_any_frac": sq["wait_any_frac"], "wait_inst_frac": sq["wait_inst_frac"],
-                                  "source": sq["source"]}
-        if world == 1 and not a.no_projection_wall:
+                                  "source": f"{sq['file']}: {sq['source']}"}
+        if world == 1 and a.config == "B" and not a.no_projection_wall:
             # the metric's second half: wall time of one whole projection call as the
             # time-stepper issues it (fresh Scene(sceneConfig, div) + wost, model_split.py:185-202)
             sys.path.insert(0, os.path.join(REPO, "tools"))
             from projection_timing import projection_timings
-            pt = projection_timings(steps=3, n_walks=a.walks)
+            pt = projection_timings(steps=3, n_walks=cfg["solver"]["nWalks"])
             line["projection_wall"] = {
                 "device_handoff_ms": pt["device_fresh_scene_ms"],
                 "reference_handoff_ms": pt["ref_style_ms"],
@@ -278,7 +330,9 @@ def main():
                         "div/points via .cpu().numpy(), nested-list outputs, grad p back to the device",
             }
         if world == 1 and not a.no_cpu_baseline:
-            threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib
+            threads = a.cpu_threads or oracle_lib.default_threads()
             line["cpu_baseline"] = cpu_baseline(cfg, threads, a.cpu_budget_s)
         print(json.dumps(line), flush=True)
     scene.close()

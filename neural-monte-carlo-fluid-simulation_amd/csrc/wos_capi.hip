@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -92,6 +93,8 @@ struct DevCtx {
   hipStream_t aux[wos::kMaxPipes] = {};  // pipelines 1.. (pipeline 0 is the caller's stream)
   float* d_rejtab = nullptr;   // rejection bound table, 2D then 3D (DevParams::rej_tab)
   hipEvent_t fork = nullptr, join[wos::kMaxPipes] = {};
+  int stat_waiters = 0;        // wos_solve_stats calls waiting on a slot's event without the lock
+  std::condition_variable no_waiters;
 };
 
 constexpr int kMaxDevices = 64;
@@ -475,7 +478,9 @@ int wos_release_caches(int32_t device) {
   for (int dv = 0; dv < std::min(ndev, kMaxDevices); dv++) {
     if (device >= 0 && dv != device) continue;
     DevCtx& c = g_ctx[dv];
-    std::lock_guard<std::mutex> lk(c.mu);
+    std::unique_lock<std::mutex> lk(c.mu);
+    // the slot events may be awaited by wos_solve_stats outside the lock
+    c.no_waiters.wait(lk, [&] { return c.stat_waiters == 0; });
     if (!c.ready) continue;
     HIP_TRY(hipSetDevice(dv));
     HIP_TRY(hipDeviceSynchronize());
@@ -862,14 +867,31 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
 
 int wos_solve_stats(wos_scene* s, uint64_t ticket, wos_stats* stats) {
   if (!s || !stats) return fail(WOS_E_INVALID, "wos_solve_stats: null scene/stats");
-  std::lock_guard<std::mutex> lock(s->mu);
-  HIP_TRY(hipSetDevice(s->device));
-  DevCtx& c = g_ctx[s->device];
-  std::lock_guard<std::mutex> lk(c.mu);
-  StatSlot& q = c.slot[ticket % kStatSlots];
-  if (ticket == 0 || q.ticket != ticket)
+  const auto unknown = [&] {
     return fail(WOS_E_INVALID, "wos_solve_stats: unknown ticket (more than " + std::to_string(kStatSlots) +
                                    " solves were enqueued on this device after it)");
+  };
+  HIP_TRY(hipSetDevice(s->device));
+  DevCtx& c = g_ctx[s->device];
+  hipEvent_t done = nullptr;
+  {
+    // only the ticket check and the event handle under the locks: waiting here would
+    // stall every other enqueuer on the device behind this solve
+    std::lock_guard<std::mutex> lock(s->mu);
+    std::lock_guard<std::mutex> lk(c.mu);
+    StatSlot& q = c.slot[ticket % kStatSlots];
+    if (ticket == 0 || q.ticket != ticket) return unknown();
+    done = q.done;
+    c.stat_waiters++;
+  }
+  const hipError_t e = hipEventSynchronize(done);
+  std::lock_guard<std::mutex> lock(s->mu);
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (--c.stat_waiters == 0) c.no_waiters.notify_all();
+  if (e != hipSuccess) return fail(WOS_E_DEVICE, std::string("wos_solve_stats: ") + hipGetErrorString(e));
+  StatSlot& q = c.slot[ticket % kStatSlots];
+  // the slot was recycled by a later solve while we waited (its event re-recorded)
+  if (q.ticket != ticket) return unknown();
   HIP_TRY(hipEventSynchronize(q.done));
   return fill_stats(q, stats);
 }

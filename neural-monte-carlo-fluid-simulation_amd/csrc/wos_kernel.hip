@@ -1198,6 +1198,13 @@ __device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0,
 #ifndef WOS_FASTDIV
 #define WOS_FASTDIV 1
 #endif
+// The sampler's generation has items = nact * B with B = clamp(64 / nact, kRejBmin, kRejBcap):
+// items <= 64 when B = floor(64 / nact) or B = kRejBcap (then nact < 2), else
+// items = nact * kRejBmin <= 64 * kRejBmin.  rej_div needs items <= 2048 and B <= 32.
+constexpr int kRejBcap = 32;
+static_assert(kRejBcap <= 32, "rej_div: e = m B - 2^16 < B <= 32");
+static_assert(kWave * (WOS_REJ_BMIN2 > WOS_REJ_BMIN3 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3) <= 2048 && kWave <= 2048,
+              "rej_div: item * e < 2^16 needs items <= 2048");
 __device__ __forceinline__ int rej_div(int item, int B, uint32_t mB) {
   if (!WOS_FASTDIV) return item / B;
   return (int)(((uint32_t)item * mB) >> 16);
@@ -1326,7 +1333,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       // generations -- each costs three wave syncs and the owners' scan -- for a
       // few iterations evaluated past an accept)
       int B = kWave / nact;
-      B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > 32 ? 32 : B);
+      B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > kRejBcap ? kRejBcap : B);
       const int items = nact * B, per = (items + kWave - 1) / kWave;
       // item / B as a multiply-shift (exact: item < 2048, B <= 32, see rej_div)
       const uint32_t mB = (65536u + (uint32_t)B - 1u) / (uint32_t)B;

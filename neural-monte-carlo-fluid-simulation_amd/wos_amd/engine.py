@@ -169,7 +169,9 @@ class WosScene:
         """Solve at query points.  Returns (p [N], grad [N,dim], stats dict[, n_est, steps])
         as numpy arrays for host input, torch tensors for GPU tensor input.  With GPU tensors
         and sync=False the solve is only enqueued on the stream: the stats dict then holds
-        just "ticket"; solve_stats(ticket) waits for that solve and returns the full dict."""
+        just "ticket"; solve_stats(ticket) waits for that solve and returns the full dict.
+        `stream`: a torch.cuda.Stream or a raw hipStream_t handle (default: torch's current
+        stream)."""
         L = _lib.load()
         params = params if params is not None else solver_params()
         st = Stats()
@@ -183,11 +185,24 @@ class WosScene:
             g = torch.empty(n, self.dim, dtype=torch.float32, device=x.device)
             ne = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
             sp = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
-            s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+            if stream is None:
+                s = torch.cuda.current_stream(x.device).cuda_stream
+            elif isinstance(stream, torch.cuda.Stream):
+                s = stream.cuda_stream
+            else:
+                s = int(stream)
             flags = _lib.WOS_PTRS_DEVICE | (0 if sync else _lib.WOS_ASYNC)
             check(L.wos_solve(self._h, C.byref(params), x.data_ptr(), n, index_base, index_stride,
                               p.data_ptr(), g.data_ptr(), ne.data_ptr() if counts else None,
                               sp.data_ptr() if counts else None, C.byref(st), s, flags), "wos_solve")
+            if not sync and stream is not None:
+                # the buffers were allocated on torch's current stream but the enqueued
+                # solve uses them on `stream`: keep the caching allocator from handing
+                # their memory out again before that stream has finished with them
+                ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(s, device=x.device)
+                for t in (x, p, g, ne, sp):
+                    if t is not None:
+                        t.record_stream(ts)
         else:
             if _is_torch(pts):
                 pts = pts.detach().cpu().numpy()

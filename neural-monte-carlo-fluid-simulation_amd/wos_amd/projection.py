@@ -149,8 +149,13 @@ class PressureProjector:
 
     def projection_loss(self, velocity, velocity_prev, grad_p, n_samples, generator=None):
         """_project_velocity (model_split.py:272-283): u <- u_prev - grad p on random
-        pressure samples, grad p indexed on the device."""
-        idx = torch.randint(0, self.samples.shape[0], (n_samples,), device=self.device, generator=generator)
+        pressure samples, grad p indexed on the device.  The index range is the
+        reference's: the 2D caller draws randint(0, N-1) (src/2d/models/model_split.py:274,
+        so the last sample is never drawn), the 3D caller randint(0, N)
+        (src/3d/models/model_split.py:297)."""
+        n = self.samples.shape[0]
+        hi = n - 1 if self.dim == 2 else n
+        idx = torch.randint(0, hi, (n_samples,), device=self.device, generator=generator)
         x = self.samples[idx]
         with torch.no_grad():
             target = velocity_prev(x) - grad_p[idx]

@@ -241,3 +241,54 @@ def gear_config(n_teeth=160, n_walks=64, res=24, holes=3, seed=7):
     return {"name": "gear2d", "dim": 2, "vertices": v, "prims": ix, "source": src, "points": pts,
             "solver": solver, "output": dict(OUTPUT_BASE), "absorption": 350.0}
 
+
+
+def _with_geometry(cfg, dim, flip=False):
+    """Adds vertices / prims (the reference's OBJ parsing rules, engine.load_obj) to a
+    config that names an OBJ, so every config has the same keys."""
+    if "vertices" not in cfg:
+        from .engine import load_obj
+        cfg["vertices"], cfg["prims"] = load_obj(cfg["obj"], dim, flip, False)
+    cfg.setdefault("absorption", float(cfg.get("scene", {}).get("absorptionCoeff", 350.0)))
+    kw = {}
+    if cfg.get("dprims") is not None:
+        kw = {"dvertices": cfg["dvertices"], "dprims": cfg["dprims"], "dirichlet_value": 1.0}
+    cfg["scene_kw"] = kw
+    return cfg
+
+
+# BASELINE.json configs by short name (SURVEY.md section 8(d) table):
+#   A  taylorgreen 2D, 32x32 points, 32 walks (maxWalkLength 10000; flipped to make
+#      the points inside -- as shipped every point is outside and the solve is empty)
+#   B  karman 2D, 64k random points (256^2 minus the cylinder), 128 walks (the metric)
+#   B_grid  karman 2D, 256x128 grid, 128 walks
+#   C  unit box + Dirichlet disk (synthetic), 512^2 points, 256 walks
+#   D  cube 3D, 128^3 points, 64 walks
+#   E  cube 3D, 256^3 points, 128 walks
+CONFIG_NAMES = ("A", "B", "B_grid", "C", "D", "E")
+
+
+def config_by_name(name, n_points=None):
+    if name == "A":
+        cfg = _with_geometry(taylorgreen_config(n_walks=32, res=32, flip=True), 2, flip=True)
+        desc = "taylorgreen2d (flipped square.obj), 32x32 cell-centred points, 32 walks, maxWalkLength 10000"
+    elif name == "B":
+        cfg = _with_geometry(karman_config(n_walks=128, n_points=n_points or 65536), 2)
+        desc = (f"karman2d: geometry_1cyl_long_open.obj, lambda=350, RR 0.99, {cfg['points'].shape[0]} random "
+                f"query pts ({n_points or 65536} minus cylinder), 128 walks/pt")
+    elif name == "B_grid":
+        cfg = _with_geometry(karman_config(n_walks=128, grid_points=True), 2)
+        desc = "karman2d, 256x128 cell-centred grid, 128 walks/pt"
+    elif name == "C":
+        cfg = _with_geometry(dirichlet_obstacle_config(n_walks=256, res=512), 2)
+        desc = "unit box (Neumann) + Dirichlet disk r=0.1 (synthetic), 512^2 points, 256 walks/pt"
+    elif name in ("D", "E"):
+        res, walks = (128, 64) if name == "D" else (256, 128)
+        cfg = _with_geometry(cube_config(res=res, n_walks=walks), 3)
+        desc = f"cube3d (cube.obj), {res}^3 cell-centred points, {walks} walks/pt, 82^3 source grid"
+    else:
+        raise KeyError(f"unknown config {name!r} (one of {CONFIG_NAMES})")
+    cfg["config_name"] = name
+    cfg["desc"] = desc
+    cfg["dim"] = int(cfg["vertices"].shape[1])
+    return cfg

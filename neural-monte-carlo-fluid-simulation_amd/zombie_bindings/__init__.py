@@ -10,9 +10,10 @@ of ../lib/libwos_hip.so (there is no CPU path).
 Differences, all deliberate (DESIGN.md "Boundary"):
   * missing required keys raise KeyError instead of abort() (config.h:8-11);
   * RNG seeds are counter-based (solver key "seed", default 0x5EED0001) instead of
-    std::chrono::system_clock, so results are reproducible;
-  * 3D wost solves at the query points it is given (the reference's 3D binding
-    ignores them and solves on a gridRes^3 lattice, zombie3d/demo/grid.h:105-146).
+    std::chrono::system_clock, so results are reproducible.
+Like the reference, 2D and 3D wost solve at the query points they are given
+(createSolutionGrid(..., pts), zombie/demo/grid.h:69-102; createSolutionGrid_3d,
+zombie3d/demo/grid.h:105-146 iterates the passed points).
 Extensions: numpy / torch inputs are accepted without nested-list conversion, a
 torch CUDA tensor of points stays on the GPU; optional scene key
 "dirichletBoundary" (OBJ) + "dirichletValue" adds Dirichlet geometry.

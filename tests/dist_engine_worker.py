@@ -1,0 +1,48 @@
+"""One rank of the multi-process sharded projection on the HIP engine (launched as a
+fresh child process by tests/test_distributed.py::test_sharded_projection_hip_engine).
+
+    python tests/dist_engine_worker.py RANK WORLD PORT OUT_DIR
+
+Every rank drives the engine on GPU 0 (a one-GPU box): it solves its stride shard
+of the karman points, keyed by global point index, then the shards are gathered over
+gloo on CPU tensors (wos_amd.dist.sharded_projection, the same path bench.py runs
+over RCCL) and rank r writes the full field to OUT_DIR/rank<r>.npz."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "neural-monte-carlo-fluid-simulation_amd")]
+
+
+def main():
+    rank, world, port, out_dir = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from wos_amd import WosScene, solver_params, workloads
+    from wos_amd import dist as wdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = workloads.config_by_name("B")
+    pts = cfg["points"][:4099]
+    dev = torch.device("cuda", 0)
+    sc = WosScene(cfg["vertices"], cfg["prims"], torch.from_numpy(cfg["source"]).to(dev), 350.0,
+                  watertight=True, device=0)
+    prm = solver_params(dict(cfg["solver"], nWalks=64), cfg["output"])
+
+    def solve_local(local, base, stride):
+        x = torch.from_numpy(np.ascontiguousarray(local)).to(dev)
+        p, g, st = sc.solve(x, prm, index_base=base, index_stride=stride)
+        assert st["points_estimated"] > 0
+        return p.cpu(), g.cpu()
+
+    p, g = wdist.sharded_projection(solve_local, pts, rank, world, 2)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), p=p.numpy(), g=g.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+    sc.close()
+
+
+if __name__ == "__main__":
+    main()

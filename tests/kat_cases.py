@@ -1,0 +1,136 @@
+"""Analytic known-answer cases of the screened Poisson problem the WoSt estimator
+solves, shared by the oracle KATs (tests/test_oracle.py) and the HIP-path KATs
+(tests/test_gpu_kat.py).
+
+The estimator integrates +G f (walk_on_stars.h:262-276) with the Yukawa Green's
+function of -lap + lambda (distributions.h:573-832), so with zero-flux Neumann
+walls it solves  -lap p + lambda p = f.  On an axis-aligned box a cosine mode
+f = prod_k cos(m_k pi (x_k - a_k) / L_k) has zero normal derivative on every wall
+and p = f / (lambda + sum_k (m_k pi / L_k)^2) exactly.
+The source grid is sampled at cell centres of the FLT_EPSILON-padded bbox, the
+layout the engine's nearest-texel lookup reads (scene.h:194-198, image.h:53-58;
+scene_3d.h:120-126).  That lookup is piecewise constant on cells of width h centred
+on the samples; the first-order error f(x) - f(centre) averages out over each cell,
+so for balls spanning many cells the estimator's mean differs from the smooth
+solution by O(h^2): `bias` below bounds it by (h^2 / 8) k^2 max|f| / lambda (three
+times the cell-average estimate h^2 k^2 / 24), and the tolerances carry it.
+
+Each case returns a dict: scene geometry, source grid, solver/output sections,
+query points, the exact p and grad p at them, and the bias bound.
+"""
+import numpy as np
+from scipy import special
+
+from wos_amd import workloads
+
+EPS32 = float(np.finfo(np.float32).eps)
+
+
+def _solver(n_walks, **kw):
+    return dict(workloads.SOLVER_BASE, nWalks=n_walks, **kw)
+
+
+def box2d(lam=350.0, m=1, n=1, n_walks=128, npts=1500, res=1000, seed=0):
+    """Unit square, Neumann walls, f = cos(m pi x) cos(n pi y)."""
+    v, ix = workloads.box_2d(1.0)
+    pmin, pmax = v.min(0) - EPS32, v.max(0) + EPS32
+    ys = (np.arange(res) + 0.5) / res * (pmax[1] - pmin[1]) + pmin[1]
+    xs = (np.arange(res) + 0.5) / res * (pmax[0] - pmin[0]) + pmin[0]
+    X, Y = np.meshgrid(xs, ys)   # rows ~ y
+    f = (np.cos(m * np.pi * X) * np.cos(n * np.pi * Y)).astype(np.float32)
+    pts = np.random.default_rng(seed).uniform(0.05, 0.95, (npts, 2)).astype(np.float32)
+    k2 = (m * np.pi) ** 2 + (n * np.pi) ** 2
+    x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+    pe = np.cos(m * np.pi * x) * np.cos(n * np.pi * y) / (lam + k2)
+    gx = -m * np.pi * np.sin(m * np.pi * x) * np.cos(n * np.pi * y) / (lam + k2)
+    gy = -n * np.pi * np.cos(m * np.pi * x) * np.sin(n * np.pi * y) / (lam + k2)
+    h = (pmax - pmin).max() / res
+    bias = h * h / 8 * k2 / lam
+    return {"name": f"box2d_l{lam:g}_m{m}n{n}", "dim": 2, "vertices": v, "prims": ix, "source": f,
+            "absorption": lam, "solver": _solver(n_walks), "output": {"boundaryDistanceMask": 1e-3},
+            "points": pts, "p": pe, "grad": np.stack([gx, gy], -1), "bias": bias, "kw": {}}
+
+
+def disk2d_dirichlet(lam=4.0, n_walks=256, npts=800, seed=3):
+    """Disk of radius 1, Dirichlet g = 1, f = 0: p = I0(mu r)/I0(mu)."""
+    mu = np.sqrt(lam)
+    dv, dix = workloads.circle_2d((0.0, 0.0), 1.0, 256, clockwise=False)
+    rng = np.random.default_rng(seed)
+    r = np.sqrt(rng.uniform(0.0, 0.7 ** 2, npts))
+    t = rng.uniform(0, 2 * np.pi, npts)
+    pts = np.stack([r * np.cos(t), r * np.sin(t)], -1).astype(np.float32)
+    pe = special.i0(mu * r) / special.i0(mu)
+    gm = mu * special.i1(mu * r) / special.i0(mu)
+    # walks stop in the epsilon shell (1e-3) and take g there (walk_on_stars.h:145,334-341),
+    # and the 256-gon's inscribed circle differs from the unit circle by 1 - cos(pi/256)
+    # ~ 7.5e-5: both shift p by at most |dp/dn| times that distance
+    bias = mu * special.i1(mu) / special.i0(mu) * (1e-3 + 1e-4)
+    return {"name": "disk2d_dirichlet", "dim": 2, "vertices": np.zeros((0, 2), np.float32),
+            "prims": np.zeros((0, 2), np.int32), "source": np.zeros((2, 2), np.float32), "absorption": lam,
+            "solver": _solver(n_walks, ignoreDirichlet=False, russianRouletteThreshold=0.0, maxWalkLength=10000),
+            "output": {"boundaryDistanceMask": 1e-3}, "points": pts, "p": pe,
+            "grad": np.stack([gm * np.cos(t), gm * np.sin(t)], -1), "bias": bias,
+            "kw": {"dvertices": dv, "dprims": dix, "dirichlet_value": 1.0}}
+
+
+def cube3d(lam=350.0, m=1, n=1, l=1, n_walks=128, npts=600, res=82, seed=5):
+    """scenes/cube.obj (the reference's examples/*/cube.obj, [-1,1]^3 up to 1e-6),
+    Neumann walls, f = cos(m pi (x+1)/2) cos(n pi (y+1)/2) cos(l pi (z+1)/2): the 3D
+    analogue of the box KAT.  res^3 source grid, [X][Y][Z]."""
+    import objparse
+    v, ix = objparse.load(workloads.CUBE_OBJ, 3)
+    pmin, pmax = v.min(0) - EPS32, v.max(0) + EPS32
+    axes = [(np.arange(res) + 0.5) / res * (pmax[k] - pmin[k]) + pmin[k] for k in range(3)]
+    X, Y, Z = np.meshgrid(*axes, indexing="ij")
+    kx, ky, kz = m * np.pi / 2, n * np.pi / 2, l * np.pi / 2
+    f = (np.cos(kx * (X + 1)) * np.cos(ky * (Y + 1)) * np.cos(kz * (Z + 1))).astype(np.float32)
+    pts = np.random.default_rng(seed).uniform(-0.9, 0.9, (npts, 3)).astype(np.float32)
+    x, y, z = (pts[:, k].astype(np.float64) for k in range(3))
+    k2 = kx ** 2 + ky ** 2 + kz ** 2
+    cx, cy, cz = np.cos(kx * (x + 1)), np.cos(ky * (y + 1)), np.cos(kz * (z + 1))
+    sx, sy, sz = np.sin(kx * (x + 1)), np.sin(ky * (y + 1)), np.sin(kz * (z + 1))
+    pe = cx * cy * cz / (lam + k2)
+    ge = np.stack([-kx * sx * cy * cz, -ky * cx * sy * cz, -kz * cx * cy * sz], -1) / (lam + k2)
+    h = (pmax - pmin).max() / res
+    bias = h * h / 8 * k2 / lam
+    return {"name": f"cube3d_l{lam:g}_m{m}{n}{l}", "dim": 3, "vertices": v, "prims": ix, "source": f,
+            "absorption": lam, "solver": _solver(n_walks), "output": {"boundaryDistanceMask": 1e-3},
+            "points": pts, "p": pe, "grad": ge, "bias": bias, "kw": {}}
+
+
+def check_unbiased(p, g, case, rel_tol, n_sigma=4.0):
+    """Aggregate checks of one solve against the exact field (independent points):
+    the mean error is within n_sigma standard errors (+ the lookup bias), and the
+    RMS error is a small fraction of the field."""
+    pe, ge, bias = case["p"], case["grad"], case["bias"]
+    err = p - pe
+    assert abs(err.mean()) < n_sigma * err.std() / np.sqrt(err.size) + bias, (err.mean(), err.std(), bias)
+    assert np.sqrt(np.mean(err ** 2)) < rel_tol * np.sqrt(np.mean(pe ** 2))
+    gerr = g - ge
+    assert np.abs(gerr.mean(0)).max() < n_sigma * gerr.std(0).max() / np.sqrt(err.size) + 5 * bias, gerr.mean(0)
+    assert np.sqrt(np.mean(gerr ** 2)) < 2.5 * rel_tol * np.sqrt(np.mean(ge ** 2))
+
+
+def per_point_z(runs_p, runs_g, case):
+    """Per-point z-scores of the seed-averaged estimate against the exact field: K
+    independent solves (different RNG keys) give the per-point standard error
+    sigma_hat / sqrt(K); the lookup bias bound is added in quadrature."""
+    P = np.asarray(runs_p, np.float64)
+    G = np.asarray(runs_g, np.float64)
+    K = P.shape[0]
+    se_p = P.std(0, ddof=1) / np.sqrt(K)
+    se_g = G.std(0, ddof=1) / np.sqrt(K)
+    zp = (P.mean(0) - case["p"]) / np.sqrt(se_p ** 2 + case["bias"] ** 2 + 1e-30)
+    zg = (G.mean(0) - case["grad"]) / np.sqrt(se_g ** 2 + (5 * case["bias"]) ** 2 + 1e-30)
+    return zp, zg
+
+
+def check_z(zp, zg, n_sigma=4.0):
+    """Per-point acceptance: with K seeds the z-scores follow ~Student-t(K-1)
+    (E z^2 = 1.15 for K = 16).  Bar: mean z^2 < 1.5, at most 1 % of the points beyond
+    n_sigma, no point beyond 8, and no systematic shift of the mean z."""
+    for z in (zp, zg.ravel()):
+        assert np.mean(z ** 2) < 1.5, np.mean(z ** 2)
+        assert np.mean(np.abs(z) > n_sigma) <= 0.01, np.mean(np.abs(z) > n_sigma)
+        assert np.abs(z).max() < 8.0, np.abs(z).max()
+        assert abs(z.mean()) < 4.5 / np.sqrt(z.size) + 0.05, z.mean()

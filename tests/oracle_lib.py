@@ -141,8 +141,19 @@ def make_params(solver=None, output=None, *, seed=0x5EED0001, math_mode=0, n_thr
     p.ignore_source = int(bool(s.get("ignoreSource", False)))
     p.seed = int(s.get("seed", seed))
     p.math_mode = math_mode
-    p.n_threads = n_threads or (os.cpu_count() or 1)
+    p.n_threads = n_threads or default_threads()
     return p
+
+
+def default_threads():
+    """Threads for the oracle: the CPUs this process may run on, capped by the
+    job's CPU share when the environment states one (OMP_NUM_THREADS; 16 on a
+    one-GPU box, whose os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
 
 
 def solve(scene: OracleScene, params: Params, pts, index_base=0, index_stride=1):

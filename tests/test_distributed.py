@@ -75,3 +75,38 @@ def test_shard_covers_all_points_once():
             seen = np.concatenate([shard(n, r, w)[0] for r in range(w)])
             assert sorted(seen.tolist()) == list(range(n))
             assert all(shard(n, r, w)[0].size <= shard(n, r, w)[1] for r in range(w))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_sharded_projection_hip_engine(tmp_path, gpu, oracle, world):
+    """World-2 gloo with the HIP ENGINE as each rank's solver: the ranks are fresh
+    child processes (tests/dist_engine_worker.py) sharing GPU 0, the gather runs on
+    CPU tensors; the gathered field equals a single-process engine solve and the
+    oracle, bit for bit."""
+    import subprocess
+    import sys
+    import torch
+    from wos_amd import WosScene, solver_params, workloads
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_engine_worker.py")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path)], env=env)
+             for r in range(world)]
+    rcs = [p.wait(timeout=100) for p in procs]
+    assert rcs == [0] * world, rcs
+    cfg = workloads.config_by_name("B")
+    pts = cfg["points"][:4099]
+    prm = solver_params(dict(cfg["solver"], nWalks=64), cfg["output"])
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0, watertight=True)
+    p1, g1, _ = sc.solve(pts, prm)
+    sc.close()
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0)
+    po, go, _, _, _ = oracle.solve(osc, oracle.make_params(dict(cfg["solver"], nWalks=64), cfg["output"]),
+                                   pts[::37], index_base=0, index_stride=37)
+    np.testing.assert_array_equal(p1[::37], po)
+    np.testing.assert_array_equal(g1[::37], go)
+    for r in range(world):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        np.testing.assert_array_equal(d["p"], p1)
+        np.testing.assert_array_equal(d["g"], g1)

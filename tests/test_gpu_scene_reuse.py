@@ -157,3 +157,66 @@ def test_async_solves_report_their_own_stats(gpu):
     with pytest.raises(Exception):
         sc.solve_stats(enq[-1][2]["ticket"] + 1000)
     sc.close()
+
+
+def _stats_equal(st, ref):
+    for k in ("walk_steps", "wasted_steps", "walks_recorded", "points_estimated", "rejection_iters"):
+        assert st[k] == ref[k], k
+
+
+def test_async_stats_slot_eviction(gpu):
+    """17 async solves (> kStatSlots = 16): the first ticket is evicted (WOS_E_INVALID),
+    the newest still reports the stats of a blocking solve of the same points."""
+    cfg, v, ix, pts = _cfg()
+    dev = torch.device("cuda", 0)
+    prm = solver_params(cfg["solver"], cfg["output"])
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    x = torch.from_numpy(np.ascontiguousarray(pts[:300])).to(dev)
+    p_ref, g_ref, st_ref = sc.solve(x, prm)
+    enq = [sc.solve(x, prm, sync=False) for _ in range(17)]
+    with pytest.raises(Exception):
+        sc.solve_stats(enq[0][2]["ticket"])
+    st = sc.solve_stats(enq[-1][2]["ticket"])
+    _stats_equal(st, st_ref)
+    assert torch.equal(enq[-1][0], p_ref) and torch.equal(enq[-1][1], g_ref)
+    sc.close()
+
+
+def test_async_stats_two_streams_alternating(gpu):
+    """async solves alternating between two torch streams (ctx_order + the shared
+    device counters): every slot's counters belong to its own solve."""
+    cfg, v, ix, pts = _cfg()
+    dev = torch.device("cuda", 0)
+    prm = solver_params(cfg["solver"], cfg["output"])
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    sets = [torch.from_numpy(np.ascontiguousarray(pts[k * 200:(k + 1) * 200 + 50 * k])).to(dev) for k in range(6)]
+    want = [sc.solve(x, prm) for x in sets]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    enq = []
+    for k, x in enumerate(sets):
+        enq.append(sc.solve(x, prm, sync=False, stream=streams[k % 2]))
+    for (p, g, st0), (pw, gw, stw) in zip(enq, want):
+        st = sc.solve_stats(st0["ticket"])
+        _stats_equal(st, stw)
+        torch.cuda.synchronize()
+        assert torch.equal(p, pw) and torch.equal(g, gw)
+    sc.close()
+
+
+def test_async_stats_split_pipelines(gpu, monkeypatch):
+    """WOS_SPLIT=2: the chunks run on two pipelines (aux streams, their own boundary
+    events); stats and outputs equal a blocking unsplit solve."""
+    cfg, v, ix, pts = _cfg()
+    dev = torch.device("cuda", 0)
+    prm = solver_params(cfg["solver"], cfg["output"])
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    x = torch.from_numpy(np.ascontiguousarray(pts[:1500])).to(dev)
+    p_ref, g_ref, st_ref = sc.solve(x, prm)
+    monkeypatch.setenv("WOS_SPLIT", "2")
+    enq = [sc.solve(x, prm, sync=False) for _ in range(3)]
+    for p, g, st0 in enq:
+        st = sc.solve_stats(st0["ticket"])
+        _stats_equal(st, st_ref)
+        assert st["walk_launches"] >= 2
+        assert torch.equal(p, p_ref) and torch.equal(g, g_ref)
+    sc.close()

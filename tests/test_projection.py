@@ -76,7 +76,44 @@ def test_device_projection_matches_host_pattern(gpu):
     g2 = np.asarray(g2, np.float32)
     assert np.array_equal(p.cpu().numpy().view(np.uint32), p2.view(np.uint32))
     assert np.array_equal(g.cpu().numpy().view(np.uint32), g2.view(np.uint32))
+    # oracle leg: the CPU restatement on the same divergence grid and samples, bit for bit
+    import objparse
+    import oracle_lib
+    v, ix = objparse.load(cfg["obj"], 2)
+    osc = oracle_lib.OracleScene(v, ix, div.cpu().numpy(), 350.0)
+    po, go, _, _, _ = oracle_lib.solve(osc, oracle_lib.make_params(cfg["solver"], cfg["output"]),
+                                       samples.cpu().numpy())
+    assert np.array_equal(p.cpu().numpy().view(np.uint32), po.view(np.uint32))
+    assert np.array_equal(g.cpu().numpy().view(np.uint32), go.view(np.uint32))
     u_prev = pj.Siren(2, 2, 2, 128).to(dev)
     loss = proj.projection_loss(u, u_prev, g, 1024)
     loss.backward()
     assert torch.isfinite(loss) and all(torch.isfinite(q.grad).all() for q in u.parameters())
+
+
+def test_projection_loss_index_range_matches_reference():
+    """2D draws randint(0, N-1) (model_split.py:274: the last sample never drawn),
+    3D randint(0, N) (3D model_split.py:297)."""
+
+    class _P(pj.PressureProjector):
+        def __init__(self, dim, n):  # no engine needed for the index draw
+            self.dim, self.device = dim, torch.device("cpu")
+            self.samples = torch.zeros(n, dim)
+
+    ident = lambda x: x[:, :1] * 0  # noqa: E731
+    for dim, n, top in ((2, 5, 3), (3, 5, 4)):
+        proj = _P(dim, n)
+        seen = set()
+        gen = torch.Generator().manual_seed(0)
+        orig = torch.randint
+        try:
+            def spy(lo, hi, size, **kw):
+                r = orig(lo, hi, size, **kw)
+                seen.update(r.tolist())
+                return r
+            torch.randint = spy
+            for _ in range(50):
+                proj.projection_loss(ident, ident, torch.zeros(n, dim), 64, generator=gen)
+        finally:
+            torch.randint = orig
+        assert max(seen) == top and min(seen) == 0

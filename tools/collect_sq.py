@@ -9,7 +9,7 @@ is the vector-instruction issue rate.  valu_issue_frac = SQ_INSTS_VALU x 4 cycle
 2.4 GHz x 256 CUs x 4 SIMDs), the kernel time from the same pass's dispatch
 timestamps; the SQ_WAIT_* split says how much of a wave's life is spent parked on
 memory / LDS waits (s_waitcnt) versus stalled at issue.
-    python3 tools/collect_sq.py [tag]
+    python3 tools/collect_sq.py [tag] [config]
 """
 import csv
 import glob
@@ -18,8 +18,12 @@ import os
 import subprocess
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import lib_sha16  # noqa: E402
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
+CONFIG = sys.argv[2] if len(sys.argv) > 2 else "B"
 OUT = os.path.join(REPO, "gpurun_out", f"{TAG}_sq")
 COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
             "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
@@ -29,7 +33,7 @@ CLOCK_HZ, SIMDS = 2.4e9, 256 * 4
 def main():
     os.makedirs(OUT, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", *COUNTERS, "-d", OUT, "-o", "sq", "--output-format", "csv", "--",
-           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline",
            "--no-projection-wall"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
                    stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=300)
@@ -47,7 +51,7 @@ def main():
     n = len(per)
     mean = {c: sum(p.get(c, 0.0) for p in per.values()) / n for c in COUNTERS}
     t = sum(dur.values()) / n
-    res = {"kernel": "wos_walk_kernel", "dispatches": n, "kernel_s": t, "counters": mean,
+    res = {"kernel": "wos_walk_kernel", "config": CONFIG, "lib_sha16": lib_sha16(), "dispatches": n, "kernel_s": t, "counters": mean,
            "valu_issue_frac": mean["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS),
            "wait_any_frac": mean["SQ_WAIT_ANY"] / mean["SQ_WAVE_CYCLES"],
            "wait_inst_frac": mean["SQ_WAIT_INST_ANY"] / mean["SQ_WAVE_CYCLES"],

@@ -10,7 +10,7 @@ _WRREQ based).  MI355X_MICROARCH.md: FETCH_SIZE counts exactly half the bytes of
 wide (16 B/lane) coalesced streaming read; this kernel's reads are 4-byte gathers
 (walk-task fields and source texels), an uncalibrated width, so the raw value is
 reported together with the 2x-corrected upper estimate.
-    python3 tools/collect_traffic.py [tag]
+    python3 tools/collect_traffic.py [tag] [config]
 This script itself never touches the GPU: rocprofv3 runs as a child process.
 """
 import csv
@@ -20,8 +20,12 @@ import os
 import subprocess
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import lib_sha16  # noqa: E402
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
+CONFIG = sys.argv[2] if len(sys.argv) > 2 else "B"
 OUT = os.path.join(REPO, "gpurun_out", "traffic")
 POINTS, WALKS = 65536, 128
 
@@ -30,7 +34,7 @@ def run_pass(counter):
     d = os.path.join(OUT, counter.lower())
     os.makedirs(d, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", counter.lower(), "--output-format", "csv", "--",
-           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-projection-wall"]
+           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline", "--no-projection-wall"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
                    stdout=open(os.path.join(d, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=600)
     vals = []
@@ -50,7 +54,7 @@ def main():
     write_kib, nw = run_pass("WRITE_SIZE")
     raw = (fetch_kib + write_kib) * 1024.0
     res = {
-        "points": POINTS, "walks": WALKS, "kernel": "wos_walk_kernel",
+        "points": POINTS, "walks": WALKS, "config": CONFIG, "lib_sha16": lib_sha16(), "kernel": "wos_walk_kernel",
         "fetch_bytes": fetch_kib * 1024.0, "write_bytes": write_kib * 1024.0, "dispatches": [nf, nw],
         "bytes_per_launch": raw,
         "bytes_per_launch_fetch_x2": 2.0 * fetch_kib * 1024.0 + write_kib * 1024.0,

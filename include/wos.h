@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 4
+#define WOS_ABI_VERSION 5
 
 enum {
     WOS_OK = 0,
@@ -161,6 +161,38 @@ int wos_solve(wos_scene *scene, const wos_solver_params *params,
               const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
               float *p, float *grad, int32_t *n_est, int32_t *steps,
               wos_stats *stats, void *stream, uint32_t flags);
+
+/* Boundary value caching: the reference's `bvc(scene, solver, output)`
+ * (bindings/zombie/demo/demo.cpp:265-363, exported at :396), replaced here.
+ * Solver keys as for wos_solve plus the BVC keys demo.cpp:269-290 reads. */
+typedef struct wos_bvc_params {
+    int32_t n_walks_solution;       /* nWalksForCachedSolutionEstimates (128) */
+    int32_t n_walks_gradient;       /* nWalksForCachedGradientEstimates (640): Dirichlet samples only */
+    int32_t boundary_cache_size;    /* boundaryCacheSize (1024) */
+    int32_t domain_cache_size;      /* domainCacheSize (1024) */
+    int32_t grid_res;               /* output.gridRes (required) */
+    int32_t use_finite_differences; /* useFiniteDifferencesForBoundaryDerivatives (Dirichlet samples only) */
+    float normal_offset;            /* normalOffsetForCachedDirichletSamples (5 epsilonShell) */
+    float radius_clamp;             /* radiusClampForKernels (1e-3) */
+    float kernel_regularization;    /* regularizationForKernels (0) */
+} wos_bvc_params;
+
+void wos_default_bvc_params(wos_bvc_params *p);
+
+/* runBoundaryValueCaching (demo.cpp:265-363) on a 2D all-Neumann scene (the only kind
+ * the reference's Scene builds: scene.h:39,68), blocking, host buffers:
+ *   solution[g*g], grad[g*g*2]  the evaluation grid (point (i, j) at index i*g + j,
+ *                               x = i/g * extent + bbox min, grid.h:352-368), masked as
+ *                               saveEvaluationGrid does (grid.h:393-409);
+ *   samples[k*8] (optional)     the cached samples [x y nx ny pdf value dn/dn kind], kind 0
+ *                               boundary, 1 normal-aligned boundary, 2 domain (value = the
+ *                               estimated solution or the source), if samples_capacity
+ *                               holds them (else WOS_E_CAPACITY);
+ *   counts[4] (optional)        boundary, normal-aligned, domain samples, total.
+ * Scenes with Dirichlet primitives or in 3D return WOS_E_INVALID (no reference analogue). */
+int wos_bvc(wos_scene *scene, const wos_solver_params *params, const wos_bvc_params *bvc,
+            float *solution, float *grad, float *samples, int64_t samples_capacity, int64_t *counts,
+            wos_stats *stats);
 
 /* Statistics of an earlier solve on the scene's device, by stats->ticket: waits for
  * that solve to finish, then fills *stats.  A time-stepper can enqueue the projection

@@ -1,0 +1,362 @@
+// wos_bvc.hip -- boundary value caching on the GPU (the reference's `bvc`,
+// bindings/zombie/demo/demo.cpp:265-363, over boundary_value_caching/*.h).
+//
+//   wos_bvc_point_info_kernel  one lane per point: distances to the boundaries, the
+//                              inside test and the source texel (grid.h:352-368,
+//                              domain_sampler.h:50-58);
+//   wos_bvc_start_kernel       one lane per boundary sample: the first sphere radius
+//                              (walk_on_stars.h:400-419, the star radius from the
+//                              sample itself, wave-cooperative) and its walk tasks;
+//   wos_walk_kernel<2,GG,true> the walks of estimateSolution (walk_on_stars.h:422-463)
+//                              on the solve's persistent walk kernel;
+//   wos_bvc_fold_kernel        the Welford mean of each sample's recorded walks;
+//   wos_bvc_splat_kernel       Splatter::splat (splatter.h:43-247): every evaluation
+//                              point (one lane) folds the cached samples in order,
+//                              staged through LDS in tiles (every lane reads the same
+//                              record: a broadcast), with the free-space Green's
+//                              functions (distributions.h:8-272) in the reference's
+//                              float/double arithmetic.
+#include "wos_bvc.h"
+#include "wos_device.h"
+#include "wos_launch.h"
+
+namespace wos {
+
+// closest point by one lane: the sequential `<=` scan keeps the highest index
+// attaining the minimum d^2 -- the primitive closest_wave picks
+template <int DIM>
+__device__ Closest closest_lane(const float* prims, int np, const float* x) {
+  constexpr int PS = Layout<DIM>::prim;
+  float bk = kFltMax;
+  int bi = -1;
+  for (int p = 0; p < np; p++) {
+    float pt[DIM], t0, t1;
+    const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+    const float d2 = d * d;
+    if (d2 <= bk) { bk = d2; bi = p; }
+  }
+  Closest c;
+  c.prim = bi;
+  c.d = kFltMax;
+  c.t0 = c.t1 = 0.0f;
+  c.p[0] = c.p[1] = c.p[2] = 0.0f;
+  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
+  return c;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void wos_bvc_point_info_kernel(const DevScene sc, const float* __restrict__ pts,
+                                                                 int64_t n, float* __restrict__ dd,
+                                                                 float* __restrict__ nd, int32_t* __restrict__ inside,
+                                                                 float* __restrict__ src) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float x[DIM];
+  for (int k = 0; k < DIM; k++) x[k] = pts[i * DIM + k];
+  float nDist = kFltMax, nSigned = kFltMax;
+  if (sc.n_prims > 0) {
+    const Closest c = closest_lane<DIM>(sc.prim, sc.n_prims, x);
+    nDist = c.d;
+    nSigned = signed_dist<DIM>(sc.paux, c, x);
+  }
+  float dDist, dSigned;
+  if (sc.n_dprims > 0) {
+    const Closest c = closest_lane<DIM>(sc.dprim, sc.n_dprims, x);
+    dDist = c.d;
+    dSigned = signed_dist<DIM>(sc.dpaux, c, x);
+  } else {
+    dDist = dSigned = bbox_far_dist<DIM>(sc, x);
+  }
+  // insideDomain (fcpw_scene_loader.h:642-648)
+  const bool in = !sc.watertight ? true
+                  : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
+  if (dd) dd[i] = dDist;
+  if (nd) nd[i] = nDist;
+  if (inside) inside[i] = in ? 1 : 0;
+  if (src) src[i] = source_value<DIM>(sc, x);
+}
+
+// The first sphere radius of estimateSolution (walk_on_stars.h:390-419) for every
+// boundary sample, then its walk tasks: WalkState(pt, n, prevDirection = n, FLT_MAX,
+// 1, onNeumann) for each of the wpp walks.  Double-sided normal-aligned samples walk
+// with the flipped normal and query the star radius with flipNormalOrientation.
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void wos_bvc_start_kernel(const DevScene sc, const DevParams prm,
+                                                               const float* __restrict__ bpt,
+                                                               const float* __restrict__ bnrm,
+                                                               const uint8_t* __restrict__ aligned,
+                                                               const float* __restrict__ bdd, int64_t nb,
+                                                               const DevTasks tk) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(reinterpret_cast<char*>(smem) +
+                                                        wave_u * walk_scratch_bytes<DIM>());
+  const LGeom G = geometry_view<DIM, true>(sc, smem, true, false);  // records read through L2
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = i < nb;
+  float x[DIM], n[DIM], dd = 0.0f;
+  bool flip = false;
+  for (int k = 0; k < DIM; k++) { x[k] = 0.0f; n[k] = 0.0f; }
+  if (valid) {
+    for (int k = 0; k < DIM; k++) { x[k] = bpt[i * DIM + k]; n[k] = bnrm[i * DIM + k]; }
+    dd = bdd[i];
+    flip = sc.double_sided && aligned[i] != 0;
+    if (flip) for (int k = 0; k < DIM; k++) n[k] *= -1.0f;
+  }
+  const bool query = valid && dd > prm.epsilon_shell && prm.steps_before_maximal_spheres != 0;
+  const float starQ = star_radius_wave<DIM>(G, sc, prm, query, x, dd, flip, starL, lane);
+  if (!valid) return;
+  float r0 = dd;
+  if (query) r0 = prm.min_star_radius <= dd ? smax(0.99f * starQ, prm.min_star_radius) : starQ;
+  const int64_t T = tk.T;
+  for (int w = 0; w < tk.wpp; w++) {
+    const int64_t t = i * tk.wpp + w;
+    for (int k = 0; k < DIM; k++) {
+      tk.pt[k * T + t] = x[k];
+      tk.n0[k * T + t] = n[k];
+    }
+    tk.thr[t] = 1.0f;
+    tk.tsrc[t] = 0.0f;
+    tk.dd[t] = dd;
+    tk.r0[t] = r0;
+    tk.sflags[t] = 1u;  // SampleType::OnNeumannBoundary
+  }
+  tk.pstate[i] = kPtEstimate;
+  tk.perm[i] = (uint32_t)i;
+}
+
+// SampleStatistics::addSolutionEstimate over each sample's recorded walks, in walk
+// order (walk_on_stars.h:450-462, 767-770)
+__global__ __launch_bounds__(256) void wos_bvc_fold_kernel(const DevTasks tk, int64_t nb, float* __restrict__ sol,
+                                                           int32_t* __restrict__ nest) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  float mean = 0.0f;
+  int N = 0;
+  for (int w = 0; w < tk.wpp; w++) {
+    const int64_t t = i * tk.wpp + w;
+    if (!(tk.code[t] & 1u)) continue;
+    N += 1;
+    const float delta = tk.total[t] - mean;
+    mean += delta / (float)N;
+  }
+  sol[i] = mean;
+  if (nest) nest[i] = N;
+}
+
+// ---- free-space Green's functions, 2D (distributions.h:85-119, 168-219) -------
+struct FreeSpace2 {
+  bool yukawa;
+  float lambda, sqrtLambda;
+
+  // K0, K1 at mu r (bessel::bessk0 / bessk1 in double, rounded to float) and
+  // bessk(2, mu r) = K0 + (1 * 2 / (mu r)) K1 from the double values (bessel.hpp:584-608)
+  __device__ __forceinline__ void bessel_k(float mur, float* K0, float* K1, float* K2) const {
+    double i0, k0, i1, k1;
+    bessel_ik<true, true>((double)mur, &i0, &k0, &i1, &k1);
+    *K0 = (float)k0;
+    *K1 = (float)k1;
+    if (K2) {
+      const double tox = 2.0 / (double)mur;
+      *K2 = (float)(k0 + (1.0 * tox) * k1);
+    }
+  }
+  __device__ __forceinline__ float evaluate(float r, float K0) const {
+    if (!yukawa) return (float)((double)(-flog(r)) / kTwoPi);
+    return (float)((double)K0 / kTwoPi);
+  }
+  __device__ __forceinline__ void gradient(float r, const float* xy, float K1, float* out) const {
+    if (!yukawa) {
+      const float s = (float)(kTwoPi * (double)(r * r));
+      for (int k = 0; k < 2; k++) out[k] = (-xy[k]) / s;
+      return;
+    }
+    const float Qr = sqrtLambda * K1;
+    const float s = (float)(kTwoPi * (double)r);
+    for (int k = 0; k < 2; k++) out[k] = ((-xy[k]) * Qr) / s;
+  }
+  __device__ __forceinline__ float poisson(float r, const float* xy, const float* n, float K1) const {
+    const float nd = n[0] * xy[0] + n[1] * xy[1];
+    if (!yukawa) return (float)((double)nd / (kTwoPi * (double)(r * r)));
+    const float Qr = sqrtLambda * K1;
+    return (float)((double)(nd * Qr) / (kTwoPi * (double)r));
+  }
+  __device__ __forceinline__ void poisson_gradient(float r, const float* xy, const float* n, float K0, float K1,
+                                                   float K2, float* out) const {
+    const float r2 = r * r;
+    const float nd = n[0] * xy[0] + n[1] * xy[1];
+    if (!yukawa) {
+      const float c = 2.0f * (nd / r2);
+      const float s = (float)(kTwoPi * (double)r2);
+      for (int k = 0; k < 2; k++) out[k] = (n[k] - c * xy[k]) / s;
+      return;
+    }
+    const float Qr1 = sqrtLambda * K1;
+    const float Qr2 = lambda * (K0 + K2) / 2.0f;
+    const float c = (nd / r2) * (Qr1 + r * Qr2);
+    const float s = (float)(kTwoPi * (double)r);
+    for (int k = 0; k < 2; k++) out[k] = (n[k] * Qr1 - c * xy[k]) / s;
+  }
+};
+
+__device__ __forceinline__ bool finite_f(float v) { return __builtin_isfinite(v); }
+
+struct SplatStat {
+  float mean, g[2];
+  int n;
+  __device__ __forceinline__ void add(float est, const float* ge) {
+    n += 1;
+    const float fN = (float)n;
+    mean += (est - mean) / fN;
+    for (int k = 0; k < 2; k++) g[k] += (ge[k] - g[k]) / fN;
+  }
+};
+
+constexpr int kSplatTile = 256;
+
+// Splatter::splat over every evaluation point (one lane each) and every cached sample
+// (boundary, normal-aligned, domain in cache order), then EvaluationPoint::
+// getEstimatedSolution / getEstimatedGradient (splatter.h:315-334) and the output mask
+// of saveEvaluationGrid (grid.h:393-409).
+__global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restrict__ recs, int nrec,
+                                                            const float* __restrict__ ept,
+                                                            const float* __restrict__ edd,
+                                                            const float* __restrict__ end_,
+                                                            const int32_t* __restrict__ ein, int64_t ne,
+                                                            float absorption, float radius_clamp, float reg,
+                                                            float cutoff, float mask, int double_sided,
+                                                            float* __restrict__ sol_out, float* __restrict__ grad_out) {
+  __shared__ float tile[kSplatTile * kBvcRec];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < ne;
+  FreeSpace2 gf;
+  gf.yukawa = absorption > 0.0f;
+  gf.lambda = absorption;
+  gf.sqrtLambda = __builtin_sqrtf(absorption);
+  float x[2] = {0.0f, 0.0f}, dDist = 0.0f;
+  if (valid) { x[0] = ept[2 * i]; x[1] = ept[2 * i + 1]; dDist = edd[i]; }
+  // evaluation points closer than the cutoff to the Dirichlet boundary are not splatted
+  // (splatter.h:94); the scenes bvc accepts have no Dirichlet boundary
+  const bool splat = valid && !(dDist < cutoff);
+  SplatStat st[3];
+  for (int q = 0; q < 3; q++) { st[q].mean = 0.0f; st[q].g[0] = st[q].g[1] = 0.0f; st[q].n = 0; }
+  for (int t0 = 0; t0 < nrec; t0 += kSplatTile) {
+    const int cnt = nrec - t0 < kSplatTile ? nrec - t0 : kSplatTile;
+    for (int e = threadIdx.x; e < cnt * kBvcRec; e += blockDim.x) tile[e] = recs[(size_t)t0 * kBvcRec + e];
+    __syncthreads();
+    if (splat) {
+      for (int j = 0; j < cnt; j++) {
+        const float* R = tile + j * kBvcRec;
+        const int kind = (int)R[7];
+        const float pdf = R[4], value = R[5];
+        const float yx[2] = {R[0] - x[0], R[1] - x[1]};
+        const float xy[2] = {x[0] - R[0], x[1] - R[1]};
+        float r = smax(radius_clamp, __builtin_sqrtf(yx[0] * yx[0] + yx[1] * yx[1]));
+        float K0 = 0.0f, K1 = 0.0f, K2 = 0.0f;
+        if (gf.yukawa) gf.bessel_k(r * gf.sqrtLambda, &K0, &K1, kind == kBvcDomain ? nullptr : &K2);
+        float G = gf.evaluate(r, K0);
+        float dG[2];
+        gf.gradient(r, xy, K1, dG);
+        const float dGNorm = __builtin_sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
+        float est, ge[2];
+        if (kind != kBvcDomain) {  // splatBoundaryData (splatter.h:214-264)
+          const float nd = R[6];
+          const float s = kind == kBvcAligned ? -1.0f : 1.0f;
+          const float n[2] = {R[2] * s, R[3] * s};
+          float P = gf.poisson(r, xy, n, K1);
+          float dP[2];
+          gf.poisson_gradient(r, xy, n, K0, K1, K2, dP);
+          const float dPNorm = __builtin_sqrtf(dP[0] * dP[0] + dP[1] * dP[1]);
+          if (!(finite_f(G) && finite_f(P) && finite_f(dGNorm) && finite_f(dPNorm))) continue;
+          if (reg > 0.0f) {
+            r /= reg;
+            P *= 1.0f - fexp(-r * r);  // computePoissonKernelRegularization<2> (splatter.h:28-32)
+          }
+          est = (G * nd - P * value) / pdf;
+          for (int k = 0; k < 2; k++) ge[k] = (dG[k] * nd - dP[k] * value) / pdf;
+        } else {  // splatSourceData (splatter.h:267-301)
+          if (!(finite_f(G) && finite_f(dGNorm))) continue;
+          est = (G * value) / pdf;
+          for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
+        }
+        st[kind].add(est, ge);
+      }
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
+  float sol = st[0].mean;
+  sol += st[1].mean;
+  sol += st[2].mean;
+  float g[2];
+  for (int k = 0; k < 2; k++) {
+    g[k] = st[0].g[k];
+    g[k] += st[1].g[k];
+    g[k] += st[2].g[k];
+  }
+  const bool in = ein[i] != 0;
+  const float ad = __builtin_fabsf(dDist), an = __builtin_fabsf(end_[i]);
+  const bool masked = (!in && !double_sided) || smin(ad, an) < mask;
+  sol_out[i] = masked ? 0.0f : sol;
+  for (int k = 0; k < 2; k++) grad_out[2 * i + k] = masked ? 0.0f : g[k];
+}
+
+template __global__ void wos_walk_kernel<2, false, true>(const DevScene, const DevParams, const DevTasks, int64_t,
+                                                           int64_t, unsigned long long*, unsigned int*, int);
+template __global__ void wos_walk_kernel<2, true, true>(const DevScene, const DevParams, const DevTasks, int64_t,
+                                                          int64_t, unsigned long long*, unsigned int*, int);
+
+// ---- host launchers ----------------------------------------------------------
+hipError_t launch_bvc_point_info(const DevScene& sc, const float* pts, int64_t n, float* dd, float* nd,
+                                 int32_t* inside, float* src, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int grid = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(wos_bvc_point_info_kernel<2>, dim3(grid), dim3(256), 0, s, sc, pts, n, dd, nd, inside, src);
+  return hipGetLastError();
+}
+
+size_t bvc_start_lds_bytes() { return (size_t)kWavesPerBlockHost * walk_scratch_bytes<2>(); }
+
+hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const float* bpt, const float* bnrm,
+                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  const int grid = (int)((nb + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(wos_bvc_start_kernel<2>, dim3(grid), dim3(kBlock), bvc_start_lds_bytes(), s, sc, prm, bpt, bnrm,
+                     aligned, bdd, nb, tk);
+  return hipGetLastError();
+}
+
+hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
+                               int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
+                               size_t shmem, int geom_floats, hipStream_t s) {
+  if (sc.geom_global)
+    hipLaunchKernelGGL((wos_walk_kernel<2, true, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride,
+                       counters, tqueue, geom_floats);
+  else
+    hipLaunchKernelGGL((wos_walk_kernel<2, false, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base,
+                       stride, counters, tqueue, geom_floats);
+  return hipGetLastError();
+}
+
+hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks) {
+  return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, true, true>, kBlock, shmem)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, false, true>, kBlock, shmem);
+}
+
+hipError_t launch_bvc_fold(const DevTasks& tk, int64_t nb, float* sol, int32_t* nest, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wos_bvc_fold_kernel, dim3((int)((nb + 255) / 256)), dim3(256), 0, s, tk, nb, sol, nest);
+  return hipGetLastError();
+}
+
+hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const float* edd, const float* end_,
+                            const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
+                            float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s) {
+  if (ne <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wos_bvc_splat_kernel, dim3((int)((ne + 255) / 256)), dim3(256), 0, s, recs, nrec, ept, edd, end_,
+                     ein, ne, absorption, radius_clamp, reg, cutoff, mask, double_sided, sol, grad);
+  return hipGetLastError();
+}
+
+}  // namespace wos

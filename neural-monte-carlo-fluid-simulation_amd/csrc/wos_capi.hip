@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/wos.h"
+#include "wos_bvc.h"
 #include "wos_detmath.h"
 #include "wos_host_scene.h"
 #include "wos_launch.h"
@@ -628,6 +629,96 @@ int fill_stats(const StatSlot& q, wos_stats* stats) {
   return WOS_OK;
 }
 
+// The walk kernel's LDS image for a solve on `s`: staged geometry, the star-radius
+// grid of the solver's precision / minR (if it fits), the Dirichlet primitives.
+struct WalkLayout {
+  wos::DevScene dsc;          // the scene with its star grid (or none)
+  int geom_floats = 0;        // Neumann records + culling boxes (what the first-ball kernel stages)
+  int geom_floats_walk = 0;   // + the star grid + the Dirichlet records (the walk kernel)
+  size_t shmem_walk = 0;      // dynamic LDS of a walk-kernel workgroup
+};
+
+int walk_layout(wos_scene* s, const wos_solver_params* prm, WalkLayout& L) {
+  Geom& geom = *s->geom;
+  const wos::HostScene& host = geom.host;
+  const int dim = host.dim;
+  const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
+  const int SS = dim == 2 ? wos::kSilStride2 : wos::kSilStride3;
+  const int primAl = (host.n_prims * PS + 3) & ~3;
+  const int silAl = (host.n_sil * SS + 3) & ~3;
+  L.geom_floats = primAl + silAl + wos::kGroupStride * host.n_pgroups + wos::kSGroupStride * host.n_sgroups;
+  // the walk kernel also stages the star-radius grid (after the silhouette groups)
+  wos::DevScene& dsc = L.dsc;
+  dsc = s->dev;
+  dsc.sgrid = nullptr;
+  dsc.sgrid_words = dsc.sgrid_off_words = 0;
+  if (star_grid_enabled() && host.n_sil > 0) {
+    const Geom::Grid* gr = nullptr;
+    int rc = star_grid(geom, prm->silhouette_precision, prm->min_star_radius, &gr);
+    if (rc != WOS_OK) return rc;
+    if (gr->ok) {
+      dsc.sgrid = gr->d;
+      dsc.sgrid_words = (int32_t)gr->grid.words.size();
+      dsc.sgrid_off_words = gr->grid.off_words;
+      for (int k = 0; k < 3; k++) {
+        dsc.sgrid_n[k] = gr->grid.n[k];
+        dsc.sgrid_min[k] = gr->grid.gmin[k];
+        dsc.sgrid_inv[k] = gr->grid.inv[k];
+      }
+    }
+  }
+  // ... and the Dirichlet primitives with their culling boxes (after the grid)
+  const int dir_floats = ((host.n_dprims * PS + 3) & ~3) + wos::kGroupStride * host.n_dgroups;
+  L.geom_floats_walk = L.geom_floats + ((dsc.sgrid_words + 3) & ~3) + dir_floats;
+  L.shmem_walk = (size_t)L.geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+  if (dsc.sgrid != nullptr && L.shmem_walk > kLdsDynamicMax) {  // no room: the group scan alone
+    dsc.sgrid = nullptr;
+    dsc.sgrid_words = dsc.sgrid_off_words = 0;
+    L.geom_floats_walk = L.geom_floats + dir_floats;
+    L.shmem_walk =
+        (size_t)L.geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
+  }
+  return WOS_OK;
+}
+
+// device allocations of one call, freed on every exit path
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() { for (void* q : p) hipFree(q); }
+  template <typename T>
+  hipError_t get(T** out, size_t n) {
+    *out = nullptr;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(1, n) * sizeof(T));
+    if (e == hipSuccess) { p.push_back(q); *out = (T*)q; }
+    return e;
+  }
+};
+
+// DevParams of a solve (walk_on_stars.h WalkSettings from the solver keys)
+wos::DevParams dev_params(const wos_solver_params* prm) {
+  wos::DevParams dp{};
+  const bool anti = !prm->disable_gradient_antithetic_variates;
+  dp.n_walks = prm->n_walks;
+  dp.n_anti = anti ? 2 : 1;
+  dp.n_pairs = anti ? std::max(1, prm->n_walks / 2) : prm->n_walks;
+  dp.max_walk_length = prm->max_walk_length;
+  dp.steps_before_tikhonov = prm->steps_before_tikhonov;
+  dp.steps_before_maximal_spheres = prm->steps_before_maximal_spheres;
+  dp.epsilon_shell = prm->epsilon_shell;
+  dp.min_star_radius = prm->min_star_radius;
+  dp.silhouette_precision = prm->silhouette_precision;
+  dp.rr_threshold = prm->russian_roulette_threshold;
+  dp.boundary_distance_mask = prm->boundary_distance_mask;
+  dp.use_cv = !prm->disable_gradient_control_variates;
+  dp.use_cosine = prm->use_cosine_sampling;
+  dp.ignore_dirichlet = prm->ignore_dirichlet;
+  dp.ignore_neumann = prm->ignore_neumann;
+  dp.ignore_source = prm->ignore_source;
+  dp.seed = prm->seed;
+  return dp;
+}
+
 }  // namespace
 
 extern "C" {
@@ -656,25 +747,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     if (rc != WOS_OK) return rc;
   }
 
-  wos::DevParams dp{};
-  const bool anti = !prm->disable_gradient_antithetic_variates;
-  dp.n_walks = prm->n_walks;
-  dp.n_anti = anti ? 2 : 1;
-  dp.n_pairs = anti ? std::max(1, prm->n_walks / 2) : prm->n_walks;
-  dp.max_walk_length = prm->max_walk_length;
-  dp.steps_before_tikhonov = prm->steps_before_tikhonov;
-  dp.steps_before_maximal_spheres = prm->steps_before_maximal_spheres;
-  dp.epsilon_shell = prm->epsilon_shell;
-  dp.min_star_radius = prm->min_star_radius;
-  dp.silhouette_precision = prm->silhouette_precision;
-  dp.rr_threshold = prm->russian_roulette_threshold;
-  dp.boundary_distance_mask = prm->boundary_distance_mask;
-  dp.use_cv = !prm->disable_gradient_control_variates;
-  dp.use_cosine = prm->use_cosine_sampling;
-  dp.ignore_dirichlet = prm->ignore_dirichlet;
-  dp.ignore_neumann = prm->ignore_neumann;
-  dp.ignore_source = prm->ignore_source;
-  dp.seed = prm->seed;
+  wos::DevParams dp = dev_params(prm);
   {
     // diagonal draws + shuffle draws of the stratified samples
     const int k_needed = 2 * (2 * dp.n_pairs) * (dim - 1);
@@ -688,45 +761,18 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
 
   // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
   // in the first-ball kernel)
-  const int PS = dim == 2 ? wos::kPrimStride2 : wos::kPrimStride3;
-  const int SS = dim == 2 ? wos::kSilStride2 : wos::kSilStride3;
-  const int primAl = (host.n_prims * PS + 3) & ~3;
-  const int silAl = (host.n_sil * SS + 3) & ~3;
-  const int geom_floats =
-      primAl + silAl + wos::kGroupStride * host.n_pgroups + wos::kSGroupStride * host.n_sgroups;
-  // the walk kernel also stages the star-radius grid (after the silhouette groups)
-  wos::DevScene dsc = s->dev;
-  dsc.sgrid = nullptr;
-  dsc.sgrid_words = dsc.sgrid_off_words = 0;
-  if (star_grid_enabled() && host.n_sil > 0) {
-    const Geom::Grid* gr = nullptr;
-    int rc = star_grid(geom, prm->silhouette_precision, prm->min_star_radius, &gr);
+  WalkLayout wl;
+  {
+    int rc = walk_layout(s, prm, wl);
     if (rc != WOS_OK) return rc;
-    if (gr->ok) {
-      dsc.sgrid = gr->d;
-      dsc.sgrid_words = (int32_t)gr->grid.words.size();
-      dsc.sgrid_off_words = gr->grid.off_words;
-      for (int k = 0; k < 3; k++) {
-        dsc.sgrid_n[k] = gr->grid.n[k];
-        dsc.sgrid_min[k] = gr->grid.gmin[k];
-        dsc.sgrid_inv[k] = gr->grid.inv[k];
-      }
-    }
   }
-  // ... and the Dirichlet primitives with their culling boxes (after the grid)
-  const int dir_floats = ((host.n_dprims * PS + 3) & ~3) + wos::kGroupStride * host.n_dgroups;
-  int geom_floats_walk = geom_floats + ((dsc.sgrid_words + 3) & ~3) + dir_floats;
+  wos::DevScene dsc = wl.dsc;
+  const int geom_floats = wl.geom_floats;
+  int geom_floats_walk = wl.geom_floats_walk;
+  size_t shmem_walk = wl.shmem_walk;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   const size_t shmem_fb =
       (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
-  size_t shmem_walk =
-      (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
-  if (dsc.sgrid != nullptr && shmem_walk > kLdsDynamicMax) {  // no room: the group scan alone
-    dsc.sgrid = nullptr;
-    dsc.sgrid_words = dsc.sgrid_off_words = 0;
-    geom_floats_walk = geom_floats + dir_floats;
-    shmem_walk = (size_t)geom_floats_walk * sizeof(float) + wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
-  }
   // scenes beyond the LDS budget (or WOS_GEOM_GLOBAL=1): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
@@ -894,6 +940,213 @@ int wos_solve_stats(wos_scene* s, uint64_t ticket, wos_stats* stats) {
   if (q.ticket != ticket) return unknown();
   HIP_TRY(hipEventSynchronize(q.done));
   return fill_stats(q, stats);
+}
+
+void wos_default_bvc_params(wos_bvc_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  // defaults of runBoundaryValueCaching (demo.cpp:274-290)
+  p->n_walks_solution = 128;
+  p->n_walks_gradient = 640;
+  p->boundary_cache_size = 1024;
+  p->domain_cache_size = 1024;
+  p->grid_res = 0;
+  p->normal_offset = 5.0f * 1e-3f;
+  p->radius_clamp = 1e-3f;
+  p->kernel_regularization = 0.0f;
+}
+
+int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp, float* solution, float* grad,
+            float* samples, int64_t samples_capacity, int64_t* counts, wos_stats* stats) {
+  if (!s || !prm || !bp || !solution || !grad) return fail(WOS_E_INVALID, "wos_bvc: null argument");
+  if (bp->grid_res < 1) return fail(WOS_E_INVALID, "wos_bvc: gridRes must be >= 1");
+  if (bp->n_walks_solution < 1) return fail(WOS_E_INVALID, "wos_bvc: nWalksForCachedSolutionEstimates must be >= 1");
+  if (bp->boundary_cache_size < 0 || bp->domain_cache_size < 0) return fail(WOS_E_INVALID, "wos_bvc: negative cache size");
+  if (prm->max_walk_length < 0) return fail(WOS_E_INVALID, "wos_bvc: maxWalkLength must be >= 0");
+  std::lock_guard<std::mutex> lock(s->mu);
+  Geom& geom = *s->geom;
+  const wos::HostScene& host = geom.host;
+  if (host.dim != 2) return fail(WOS_E_INVALID, "wos_bvc: boundary value caching is 2D (the reference exports it from the 2D module only)");
+  if (host.n_dprims > 0)
+    return fail(WOS_E_INVALID, "wos_bvc: Dirichlet boundaries are not supported (the reference's scenes are all-Neumann, scene.h:39,68)");
+  if (host.n_prims <= 0) return fail(WOS_E_INVALID, "wos_bvc: scene has no boundary");
+  // no Dirichlet boundary: every evaluation point's Dirichlet distance is the bounding
+  // box's far-corner distance (>= half the diagonal), above the splat cutoff unless the
+  // box is degenerate -- pointwise estimation near the Dirichlet boundary never runs
+  {
+    const float hx = 0.5f * host.ext[0], hy = 0.5f * host.ext[1];
+    if (!(std::sqrt(hx * hx + hy * hy) >= bp->normal_offset))
+      return fail(WOS_E_INVALID, "wos_bvc: scene bounding box smaller than normalOffsetForCachedDirichletSamples");
+  }
+  HIP_TRY(hipSetDevice(s->device));
+  DevCtx& c = g_ctx[s->device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  {
+    int rc = ctx_ready(c, s->device);
+    if (rc != WOS_OK) return rc;
+  }
+  hipStream_t st = nullptr;
+  HIP_TRY(ctx_order(c, st));
+  HIP_TRY(hipStreamSynchronize(st));
+
+  // ---- host: boundary samples, domain candidates, evaluation grid
+  wos::BvcSampling smp;
+  std::string err;
+  const float pmin[2] = {host.pmin[0], host.pmin[1]}, pmax[2] = {host.pmax[0], host.pmax[1]};
+  if (!wos::bvc_generate_samples(geom.v.data(), (int)(geom.v.size() / 2), geom.ix.data(), (int)(geom.ix.size() / 2),
+                                 pmin, pmax, geom.double_sided != 0, bp->boundary_cache_size, bp->domain_cache_size,
+                                 bp->normal_offset, prm->ignore_source != 0, prm->seed, smp, err))
+    return fail(WOS_E_INVALID, "wos_bvc: " + err);
+  std::vector<float> ept;
+  wos::bvc_evaluation_grid(bp->grid_res, pmin, pmax, ept);
+  const int64_t nb = (int64_t)smp.aligned.size();
+  const int64_t nd = (int64_t)(smp.dcand.size() / 2);
+  const int64_t ne = (int64_t)bp->grid_res * bp->grid_res;
+
+  // ---- device buffers (freed on every exit)
+  DevBufs B;
+  float *d_bpt, *d_bnrm, *d_bdd, *d_bsol, *d_dc, *d_dsrc, *d_ept, *d_edd, *d_end, *d_sol, *d_grad;
+  int32_t *d_bnest, *d_din, *d_ein;
+  uint8_t* d_al;
+  HIP_TRY(B.get(&d_bpt, 2 * nb)); HIP_TRY(B.get(&d_bnrm, 2 * nb)); HIP_TRY(B.get(&d_bdd, nb));
+  HIP_TRY(B.get(&d_bsol, nb)); HIP_TRY(B.get(&d_bnest, nb)); HIP_TRY(B.get(&d_al, nb));
+  HIP_TRY(B.get(&d_dc, 2 * nd)); HIP_TRY(B.get(&d_din, nd)); HIP_TRY(B.get(&d_dsrc, nd));
+  HIP_TRY(B.get(&d_ept, 2 * ne)); HIP_TRY(B.get(&d_edd, ne)); HIP_TRY(B.get(&d_end, ne)); HIP_TRY(B.get(&d_ein, ne));
+  HIP_TRY(B.get(&d_sol, ne)); HIP_TRY(B.get(&d_grad, 2 * ne));
+  if (nb > 0) {
+    HIP_TRY(hipMemcpy(d_bpt, smp.bpt.data(), 2 * nb * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_bnrm, smp.bnrm.data(), 2 * nb * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_al, smp.aligned.data(), nb, hipMemcpyHostToDevice));
+  }
+  if (nd > 0) HIP_TRY(hipMemcpy(d_dc, smp.dcand.data(), 2 * nd * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d_ept, ept.data(), 2 * ne * sizeof(float), hipMemcpyHostToDevice));
+
+  const uint64_t ticket = c.next_ticket++;
+  StatSlot& q = c.slot[ticket % kStatSlots];
+  while (q.bev.size() < 4) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreate(&e));
+    q.bev.push_back(e);
+  }
+  q.ticket = ticket;
+  q.n_batches = 1;
+  HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
+  HIP_TRY(hipEventRecord(q.ev0, st));
+  HIP_TRY(hipEventRecord(q.bev[0], st));
+  const wos::DevScene& sc0 = s->dev;
+  HIP_TRY(wos::launch_bvc_point_info(sc0, d_bpt, nb, d_bdd, nullptr, nullptr, nullptr, st));
+  HIP_TRY(wos::launch_bvc_point_info(sc0, d_dc, nd, nullptr, nullptr, d_din, d_dsrc, st));
+  HIP_TRY(wos::launch_bvc_point_info(sc0, d_ept, ne, d_edd, d_end, d_ein, nullptr, st));
+
+  // ---- estimates at the boundary samples: estimateSolution walks (walk_on_stars.h:353-464)
+  wos_solver_params wp = *prm;
+  wp.n_walks = bp->n_walks_solution;
+  wp.disable_gradient_antithetic_variates = 1;  // one walk per task, no pairs
+  wos::DevParams dp = dev_params(&wp);
+  {
+    int rc = ensure_jump(c, 4096);
+    if (rc != WOS_OK) return rc;
+    dp.jump = c.d_jump;
+    dp.n_jump = c.n_jump;
+    dp.rej_tab = c.d_rejtab;
+  }
+  WalkLayout wl;
+  {
+    int rc = walk_layout(s, &wp, wl);
+    if (rc != WOS_OK) return rc;
+  }
+  wos::DevScene dsc = wl.dsc;
+  const char* gg = std::getenv("WOS_GEOM_GLOBAL");
+  if ((gg && gg[0] == '1') || wl.shmem_walk > kLdsDynamicMax) {
+    dsc.geom_global = 1;
+    wl.geom_floats_walk = 0;
+    wl.shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(2);
+  }
+  const int64_t wpp = wp.n_walks;
+  if (nb * wpp > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: boundaryCacheSize x nWalks exceeds one task batch");
+  if (nb > 0) {
+    int rc = ensure_tasks(c, 2, nb * wpp, nb);
+    if (rc != WOS_OK) return rc;
+    wos::DevTasks tk = task_view(c, 2, nb * wpp, (int32_t)wpp, 0, nb * wpp, nb);
+    tk.n0 = tk.bdir;
+    tk.r0 = tk.first;
+    tk.sflags = reinterpret_cast<uint32_t*>(tk.sdir);
+    HIP_TRY(wos::launch_bvc_start(dsc, dp, d_bpt, d_bnrm, d_al, d_bdd, nb, tk, st));
+    HIP_TRY(hipEventRecord(q.bev[1], st));
+    int bpc = 0;
+    HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc));
+    const int grid = (int)std::min<int64_t>((int64_t)std::max(1, bpc) * std::max(1, c.num_cus), (tk.T + 63) / 64);
+    unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kNumCounters + 1);
+    HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, 0, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,
+                                     wl.geom_floats_walk, st));
+    HIP_TRY(hipEventRecord(q.bev[2], st));
+    HIP_TRY(wos::launch_bvc_fold(tk, nb, d_bsol, d_bnest, st));
+    q.bpc_walk = bpc;
+  } else {
+    HIP_TRY(hipEventRecord(q.bev[1], st));
+    HIP_TRY(hipEventRecord(q.bev[2], st));
+  }
+  q.walk_lds = (int32_t)wl.shmem_walk;
+  q.star_grid = dsc.sgrid != nullptr;
+  q.geom_global = dsc.geom_global;
+
+  // ---- the cache: boundary samples (solution, Neumann value 0: pde.neumann, scene.h:176-181)
+  // then the domain samples inside the solve region (source)
+  std::vector<float> bsol(nb), dsrc(nd);
+  std::vector<int32_t> din(nd);
+  if (nb > 0) HIP_TRY(hipMemcpyAsync(bsol.data(), d_bsol, nb * sizeof(float), hipMemcpyDeviceToHost, st));
+  if (nd > 0) {
+    HIP_TRY(hipMemcpyAsync(dsrc.data(), d_dsrc, nd * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(din.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<float> recs;
+  recs.reserve((size_t)(nb + nd) * wos::kBvcRec);
+  for (int64_t i = 0; i < nb; i++) {
+    const bool al = smp.aligned[i] != 0;
+    const float r[wos::kBvcRec] = {smp.bpt[2 * i], smp.bpt[2 * i + 1], smp.bnrm[2 * i], smp.bnrm[2 * i + 1],
+                                   al ? smp.pdf_aligned : smp.pdf_main, bsol[i], 0.0f,
+                                   (float)(al ? wos::kBvcAligned : wos::kBvcBoundary)};
+    recs.insert(recs.end(), r, r + wos::kBvcRec);
+  }
+  int64_t nd_kept = 0;
+  for (int64_t i = 0; i < nd; i++) {
+    const float x = smp.dcand[2 * i], y = smp.dcand[2 * i + 1];
+    // insideSolveRegion (demo.cpp:302-304): the inside test, or the bounding box if double-sided
+    const bool keep = geom.double_sided ? (x >= pmin[0] && y >= pmin[1] && x <= pmax[0] && y <= pmax[1]) : din[i] != 0;
+    if (!keep) continue;
+    const float r[wos::kBvcRec] = {x, y, 0.0f, 0.0f, smp.pdf_domain, dsrc[i], 0.0f, (float)wos::kBvcDomain};
+    recs.insert(recs.end(), r, r + wos::kBvcRec);
+    nd_kept++;
+  }
+  const int64_t nrec = nb + nd_kept;
+  float* d_recs = nullptr;
+  HIP_TRY(B.get(&d_recs, (size_t)nrec * wos::kBvcRec));
+  if (nrec > 0) HIP_TRY(hipMemcpy(d_recs, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(wos::launch_bvc_splat(d_recs, (int)nrec, d_ept, d_edd, d_end, d_ein, ne, s->dev.absorption,
+                                bp->radius_clamp, bp->kernel_regularization, bp->normal_offset,
+                                prm->boundary_distance_mask, geom.double_sided, d_sol, d_grad, st));
+  HIP_TRY(hipEventRecord(q.bev[3], st));
+  HIP_TRY(hipEventRecord(q.ev1, st));
+  HIP_TRY(hipMemcpyAsync(q.h_cnt, c.d_counters, wos::kNumCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(solution, d_sol, ne * sizeof(float), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(grad, d_grad, 2 * ne * sizeof(float), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(q.done, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  c.inflight = false;
+  if (counts) { counts[0] = smp.nb_main; counts[1] = smp.nb_aligned; counts[2] = nd_kept; counts[3] = nrec; }
+  if (stats) {
+    int rc = fill_stats(q, stats);
+    if (rc != WOS_OK) return rc;
+    stats->points_estimated = (uint64_t)nb;
+  }
+  if (samples) {
+    if (samples_capacity < nrec)
+      return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
+                                      std::to_string(nrec) + " samples");
+    if (nrec > 0) std::memcpy(samples, recs.data(), recs.size() * sizeof(float));
+  }
+  return WOS_OK;
 }
 
 int wos_selftest_math(int32_t which, const double* x, double* out, int64_t n, int32_t device) {

@@ -1,2574 +1,12 @@
-// wos_kernel.hip -- gfx950 walk-on-stars solve kernel.
+// wos_kernel.hip -- gfx950 walk-on-stars solve: the kernel instantiations and their
+// host launchers (device code in wos_device.h).
 //
-// One wavefront (64 lanes) owns one query point at a time; lane l runs
-// antithetic pair l of that point (both members, sharing the pair's walk
-// stream, walk_on_stars.h:494-616).  Neumann segments/triangles and the
-// silhouette candidates are staged in LDS once per workgroup and scanned
-// brute-force (every lane reads the same LDS word: broadcast, no conflicts).
-// The per-point statistics (Welford means with sequential control variates,
-// walk_on_stars.h:500-506,744-877) are folded in walk order by lanes 0..DIM
-// in lockstep so the result is bit-identical to the sequential CPU oracle.
-// Points are handed out by a device-scope atomic work counter (one returning
-// atomicAdd per point), so uneven per-point cost (near-wall points run longer
-// walks) does not leave waves idle at the tail.
-//
-// Numerics follow the reference operation by operation: float state, double
-// Bessel evaluations rounded to float members (distributions.h:573-696), double
-// 2*pi divisors, Eigen's float-scalar conversions -- see the oracle restatement
-// (oracle/wos_oracle.c) which is the parity checker for this file.
-
-#include <cstdio>
-
-#include "wos_detmath.h"
-#include "wos_scene.h"
+// One projection = wos_first_ball_kernel (point setup + first balls), the walk-queue
+// order (wos_lpt_*), the persistent wos_walk_kernel and wos_fold_kernel (statistics
+// + masked outputs), all on the caller's stream.
+#include "wos_device.h"
 
 namespace wos {
-
-// 1: the star-grid candidate lists of all lanes are evaluated wave-cooperatively;
-// 0: each lane scans its own cell list sequentially
-#ifndef WOS_CELL_COOP
-#define WOS_CELL_COOP 1
-#endif
-#ifndef WOS_ABL_NO_SIL
-#define WOS_ABL_NO_SIL 0
-#endif
-#ifndef WOS_ABL_NO_RAY
-#define WOS_ABL_NO_RAY 0
-#endif
-#ifndef WOS_ABL_ONE_REJ
-#define WOS_ABL_ONE_REJ 0
-#endif
-#ifndef WOS_NO_FASTREJ
-#define WOS_NO_FASTREJ 0
-#endif
-// timing-only ablations (wrong results): float Bessels in the ball update and the
-// direction-sampled Poisson kernel; a constant source texel
-#ifndef WOS_ABL_FAST_BESSEL
-#define WOS_ABL_FAST_BESSEL 0
-#endif
-#ifndef WOS_ABL_CONST_SRC
-#define WOS_ABL_CONST_SRC 0
-#endif
-#ifndef WOS_ABL_FB
-#define WOS_ABL_FB 0
-#endif
-#ifndef WOS_ABL_NO_STATS
-#define WOS_ABL_NO_STATS 0
-#endif
-
-#ifndef WOS_DIAG
-#define WOS_DIAG 0
-#endif
-#ifndef WOS_RAY_WAVE
-#define WOS_RAY_WAVE 1
-#endif
-
-constexpr int kWave = 64;
-constexpr int kBlock = 256;
-
-enum { WC_DIRICHLET = 0, WC_RR = 1, WC_MAXLEN = 2, WC_ESCAPED = 3 };
-
-// counters[] slots
-enum { C_STEPS = 0, C_WASTED, C_REC, C_ESC, C_MAXL, C_RR, C_DIR, C_PTS, C_ITERS, C_NUM };
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
-// (s_memtime) and lane-packing counters of the walk kernel.
-enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_MID, D_END, D_TAIL, D_NUM };
-// slots holding maxima (folded with atomicMax)
-__host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
-__device__ unsigned long long g_diag[D_NUM];
-#if WOS_DIAG
-__shared__ unsigned long long s_diag[D_NUM];
-#endif
-#if WOS_DIAG
-#define DIAG_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define DIAG_ADD(slot, v)                                                              \
-  do {                                                                                 \
-    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - (v);                           \
-    if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
-      atomicAdd(&s_diag[slot], (unsigned long long)dt_);                               \
-  } while (0)
-#define DIAG_COUNT(slot, n)                                                            \
-  do {                                                                                 \
-    const unsigned long long n_ = (n);                                                 \
-    if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
-      atomicAdd(&s_diag[slot], n_);                                                    \
-  } while (0)
-#define DIAG_LANE(slot) atomicAdd(&s_diag[slot], 1ull)
-#define DIAG_MAX(slot, v) atomicMax(&s_diag[slot], (unsigned long long)(v))
-#else
-#define DIAG_T0(v)
-#define DIAG_ADD(slot, v)
-#define DIAG_COUNT(slot, n)
-#define DIAG_LANE(slot)
-#define DIAG_MAX(slot, v)
-#endif
-
-template <int DIM>
-__device__ __forceinline__ float dotv(const float* a, const float* b) {
-  float s = a[0] * b[0] + a[1] * b[1];
-  if constexpr (DIM == 3) s = s + a[2] * b[2];
-  return s;
-}
-template <int DIM>
-__device__ __forceinline__ float normv(const float* a) { return __builtin_sqrtf(dotv<DIM>(a, a)); }
-
-__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
-  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
-  r[0] = x; r[1] = y; r[2] = z;
-}
-
-// Eigen normalized(): v / sqrt(|v|^2) when |v|^2 > 0
-template <int DIM>
-__device__ __forceinline__ void normalize_div(float* v) {
-  float z = dotv<DIM>(v, v);
-  if (z > 0.0f) { float s = __builtin_sqrtf(z); for (int k = 0; k < DIM; k++) v[k] = v[k] / s; }
-}
-// enoki::normalize restated: v * (1/sqrt(|v|^2))
-template <int DIM>
-__device__ __forceinline__ void normalize_rcp(float* v) {
-  float inv = 1.0f / __builtin_sqrtf(dotv<DIM>(v, v));
-  for (int k = 0; k < DIM; k++) v[k] = v[k] * inv;
-}
-
-// ---------------------------------------------------------------------------
-// geometry queries (brute force over LDS / global arrays)
-// ---------------------------------------------------------------------------
-
-// wide closest point on a segment (wide_query_operations.h:121-141)
-template <int DIM>
-__device__ __forceinline__ float cp_segment(const float* pa, const float* pb, const float* x, float* pt, float* t) {
-  float u[DIM], v[DIM];
-  for (int k = 0; k < DIM; k++) { u[k] = pb[k] - pa[k]; v[k] = x[k] - pa[k]; }
-  float c1 = dotv<DIM>(u, v), c2 = dotv<DIM>(u, u);
-  float tt = c1 * (1.0f / c2);
-  if (c1 <= 0.0f) tt = 0.0f;
-  if (c2 <= c1) tt = 1.0f;
-  float d[DIM];
-  for (int k = 0; k < DIM; k++) { pt[k] = pa[k] + u[k] * tt; d[k] = x[k] - pt[k]; }
-  *t = tt;
-  return normv<DIM>(d);
-}
-
-// wide closest point on a triangle (wide_query_operations.h:144-235)
-__device__ __forceinline__ float cp_triangle(const float* pa, const float* pb, const float* pc, const float* x,
-                                             float* pt, float* t0, float* t1) {
-  float ab[3], ac[3], ax[3], d[3];
-  for (int k = 0; k < 3; k++) { ab[k] = pb[k] - pa[k]; ac[k] = pc[k] - pa[k]; ax[k] = x[k] - pa[k]; }
-  float d1 = dotv<3>(ab, ax), d2 = dotv<3>(ac, ax);
-  if (d1 <= 0.0f && d2 <= 0.0f) {
-    for (int k = 0; k < 3; k++) { pt[k] = pa[k]; d[k] = x[k] - pt[k]; }
-    *t0 = 1.0f; *t1 = 0.0f; return normv<3>(d);
-  }
-  float bx[3]; for (int k = 0; k < 3; k++) bx[k] = x[k] - pb[k];
-  float d3 = dotv<3>(ab, bx), d4 = dotv<3>(ac, bx);
-  if (d3 >= 0.0f && d4 <= d3) {
-    for (int k = 0; k < 3; k++) { pt[k] = pb[k]; d[k] = x[k] - pt[k]; }
-    *t0 = 0.0f; *t1 = 1.0f; return normv<3>(d);
-  }
-  float cx[3]; for (int k = 0; k < 3; k++) cx[k] = x[k] - pc[k];
-  float d5 = dotv<3>(ab, cx), d6 = dotv<3>(ac, cx);
-  if (d6 >= 0.0f && d5 <= d6) {
-    for (int k = 0; k < 3; k++) { pt[k] = pc[k]; d[k] = x[k] - pt[k]; }
-    *t0 = 0.0f; *t1 = 0.0f; return normv<3>(d);
-  }
-  float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.0f && d1 >= 0.0f && d3 <= 0.0f) {
-    float v = d1 * (1.0f / (d1 - d3));
-    for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ab[k] * v; d[k] = x[k] - pt[k]; }
-    *t0 = 1.0f - v; *t1 = v; return normv<3>(d);
-  }
-  float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) {
-    float w = d2 * (1.0f / (d2 - d6));
-    for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ac[k] * w; d[k] = x[k] - pt[k]; }
-    *t0 = 1.0f - w; *t1 = 0.0f; return normv<3>(d);
-  }
-  float va = d3 * d6 - d5 * d4;
-  if (va <= 0.0f && (d4 - d3) >= 0.0f && (d5 - d6) >= 0.0f) {
-    float w = (d4 - d3) * (1.0f / ((d4 - d3) + (d5 - d6)));
-    for (int k = 0; k < 3; k++) { pt[k] = pb[k] + (pc[k] - pb[k]) * w; d[k] = x[k] - pt[k]; }
-    *t0 = 0.0f; *t1 = 1.0f - w; return normv<3>(d);
-  }
-  float denom = 1.0f / (va + vb + vc);
-  float v = vb * denom, w = vc * denom;
-  for (int k = 0; k < 3; k++) { pt[k] = pa[k] + ab[k] * v + ac[k] * w; d[k] = x[k] - pt[k]; }
-  *t0 = 1.0f - v - w; *t1 = v;
-  return normv<3>(d);
-}
-
-// closest point on a 2D segment record [pa | u = pb - pa] (same arithmetic as cp_segment)
-__device__ __forceinline__ float cp_segment_rec(const float* P, const float* x, float* pt, float* t) {
-  float u0 = P[2], u1 = P[3];
-  float v0 = x[0] - P[0], v1 = x[1] - P[1];
-  float c1 = u0 * v0 + u1 * v1, c2 = u0 * u0 + u1 * u1;
-  float tt = c1 * (1.0f / c2);
-  if (c1 <= 0.0f) tt = 0.0f;
-  if (c2 <= c1) tt = 1.0f;
-  pt[0] = P[0] + u0 * tt; pt[1] = P[1] + u1 * tt;
-  float d0 = x[0] - pt[0], d1 = x[1] - pt[1];
-  *t = tt;
-  return __builtin_sqrtf(d0 * d0 + d1 * d1);
-}
-
-template <int DIM>
-__device__ __forceinline__ float cp_prim(const float* P, const float* x, float* pt, float* t0, float* t1) {
-  if constexpr (DIM == 2) { *t1 = 0.0f; return cp_segment_rec(P, x, pt, t0); }
-  else return cp_triangle(P, P + 3, P + 6, x, pt, t0, t1);
-}
-
-struct Closest { float d; float p[3]; float t0, t1; int prim; };
-
-// Wave-cooperative closest point over `np` primitives (key fl(d*d), last index
-// wins ties, mbvh.inl:1297-1351); the result is uniform across the wave.
-template <int DIM>
-__device__ Closest closest_wave(const float* prims, int np, const float* x, int lane) {
-  constexpr int PS = Layout<DIM>::prim;
-  float bk = kFltMax; int bi = -1;
-  for (int p = lane; p < np; p += kWave) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    float d2 = d * d;
-    if (d2 <= bk) { bk = d2; bi = p; }
-  }
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    float ok = __shfl_xor(bk, off);
-    int oi = __shfl_xor(bi, off);
-    if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
-  }
-  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
-  c.p[0] = c.p[1] = c.p[2] = 0.0f;
-  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
-  return c;
-}
-
-// Interaction::computeNormal via normal(uv) (line_segments.inl:57-73, triangles.inl:61-89)
-template <int DIM>
-__device__ __forceinline__ void closest_normal(const float* aux, const Closest& c, float* n) {
-  constexpr int AS = Layout<DIM>::aux;
-  const float* A = aux + c.prim * AS;
-  if constexpr (DIM == 2) {
-    const float* src = (c.t0 <= kFltEps) ? A : (c.t0 >= 1.0f - kFltEps) ? A + 2 : A + 4;
-    n[0] = src[0]; n[1] = src[1];
-  } else {
-    float u0 = c.t0, u1 = c.t1;
-    int vI = -1, eI = -1;
-    if (u0 >= 1.0f - kFltEps && u1 <= kFltEps) vI = 0;
-    else if (u0 <= kFltEps && u1 >= 1.0f - kFltEps) vI = 1;
-    else if (u0 <= kFltEps && u1 <= kFltEps) vI = 2;
-    if (vI == -1) {
-      if (u0 <= kFltEps) eI = 1;
-      else if (u1 <= kFltEps) eI = 2;
-      else if (u0 + u1 >= 1.0f - kFltEps) eI = 0;
-    }
-    const float* src = vI >= 0 ? A + 3 * vI : eI >= 0 ? A + 9 + 3 * eI : A + 18;
-    n[0] = src[0]; n[1] = src[1]; n[2] = src[2];
-  }
-}
-
-template <int DIM>
-__device__ __forceinline__ float signed_dist(const float* aux, const Closest& c, const float* x) {
-  float n[DIM], d[DIM];
-  closest_normal<DIM>(aux, c, n);
-  for (int k = 0; k < DIM; k++) d[k] = x[k] - c.p[k];
-  return (dotv<DIM>(d, n) > 0.0f ? 1.0f : -1.0f) * c.d;
-}
-
-// computeDistToDirichlet without Dirichlet geometry: far bbox corner
-// (fcpw_scene_loader.h:312-314, bounding_volumes.h:64-69)
-template <int DIM>
-__device__ __forceinline__ float bbox_far_dist(const DevScene& sc, const float* x) {
-  float m[DIM];
-  for (int k = 0; k < DIM; k++) m[k] = smin(sc.pmin[k] - x[k], x[k] - sc.pmax[k]);
-  return __builtin_sqrtf(dotv<DIM>(m, m));
-}
-
-// per-lane (non-cooperative) closest distance to the Dirichlet boundary
-// Squared distance from x to a padded group box: below the computed distance of
-// every member (the padding dwarfs the rounding of both), so skipping a group whose
-// bound exceeds the running minimum never skips the scan's result.
-template <int DIM>
-__device__ __forceinline__ float box_dist2(const float* B, const float* x) {
-  float d2 = 0.0f;
-  for (int k = 0; k < DIM; k++) {
-    const float e = smax(smax(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
-    d2 += e * e;
-  }
-  return d2;
-}
-
-// computeDistToDirichlet (fcpw_scene_loader.h:299-315) over the Dirichlet
-// primitives, groups of kGroup culled by their boxes.  The sequential `<=` scan
-// returns d of the highest-index primitive attaining the minimum computed d^2;
-// here the group with the smallest box bound is evaluated first (a tight running
-// minimum), then every other group whose bound does not exceed it, keeping
-// (min d^2, highest index) -- the same primitive, hence the same d.
-template <int DIM>
-__device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, const float* dgroup,
-                                       const float* x) {
-  if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
-  constexpr int PS = Layout<DIM>::prim;
-  const int ng = sc.n_dgroups;
-  int g0 = 0;
-  float lb0 = kFltMax;
-  for (int gi = 0; gi < ng; gi++) {
-    const float lb = box_dist2<DIM>(dgroup + gi * kGroupStride, x);
-    if (lb < lb0) { lb0 = lb; g0 = gi; }
-  }
-  float sr2 = kFltMax, best = kFltMax;
-  int bestp = -1;
-  for (int k = 0; k < ng; k++) {
-    const int gi = k == 0 ? g0 : (k <= g0 ? k - 1 : k);
-    if (k > 0 && box_dist2<DIM>(dgroup + gi * kGroupStride, x) > sr2) continue;
-    const int p1 = (gi + 1) * kGroup < sc.n_dprims ? (gi + 1) * kGroup : sc.n_dprims;
-    for (int p = gi * kGroup; p < p1; p++) {
-      float pt[DIM], t0, t1;
-      const float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
-      const float d2 = d * d;
-      if (d2 < sr2 || (d2 == sr2 && p > bestp)) { sr2 = d2; best = d; bestp = p; }
-    }
-  }
-  return best;
-}
-
-template <int DIM>
-__device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
-  if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
-  constexpr int PS = Layout<DIM>::prim;
-  float sr2 = kFltMax, best = kFltMax;
-  for (int p = 0; p < sc.n_dprims; p++) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(sc.dprim + p * PS, x, pt, &t0, &t1);
-    float d2 = d * d;
-    if (d2 <= sr2) { sr2 = d2; best = d; }
-  }
-  return best;
-}
-
-struct Hit { float p[3], n[3], d; };
-
-// Exact ray-primitive test of the reference (mbvh.inl:521-609 + wide_query_operations.h
-// 27-92, line_segments.inl / triangles.inl ray queries): accepts when the hit
-// distance d satisfies 0 <= d <= rt and then shrinks rt to d.  Visiting primitives
-// in index order this yields the minimum d, ties going to the larger index.
-template <int DIM>
-__device__ __forceinline__ bool ray_prim_exact(const float* P, const float* o, const float* dir, float& rt, Hit* h) {
-  if constexpr (DIM == 2) {
-    float u0 = P[0] - o[0], u1 = P[1] - o[1];
-    float v0 = P[2], v1 = P[3];  // record holds v = pb - pa
-    float dv = dir[0] * v1 - dir[1] * v0;
-    if (!(__builtin_fabsf(dv) > kFltEps)) return false;
-    float ud = u0 * dir[1] - u1 * dir[0];
-    float uv = u0 * v1 - u1 * v0;
-    float inv = 1.0f / dv;
-    float t = ud * inv;
-    if (!(t >= 0.0f && t <= 1.0f)) return false;
-    float d = uv * inv;
-    if (!(d >= 0.0f && d <= rt)) return false;
-    rt = d;
-    h->d = d;
-    h->p[0] = P[0] + t * v0; h->p[1] = P[1] + t * v1;
-    h->n[0] = v1; h->n[1] = -v0;
-    return true;
-  } else {
-    float v1[3], v2[3], pp[3], s[3], q[3];
-    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; s[k] = o[k] - P[k]; }
-    cross3(pp, dir, v2);
-    float det = dotv<3>(v1, pp);
-    if (!(__builtin_fabsf(det) > kFltEps)) return false;
-    float inv = 1.0f / det;
-    float v = dotv<3>(s, pp) * inv;
-    if (!(v >= 0.0f && v <= 1.0f)) return false;
-    cross3(q, s, v1);
-    float w = dotv<3>(dir, q) * inv;
-    if (!(w >= 0.0f && v + w <= 1.0f)) return false;
-    float d = dotv<3>(v2, q) * inv;
-    if (!(d >= 0.0f && d <= rt)) return false;
-    rt = d;
-    h->d = d;
-    for (int k = 0; k < 3; k++) h->p[k] = P[k] + v1[k] * v + v2[k] * w;
-    cross3(h->n, v1, v2);
-    return true;
-  }
-}
-
-template <int DIM>
-__device__ __forceinline__ bool ray_hit_scan(const float* prims, int np, const float* o, const float* dir,
-                                             float tmax, Hit* h) {
-  constexpr int PS = Layout<DIM>::prim;
-  bool found = false;
-  float rt = tmax;
-  for (int p = 0; p < np; p++) found |= ray_prim_exact<DIM>(prims + p * PS, o, dir, rt, h);
-  if (found) normalize_rcp<DIM>(h->n);
-  return found;
-}
-
-// Geometry as staged in LDS: primitives, silhouette candidates and the culling
-// boxes of kGroup consecutive primitives / silhouettes.
-struct LGeom {
-  const float* prim;
-  const float* sil;
-  const float* pgroup;
-  const float* sgroup;
-  const uint32_t* sgrid;  // star-radius cell grid (u16 offsets | u8 lists), nullptr if none
-  int sgrid_off_words;
-  const float* dprim;     // Dirichlet primitives + their culling boxes (walk kernel)
-  const float* dgroup;
-};
-
-// Certain rejection of a whole group for a ray segment [o, o + rt*dir]: slab
-// test against the group's padded box.  The padding (1e-4 of the scene span)
-// dwarfs the rounding of the slab arithmetic, so a group whose primitives the
-// exact test could hit within rt is never skipped.  rcp(0) = inf and NaN slabs
-// (origin exactly on a padded face) fall out of min/max, which only errs
-// toward visiting.
-template <int DIM>
-__device__ __forceinline__ bool ray_box_maybe(const float* B, const float* o, const float* inv, float rt) {
-  float tn = -kFltMax, tf = kFltMax;
-  for (int k = 0; k < DIM; k++) {
-    const float t1 = (B[k] - o[k]) * inv[k], t2 = (B[4 + k] - o[k]) * inv[k];
-    tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
-    tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
-  }
-  return tn <= tf && tf >= 0.0f && tn <= rt * 1.00001f + 1e-6f;
-}
-
-// First ray hit within tmax (mbvh.inl:521-609 + wide_query_operations.h:27-92)
-// in index order: min d, ties to the larger index.  Groups of primitives the
-// ray cannot reach are skipped (for the whole wave when no lane needs them);
-// inside a group every primitive first goes through a division-free
-// certain-rejection test using the hardware reciprocal (v_rcp_f32, |rel err| <=
-// 2^-22; signs exact, magnitudes with a 1e-5 relative margin), so only
-// primitives the exact test could accept reach the IEEE division.  Skipped
-// groups and pre-filtered primitives are exactly those the plain loop rejects,
-// so the result and every computed value equal the plain loop's (and the
-// oracle's).
-template <int DIM>
-__device__ __forceinline__ bool ray_hit(const LGeom& G, int np, int ng, const float* o, const float* dir,
-                                        float tmax, Hit* h) {
-  constexpr int PS = Layout<DIM>::prim;
-  float inv[DIM];
-  for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
-  bool found = false;
-  float rt = tmax;
-  for (int gi = 0; gi < ng; gi++) {
-    if (!ray_box_maybe<DIM>(G.pgroup + gi * kGroupStride, o, inv, rt)) continue;
-    const int p1 = (gi + 1) * kGroup < np ? (gi + 1) * kGroup : np;
-    for (int p = gi * kGroup; p < p1; p++) {
-      const float* P = G.prim + p * PS;
-      if constexpr (DIM == 2) {
-        const float u0 = P[0] - o[0], u1 = P[1] - o[1];
-        const float v0 = P[2], v1 = P[3];
-        const float dv = dir[0] * v1 - dir[1] * v0;
-        if (!(__builtin_fabsf(dv) > kFltEps)) continue;
-        const float ud = u0 * dir[1] - u1 * dir[0];
-        const float uv = u0 * v1 - u1 * v0;
-        const float ra = __builtin_amdgcn_rcpf(dv);
-        const float ta = ud * ra, da = uv * ra;
-        if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
-            (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
-          continue;
-      } else {
-        float v1[3], v2[3], pp[3], sv[3], q[3];
-        for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; sv[k] = o[k] - P[k]; }
-        cross3(pp, dir, v2);
-        const float det = dotv<3>(v1, pp);
-        if (!(__builtin_fabsf(det) > kFltEps)) continue;
-        const float ra = __builtin_amdgcn_rcpf(det);
-        const float vn = dotv<3>(sv, pp), va = vn * ra;
-        if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) continue;
-        cross3(q, sv, v1);
-        const float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
-        const float wa = wn * ra, da = dn * ra;
-        if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
-            (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
-          continue;
-      }
-      found |= ray_prim_exact<DIM>(P, o, dir, rt, h);
-    }
-  }
-  if (found) normalize_rcp<DIM>(h->n);
-  return found;
-}
-
-// occlusion-only ray test (hasLineOfSight, primitive.h:225-235)
-template <int DIM>
-__device__ bool ray_occluded(const float* prims, int np, const float* o, const float* dir, float tmax) {
-  Hit h;
-  return ray_hit_scan<DIM>(prims, np, o, dir, tmax, &h);
-}
-
-// isWideSilhouetteVertex / isWideSilhouetteEdge (wide_query_operations.h:328-395)
-template <int DIM>
-__device__ __forceinline__ bool is_silhouette(const float* S, const float* view, float d, bool flip, float prec) {
-  float sign = flip ? 1.0f : -1.0f;
-  const float* n0 = DIM == 2 ? S + 2 : S + 6;
-  const float* n1 = DIM == 2 ? S + 4 : S + 9;
-  if (!(d > prec)) {
-    if constexpr (DIM == 2) {
-      float det = n0[0] * n1[1] - n0[1] * n1[0];
-      return sign * det > prec;
-    } else {
-      float ed[3], c[3];
-      for (int k = 0; k < 3; k++) ed[k] = S[3 + k] - S[k];
-      normalize_rcp<3>(ed);
-      cross3(c, n0, n1);
-      float ang = fatan2(dotv<3>(ed, c), dotv<3>(n0, n1));
-      return sign * ang > prec;
-    }
-  }
-  float inv = 1.0f / d;
-  float u[DIM];
-  for (int k = 0; k < DIM; k++) u[k] = view[k] * inv;
-  float dot0 = dotv<DIM>(u, n0), dot1 = dotv<DIM>(u, n1);
-  if (__builtin_fabsf(dot0) <= prec) return sign * dot1 > prec;
-  if (__builtin_fabsf(dot1) <= prec) return sign * dot0 > prec;
-  return dot0 * dot1 < 0.0f;
-}
-
-// isWideSilhouetteVertex without the division and square root: the view
-// direction is normalised with the hardware rsq, whose error (with the dot-product
-// rounding) stays below 1e-6 on the unit-scale dots, so outside a 1e-5 band
-// around every threshold the decision equals the exact test's.  Returns 1/0 when
-// certain, 2 when the exact test must decide.  (2D vertex candidates.)
-__device__ __forceinline__ int silhouette_class2(const float* S, const float* view, float d2raw, bool flip,
-                                                 float prec) {
-  const float sign = flip ? 1.0f : -1.0f;
-  const float* n0 = S + 2;
-  const float* n1 = S + 4;
-  const float p2 = prec * prec;
-  if (d2raw < p2 * 0.9999f) {  // certainly d <= prec: the exact test's normal-only branch
-    const float det = n0[0] * n1[1] - n0[1] * n1[0];
-    return sign * det > prec ? 1 : 0;
-  }
-  if (d2raw <= p2 * 1.0001f) return 2;
-  const float r = __builtin_amdgcn_rsqf(d2raw);
-  const float dot0 = (view[0] * n0[0] + view[1] * n0[1]) * r;
-  const float dot1 = (view[0] * n1[0] + view[1] * n1[1]) * r;
-  const float tol = 1e-5f;
-  const float a0 = __builtin_fabsf(dot0), a1 = __builtin_fabsf(dot1);
-  float v;
-  if (a0 < prec - tol) {
-    v = sign * dot1;
-  } else if (a0 > prec + tol) {
-    if (a1 > prec + tol) return dot0 * dot1 < 0.0f ? 1 : 0;
-    if (!(a1 < prec - tol)) return 2;
-    v = sign * dot0;
-  } else {
-    return 2;
-  }
-  return v > prec + tol ? 1 : (v < prec - tol ? 0 : 2);
-}
-
-// Certain rejection of a whole silhouette group: the squared distance from x to
-// the group's padded box exceeds r2 (with margin), so every candidate in it is
-// rejected by the exact distance test too.
-template <int DIM>
-__device__ __forceinline__ bool ball_box_maybe(const float* B, const float* x, float r2) {
-  float d2 = 0.0f;
-  for (int k = 0; k < DIM; k++) {
-    const float e = __builtin_fmaxf(__builtin_fmaxf(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
-    d2 += e * e;
-  }
-  return !(d2 > r2 * 1.00001f);
-}
-
-// Certain absence of silhouettes in a group, from the normal cone (axis a,
-// half-angle alpha) and the view cone of x on the group's bounding sphere (axis
-// w = x - c, half-angle beta = asin(rho/|w|)): every view direction u and every
-// adjacent normal n then satisfy angle(u, n) in [theta - alpha - beta, theta +
-// alpha + beta], theta = angle(w, a).  When that interval lies inside
-// [0, acos(prec + m)) every dot is > prec + m (all faces front-facing), when it
-// lies inside (pi - acos(prec + m), pi] every dot is < -(prec + m): either way the
-// exact test (isWideSilhouetteVertex/Edge) rejects every candidate.  m = 1e-3
-// dwarfs the error of the rsq/sqrt arithmetic used here.  Groups holding a
-// candidate next to a missing primitive, or x within prec of the sphere, are
-// never culled.
-template <int DIM>
-__device__ __forceinline__ bool cone_culled(const float* B, const float* x, float prec) {
-  if (B[15] != 0.0f) return false;
-  const float rho = B[11];
-  float w[DIM];
-  for (int k = 0; k < DIM; k++) w[k] = x[k] - B[8 + k];
-  const float D2 = dotv<DIM>(w, w);
-  const float lim = rho + 1.01f * prec + 1e-6f;
-  if (!(D2 > lim * lim)) return false;
-  const float invD = __builtin_amdgcn_rsqf(D2);
-  const float sinb = rho * invD, cosb = __builtin_amdgcn_sqrtf(smax(0.0f, 1.0f - sinb * sinb));
-  const float sina = B[3], cosa = B[7];
-  const float cosg = cosa * cosb - sina * sinb, sing = sina * cosb + cosa * sinb;  // gamma = alpha + beta
-  float wa = 0.0f;
-  for (int k = 0; k < DIM; k++) wa += w[k] * B[12 + k];
-  const float cost = smin(smax(wa * invD, -1.0f), 1.0f), sint = __builtin_amdgcn_sqrtf(smax(0.0f, 1.0f - cost * cost));
-  const float thr = prec + 1e-3f;
-  // front: theta + gamma in (0, pi) and cos(theta + gamma) > thr
-  const float c_p = cost * cosg - sint * sing, s_p = sint * cosg + cost * sing;
-  if (s_p > 1e-3f && c_p > thr) return true;
-  // back: theta - gamma in (0, pi) and cos(theta - gamma) < -thr
-  const float c_m = cost * cosg + sint * sing, s_m = sint * cosg - cost * sing;
-  return s_m > 1e-3f && c_m < -thr;
-}
-
-// computeStarRadius (fcpw_scene_loader.h:621-641): the closest silhouette point
-// within maxR, candidates in index order (brute force over the staged records,
-// fcpw Baseline semantics); groups out of reach are skipped, 2D candidates are
-// classified by silhouette_class2 before any exact square root or division.
-template <int DIM>
-__device__ __forceinline__ float star_radius(const LGeom& G, int ns, int nsg, int np, const float* x, float minR,
-                                             float maxR, float prec, bool flipOrient) {
-  constexpr int SS = Layout<DIM>::sil;
-  if (minR > maxR) return maxR;
-  if (np > 0) {
-    bool flip = !flipOrient;
-    float r2 = maxR < kFltMax ? maxR * maxR : kFltMax;
-    float minR2 = minR * minR;
-    bool found = false, done = false;
-    float best = 0.0f;
-    DIAG_LANE(D_SCALLS);
-    if (!(minR2 >= r2)) {
-      for (int gi = 0; gi < nsg && !done; gi++) {
-        const float* B = G.sgroup + gi * kSGroupStride;
-        if (!ball_box_maybe<DIM>(B, x, r2) || cone_culled<DIM>(B, x, prec)) continue;
-        DIAG_LANE(D_SGVISIT);
-        const int s1 = (gi + 1) * kGroup < ns ? (gi + 1) * kGroup : ns;
-        for (int s = gi * kGroup; s < s1; s++) {
-          const float* S = G.sil + s * SS;
-          const float miss = DIM == 2 ? S[6] : S[12];
-          float view[DIM], d;
-          int cls = 2;
-          if constexpr (DIM == 2) {
-            view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
-            float d2raw = view[0] * view[0] + view[1] * view[1];
-            // certain rejection: fl(fl(sqrt(q))^2) >= q(1 - 2^-22) > r2 (no sqrt needed)
-            if (d2raw > r2 * 1.000001f) continue;
-            DIAG_LANE(D_SCAND);
-            cls = miss != 0.0f ? 1 : silhouette_class2(S, view, d2raw, flip, prec);
-            if (cls == 0) continue;  // certainly not a silhouette: the exact loop skips it too
-            DIAG_LANE(D_SEXACT);
-            d = __builtin_sqrtf(d2raw);
-          } else {
-            // certain rejection against the edge's bounding sphere before the exact query
-            float e[3], hl[3];
-            for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
-            float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
-            float lo = dm - hr;
-            if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) continue;
-            float pt[3], t;
-            d = cp_segment<3>(S, S + 3, x, pt, &t);
-            for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
-            if (miss != 0.0f) cls = 1;
-          }
-          float d2 = d * d;
-          if (d2 > r2) continue;
-          bool sil_ok = cls == 1 ? true : is_silhouette<DIM>(S, view, d, flip, prec);
-          if (sil_ok && d2 <= r2) {
-            r2 = d2; best = d; found = true;
-            if (minR2 >= r2) { done = true; break; }
-          }
-        }
-      }
-    }
-    if (found) return smax(best, minR);
-  }
-  return smax(maxR, minR);
-}
-
-// offsetPointAlongDirection (fcpw_scene_loader.h:258-290)
-template <int DIM>
-__device__ __forceinline__ void offset_point(const float* p, const float* n, float* out) {
-  const float origin = 1.0f / 32.0f, floatScale = 1.0f / 65536.0f, intScale = 256.0f;
-  for (int k = 0; k < DIM; k++) {
-    int no = cvt_trunc(n[k] * intScale);
-    float po = bits_to_float((uint32_t)((int32_t)float_to_bits(p[k]) + (p[k] < 0 ? -no : no)));
-    out[k] = __builtin_fabsf(p[k]) < origin ? p[k] + floatScale * n[k] : po;
-  }
-}
-
-// PDE source lookup: scene.h:194-198 + image.h:53-58 (2D), scene_3d.h:120-126 (3D)
-template <int DIM>
-__device__ __forceinline__ float source_value(const DevScene& sc, const float* x) {
-  if (sc.source == nullptr) return 0.0f;
-  if (WOS_ABL_CONST_SRC) return 0.5f;
-  if constexpr (DIM == 2) {
-    float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
-    float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
-    int h = sc.sdims[0], w = sc.sdims[1];
-    int i = sclamp(cvt_trunc(uy * (float)h), 0, h - 1);
-    int j = sclamp(cvt_trunc(ux * (float)w), 0, w - 1);
-    return sc.source[(size_t)i * w + j];
-  } else {
-    int X = sc.sdims[0], Y = sc.sdims[1], Z = sc.sdims[2];
-    float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
-    float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
-    float uz = (x[2] - sc.pmin[2]) / sc.ext[2];
-    int i = sclamp(cvt_trunc(ux * (float)X), 0, X - 1);
-    int j = sclamp(cvt_trunc(uy * (float)Y), 0, Y - 1);
-    int k = sclamp(cvt_trunc(uz * (float)Z), 0, Z - 1);
-    return sc.source[((size_t)i * Y + j) * Z + k];
-  }
-}
-
-template <int DIM>
-__device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x) {
-  for (int k = 0; k < DIM; k++)
-    if (!(x[k] >= sc.pmin[k] && x[k] <= sc.pmax[k])) return true;
-  return false;
-}
-
-// float Bessel approximations (defined with the certified rejection fast path below)
-__device__ __forceinline__ float i0_fast(float x);
-__device__ __forceinline__ float k0_fast(float x);
-__device__ __forceinline__ float i1_fast(float x);
-__device__ __forceinline__ float k1_fast(float x);
-
-// ---------------------------------------------------------------------------
-// Green's functions on balls (distributions.h:273-832)
-// ---------------------------------------------------------------------------
-template <int DIM>
-struct Gfn {
-  bool yukawa;
-  float c[DIM], yVol[DIM], ySurf[DIM];
-  float R, r;
-  float lambda, sqrtLambda;
-  float muR, A0, A1, B0, B1;   // 2D: K0muR I0muR K1muR I1muR ; 3D: expmuR sinhmuR K32muR I32muR
-  static constexpr float rClamp = 1e-4f;
-
-  __device__ __forceinline__ void init(bool yuk, float lam) {
-    yukawa = yuk; lambda = lam; sqrtLambda = __builtin_sqrtf(lam);
-  }
-
-  __device__ __forceinline__ void update_ball(const float* cc, float RR) {
-    for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
-    R = RR; r = 0.0f;
-    if (!yukawa) return;
-    muR = R * sqrtLambda;
-    if constexpr (DIM == 2) {
-#if WOS_ABL_FAST_BESSEL
-      A0 = k0_fast(muR); A1 = i0_fast(muR); B0 = k1_fast(muR); B1 = i1_fast(muR);
-#else
-      double i0, k0, i1, k1;
-      bessel_ik<true, true>((double)muR, &i0, &k0, &i1, &k1);
-      A0 = (float)k0;
-      A1 = (float)i0;
-      B0 = (float)k1;
-      B1 = (float)i1;
-#endif
-    } else {
-      float expmuR = fexp(-muR);
-      float exp2muR = expmuR * expmuR;
-      float coshmuR = (1.0f + exp2muR) / (2.0f * expmuR);
-      float sinhmuR = (1.0f - exp2muR) / (2.0f * expmuR);
-      A0 = expmuR; A1 = sinhmuR;
-      B0 = expmuR * (1.0f + 1.0f / muR);
-      B1 = coshmuR - sinhmuR / muR;
-    }
-  }
-
-  // G(r) for the current r (evaluate())
-  __device__ __forceinline__ float evaluate() const {
-    if (!yukawa) {
-      if constexpr (DIM == 2) return (float)((double)flog(R / r) / kTwoPi);
-      else return (float)((double)(1.0f / r - 1.0f / R) / kFourPi);
-    }
-    float mur = r * sqrtLambda;
-    if constexpr (DIM == 2) {
-      double i0, k0;
-      bessel_ik<true, false>((double)mur, &i0, &k0, nullptr, nullptr);
-      float K0mur = (float)k0;
-      float I0mur = (float)i0;
-      return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
-    } else {
-      float expmur = fexp(-mur);
-      float sinhmur = (1.0f - expmur * expmur) / (2.0f * expmur);
-      return (float)((double)(expmur - A0 * sinhmur / A1) / (kFourPi * (double)r));
-    }
-  }
-
-  __device__ __forceinline__ float poisson_kernel() const {
-    if (!yukawa) return DIM == 2 ? (float)(1.0 / kTwoPi) : (float)(1.0 / kFourPi);
-    if constexpr (DIM == 2) return (float)(1.0 / (kTwoPi * (double)A1));
-    else return (float)((double)muR / (kFourPi * (double)A1));
-  }
-
-  __device__ __forceinline__ float norm() const {
-    if (!yukawa) return DIM == 2 ? R * R / 4.0f : R * R / 6.0f;
-    double pk = (double)poisson_kernel();
-    return (float)((1.0 - (DIM == 2 ? kTwoPi : kFourPi) * pk) / (double)lambda);
-  }
-
-  __device__ __forceinline__ float gradient_norm() const {
-    if (!yukawa) {
-      if constexpr (DIM == 2) { float r2 = r * r; return (float)((double)(1.0f / r2 - 1.0f / (R * R)) / kTwoPi); }
-      else { float r3 = r * r * r; return (float)((double)(1.0f / r3 - 1.0f / (R * R * R)) / kFourPi); }
-    }
-    float mur = r * sqrtLambda;
-    if constexpr (DIM == 2) {
-      double i1, k1;
-      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
-      float K1mur = (float)k1;
-      float I1mur = (float)i1;
-      float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
-      return (float)((double)Qr / (kTwoPi * (double)r));
-    } else {
-      float r2 = r * r;
-      float expmur = fexp(-mur);
-      float exp2mur = expmur * expmur;
-      float coshmur = (1.0f + exp2mur) / (2.0f * expmur);
-      float sinhmur = (1.0f - exp2mur) / (2.0f * expmur);
-      float K32mur = expmur * (1.0f + 1.0f / mur);
-      float I32mur = coshmur - sinhmur / mur;
-      float Qr = sqrtLambda * (K32mur - I32mur * B0 / B1);
-      return (float)((double)Qr / (kFourPi * (double)r2));
-    }
-  }
-
-  __device__ __forceinline__ void gradient(float* out) const {
-    float gn = gradient_norm();
-    for (int k = 0; k < DIM; k++) out[k] = (yVol[k] - c[k]) * gn;
-  }
-
-  __device__ __forceinline__ void poisson_kernel_gradient(float* out) const {
-    float d[DIM];
-    for (int k = 0; k < DIM; k++) d[k] = ySurf[k] - c[k];
-    if (!yukawa) {
-      if constexpr (DIM == 2) {
-        float s = (float)((kTwoPi * (double)R) * (double)R);
-        for (int k = 0; k < 2; k++) out[k] = (2.0f * d[k]) / s;
-      } else {
-        float s = (float)((kFourPi * (double)R) * (double)R);
-        for (int k = 0; k < 3; k++) out[k] = (3.0f * d[k]) / s;
-      }
-      return;
-    }
-    if constexpr (DIM == 2) {
-      float QR = sqrtLambda / (R * B1);
-      for (int k = 0; k < 2; k++) out[k] = (d[k] * QR) / (float)kTwoPi;
-    } else {
-      float QR = lambda / B1;
-      for (int k = 0; k < 3; k++) out[k] = (d[k] * QR) / (float)kFourPi;
-    }
-  }
-
-  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y) const {
-    if (!yukawa) return 1.0f;
-    float d[DIM];
-    for (int k = 0; k < DIM; k++) d[k] = y[k] - c[k];
-    float rr = smax(rClamp, normv<DIM>(d));
-    float mur = rr * sqrtLambda;
-    if constexpr (DIM == 2) {
-#if WOS_ABL_FAST_BESSEL
-      float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
-#else
-      double i1, k1;
-      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
-      float K1mur = (float)k1;
-      float I1mur = (float)i1;
-#endif
-      float Q = K1mur + I1mur * A0 / A1;
-      return mur * Q;
-    } else {
-      float expmur = fexp(-mur);
-      float exp2mur = expmur * expmur;
-      float coshmur = (1.0f + exp2mur) / (2.0f * expmur);
-      float sinhmur = (1.0f - exp2mur) / (2.0f * expmur);
-      float K32mur = expmur * (1.0f + 1.0f / mur);
-      float I32mur = coshmur - sinhmur / mur;
-      float Q = K32mur + I32mur * A0 / A1;
-      return mur * Q;
-    }
-  }
-
-  // off-centred G(x,y): only reached in the non-finite (NaN-propagation) regime
-  __device__ float evaluate_xy(const float* x, const float* y) const {
-    float yx[DIM], xc[DIM], yc[DIM];
-    for (int k = 0; k < DIM; k++) { yx[k] = y[k] - x[k]; xc[k] = x[k] - c[k]; yc[k] = y[k] - c[k]; }
-    if (!yukawa) {
-      float rr = smax(rClamp, normv<DIM>(yx));
-      if constexpr (DIM == 2) return (float)((double)(flog(R * R - dotv<2>(xc, yc)) - flog(R * rr)) / kTwoPi);
-      else return (float)((double)(1.0f / rr - R / (R * R - dotv<3>(xc, yc))) / kFourPi);
-    }
-    float r1 = smax(rClamp, normv<DIM>(yx));
-    float r2 = (R * R - dotv<DIM>(xc, yc)) / R;
-    float mur1 = r1 * sqrtLambda, mur2 = r2 * sqrtLambda;
-    if constexpr (DIM == 2) {
-      float K0mur1 = (float)bessk0((double)mur1), K0mur2 = (float)bessk0((double)mur2);
-      float I0mur1 = (float)bessi0((double)mur1), I0mur2 = (float)bessi0((double)mur2);
-      float Q1 = K0mur1 - I0mur1 * A0 / A1;
-      float Q2 = K0mur2 - I0mur2 * A0 / A1;
-      return (float)((double)(Q1 - Q2) / kTwoPi);
-    } else {
-      float e1 = fexp(-mur1), e2 = fexp(-mur2);
-      float s1 = (1.0f - e1 * e1) / (2.0f * e1), s2 = (1.0f - e2 * e2) / (2.0f * e2);
-      float Q1 = (e1 - A0 * s1 / A1) / r1;
-      float Q2 = (e2 - A0 * s2 / A1) / r2;
-      return (float)((double)(Q1 - Q2) / kFourPi);
-    }
-  }
-};
-
-template <int DIM>
-__device__ __forceinline__ float pdf_sphere_uniform(float r) {
-  if constexpr (DIM == 2) return (float)(1.0 / (kTwoPi * (double)r));
-  else return (float)(1.0 / ((kFourPi * (double)r) * (double)r));
-}
-
-template <int DIM>
-__device__ __forceinline__ void sample_unit_sphere(const float* u, float* out) {
-  if constexpr (DIM == 2) {
-    float phi = (float)(kTwoPi * (double)u[0]);
-    fsincos(phi, &out[1], &out[0]);
-  } else {
-    float z = 1.0f - 2.0f * u[0];
-    float r = __builtin_sqrtf(smax(0.0f, 1.0f - z * z));
-    float phi = (float)(kTwoPi * (double)u[1]);
-    float s, c;
-    fsincos(phi, &s, &c);
-    out[0] = r * c; out[1] = r * s; out[2] = z;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Certified float fast path for the rejection test.  The accept decision
-// u < pdfRadius/bound is first evaluated with float Bessel approximations (same
-// A&S polynomials, hardware exp2/log2/rsq); only when |u - T| falls inside a
-// rigorous error band is the exact double-precision path (the reference's
-// arithmetic) evaluated.  The decision -- hence every RNG draw and every later
-// value -- is therefore identical to the exact loop.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float exp_fast(float x) {  // e^x to ~2 ulp for |x| < 87
-  const float L = 1.44269502162933349609375f, Llo = 1.925963033500011e-08f;
-  float hi = x * L;
-  float lo = __builtin_fmaf(x, L, -hi) + x * Llo;
-  return __builtin_amdgcn_exp2f(hi) * (1.0f + lo * 0.693147182f);
-}
-
-__device__ __forceinline__ float i0_fast(float x) {
-  if (x < 3.75f) {
-    float y = x / 3.75f;
-    y = y * y;
-    return 1.0f + y * (3.5156229f + y * (3.0899424f + y * (1.2067492f + y * (0.2659732f + y * (0.360768e-1f +
-           y * 0.45813e-2f)))));
-  }
-  float y = 3.75f / x;
-  float poly = 0.39894228f + y * (0.1328592e-1f + y * (0.225319e-2f + y * (-0.157565e-2f + y * (0.916281e-2f +
-               y * (-0.2057706e-1f + y * (0.2635537e-1f + y * (-0.1647633e-1f + y * 0.392377e-2f)))))));
-  return exp_fast(x) * __builtin_amdgcn_rsqf(x) * poly;
-}
-
-__device__ __forceinline__ float k0_fast(float x) {
-  if (x <= 2.0f) {
-    float y = x * x / 4.0f;
-    return (-__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * i0_fast(x) +
-           (-0.57721566f + y * (0.42278420f + y * (0.23069756f + y * (0.3488590e-1f + y * (0.262698e-2f +
-            y * (0.10750e-3f + y * 0.74e-5f))))));
-  }
-  float y = 2.0f / x;
-  return exp_fast(-x) * __builtin_amdgcn_rsqf(x) * (1.25331414f + y * (-0.7832358e-1f + y * (0.2189568e-1f +
-         y * (-0.1062446e-1f + y * (0.587872e-2f + y * (-0.251540e-2f + y * 0.53208e-3f))))));
-}
-
-__device__ __forceinline__ float i1_fast(float x) {
-  if (x < 3.75f) {
-    float y = x / 3.75f;
-    y = y * y;
-    return x * (0.5f + y * (0.87890594f + y * (0.51498869f + y * (0.15084934f + y * (0.2658733e-1f +
-           y * (0.301532e-2f + y * 0.32411e-3f))))));
-  }
-  float y = 3.75f / x;
-  float a = 0.2282967e-1f + y * (-0.2895312e-1f + y * (0.1787654e-1f - y * 0.420059e-2f));
-  a = 0.39894228f + y * (-0.3988024e-1f + y * (-0.362018e-2f + y * (0.163801e-2f + y * (-0.1031555e-1f + y * a))));
-  return exp_fast(x) * __builtin_amdgcn_rsqf(x) * a;
-}
-
-__device__ __forceinline__ float k1_fast(float x) {
-  if (x <= 2.0f) {
-    float y = x * x / 4.0f;
-    return (__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * i1_fast(x) +
-           (1.0f / x) * (1.0f + y * (0.15443144f + y * (-0.67278579f + y * (-0.18156897f + y * (-0.1919402e-1f +
-           y * (-0.110404e-2f + y * (-0.4686e-4f)))))));
-  }
-  float y = 2.0f / x;
-  return exp_fast(-x) * __builtin_amdgcn_rsqf(x) * (1.25331414f + y * (0.23498619f + y * (-0.3655620e-1f +
-         y * (0.1504268e-1f + y * (-0.780353e-2f + y * (0.325614e-2f + y * (-0.68245e-3f)))))));
-}
-
-// K0 and I0 of the rejection fast path at one argument: the polynomials of
-// k0_fast / i0_fast, with I0 and x^-1/2 shared (k0_fast at x <= 2 re-evaluates I0) and
-// the divisions by / of x as reciprocal products.  The reciprocals add ~1 ulp to y,
-// far inside the 8e-6 band the decisions are certified with (the GPU self-test checks
-// the <= 2e-6 error against the double-precision A&S functions).
-#ifndef WOS_FUSED_K0I0
-#define WOS_FUSED_K0I0 1
-#endif
-__device__ __forceinline__ void k0i0_fast(float x, float* k0, float* i0) {
-  if (!WOS_FUSED_K0I0) { *k0 = k0_fast(x); *i0 = i0_fast(x); return; }
-  const float rs = __builtin_amdgcn_rsqf(x);
-  const float rx = __builtin_amdgcn_rcpf(x);
-  float iv;
-  if (x < 3.75f) {
-    float y = x * 0.266666681f;
-    y = y * y;
-    iv = 1.0f + y * (3.5156229f + y * (3.0899424f + y * (1.2067492f + y * (0.2659732f + y * (0.360768e-1f +
-         y * 0.45813e-2f)))));
-  } else {
-    const float y = 3.75f * rx;
-    const float poly = 0.39894228f + y * (0.1328592e-1f + y * (0.225319e-2f + y * (-0.157565e-2f + y * (0.916281e-2f +
-                       y * (-0.2057706e-1f + y * (0.2635537e-1f + y * (-0.1647633e-1f + y * 0.392377e-2f)))))));
-    iv = exp_fast(x) * rs * poly;
-  }
-  float kv;
-  if (x <= 2.0f) {
-    const float y = x * x * 0.25f;
-    kv = (-__builtin_amdgcn_logf(x * 0.5f) * 0.693147182f) * iv +
-         (-0.57721566f + y * (0.42278420f + y * (0.23069756f + y * (0.3488590e-1f + y * (0.262698e-2f +
-          y * (0.10750e-3f + y * 0.74e-5f))))));
-  } else {
-    const float y = 2.0f * rx;
-    kv = exp_fast(-x) * rs * (1.25331414f + y * (-0.7832358e-1f + y * (0.2189568e-1f +
-         y * (-0.1062446e-1f + y * (0.587872e-2f + y * (-0.251540e-2f + y * 0.53208e-3f))))));
-  }
-  *k0 = kv;
-  *i0 = iv;
-}
-
-// Certain-reject bound of the Yukawa rejection test.  The test accepts iff
-// u < T(r) = (K0(mu r) - rho I0(mu r)) r / (norm bound) (2D) or
-// (e^{-mu r} - rho sinh(mu r)) r / (norm bound) (3D), with rho = A0/A1 > 0 and the
-// subtracted term >= 0 for 0 <= r <= R, so T(r) <= r K0(mu r) / (norm bound)
-// <= 0.46652 / (mu norm bound) (max_z z K0(z) at z = 0.595) and in 3D
-// T(r) <= r e^{-mu r} / (norm bound) <= 1 / (e mu norm bound).  The constants carry
-// a 1e-3 margin (far above the A&S polynomial error and the float rounding of the
-// exact path), so u above the bound is the exact test's reject without evaluating
-// r at all.  A non-positive or non-finite bound disables the shortcut.
-// Tighter, per ball: T(r) <= R F(mu R) / (norm bound) with F(s) = max_x x Q_s(x)
-// tabulated by bins of s with a 2 % margin (DevParams::rej_tab, wos_host_scene.h
-// rejection_bound_table) -- the subtracted term is kept, so the bound follows the
-// real peak of the threshold (tests/test_rejection_bounds.py checks both bounds).
-#ifndef WOS_QUICK_REJ
-#define WOS_QUICK_REJ 1
-#endif
-template <int DIM>
-__device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, float muR, float sqrtL, float invNB) {
-  if (!WOS_QUICK_REJ) return 3.0e38f;
-  const float C = DIM == 2 ? 0.4670f : 0.3683f;
-  float q = C * invNB / sqrtL;
-  if (prm.rej_tab != nullptr && muR >= 0.0f) {
-    const int k = (int)(kRejTabScale * __builtin_sqrtf(muR));
-    if (k < kRejTabBins) {
-      const float qt = R * prm.rej_tab[(DIM == 3 ? kRejTabBins : 0) + k] * invNB;
-      q = qt < q ? qt : q;
-    }
-  }
-  return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
-}
-
-// sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
-// need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
-template <int DIM>
-__device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg32& s, float* pdf, float* out,
-                                              uint32_t* iters, bool need_pdf) {
-  const float R = g.R;
-  if (DIM == 3 && !g.yukawa) {
-    float u1 = s.nextf(), u2 = s.nextf();
-    float phi = (float)(kTwoPi * (double)u2);
-    float r = (1.0f + __builtin_sqrtf(1.0f - fcbrt(u1 * u1)) * fcos(phi)) * R / 2.0f;
-    r = smax(Gfn<DIM>::rClamp, r);
-    if (r > R) r = R / 2.0f;
-    g.r = r;
-    for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + r * dir[k]; out[k] = g.yVol[k]; }
-    *pdf = g.evaluate() / g.norm();
-    return;
-  }
-  float bound;
-  if (!g.yukawa) {
-    bound = 1.5f / R;
-  } else {
-    const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
-    const float lam = g.lambda, sl = g.sqrtLambda;
-    bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
-                     : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
-  }
-  // norm() depends only on the ball: hoisted out of the loop (same value every iteration)
-  const float nrm = g.norm();
-  // fast path: 2D Yukawa while I0 stays finite in float (float Bessels need mu*r < ~88)
-  const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
-  const float rho = g.A0 / g.A1;
-  const float invNB = 1.0f / (nrm * bound);
-  const float quick = g.yukawa ? rej_quick_bound<DIM>(DevParams{}, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
-  int iter = 0;
-  do {
-    float u = s.nextf();
-    g.r = s.nextf() * R;
-    iter++;
-    int decided = -1;  // 1 accept, 0 reject, -1 undecided
-    if (u > quick) {
-      decided = 0;
-    } else if (fast) {
-      const float mur = g.r * g.sqrtLambda;
-      float k0, i0v;
-      k0i0_fast(mur, &k0, &i0v);
-      const float ip = i0v * rho;
-      const float c = g.r * invNB;
-      const float Tf = (k0 - ip) * c;
-      const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
-      if (u < Tf - M) decided = 1;
-      else if (u > Tf + M) decided = 0;
-    }
-    if (decided < 0) {
-      float p = g.evaluate() / nrm;
-      float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
-      decided = u < pdfRadius / bound ? 1 : 0;
-    }
-    if (decided == 1 || WOS_ABL_ONE_REJ) break;
-  } while (iter < 1000);
-  if (need_pdf) *pdf = g.evaluate() / nrm;  // pdf of the last sampled radius (before the clamps)
-  *iters += (uint32_t)iter;
-  g.r = smax(Gfn<DIM>::rClamp, g.r);
-  if (g.r > R) g.r = R / 2.0f;
-  for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
-}
-
-// ---------------------------------------------------------------------------
-// Wave-cooperative rejection sampling (rejectionSampleGreensFn, distributions.h:
-// 362-383) for the 2D Yukawa fast path.  Iteration j of a lane's loop consumes
-// draws 2j and 2j+1 of its PCG32 stream, and state_k = A_k * state_0 + C_k (the
-// jump table), so the iterations of all lanes can be evaluated in any order by
-// any lane.  Each generation gives every unfinished lane a block of B = 64 /
-// (#unfinished) consecutive iterations spread over the wave; the owner then scans
-// its block in order -- the first certain accept wins, an undecided iteration is
-// decided by the owner with the exact double-precision test -- exactly the
-// sequential loop's decisions, so the accepted radius, the iteration count and
-// the stream position after the loop are the sequential ones.  This removes the
-// geometric tail (the wave paid for the longest loop of its lanes).  Lanes off
-// the fast path (3D, harmonic, mu*R >= 80) run the sequential loop.
-// ---------------------------------------------------------------------------
-constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
-// minimum iterations per unfinished lane and generation of the cooperative sampler
-// (2D acceptance ~21 %, 3D ~7 % on the shipped scenes)
-#ifndef WOS_REJ_BMIN2
-#define WOS_REJ_BMIN2 1
-#endif
-#ifndef WOS_REJ_BMIN3
-#define WOS_REJ_BMIN3 16
-#endif
-template <int DIM>
-constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3;
-static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16, "RejLDS::surv holds 64 * 16 items");
-// 1: screen a generation's items with the certain-reject bound, then evaluate the
-// survivors compacted over the wave; 0 (default): every lane evaluates its own
-// items (the screen + compaction measured 15-20 % slower on karman / cube / C)
-#ifndef WOS_REJ_COMPACT
-#define WOS_REJ_COMPACT 0
-#endif
-
-// PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
-__device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
-  const uint64_t A = prm.jump[2 * k], Cc = prm.jump[2 * k + 1];
-  return A * s0 + Cc;
-}
-
-// The jump constants of the first kRejJumpLds rejection iterations (draw 2j) are
-// staged in LDS by every kernel that samples (stage_rej_jump); later iterations
-// (P ~ 1e-4 per sample) read the global table.
-#ifndef WOS_REJ_JUMP_LDS
-#define WOS_REJ_JUMP_LDS 128
-#endif
-constexpr int kRejJumpLds = WOS_REJ_JUMP_LDS > 0 ? WOS_REJ_JUMP_LDS : 1;
-__shared__ unsigned long long s_rej_jump[2 * kRejJumpLds];
-
-__device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
-  for (int i = threadIdx.x; i < 2 * kRejJumpLds; i += blockDim.x) s_rej_jump[i] = prm.jump[4 * (i >> 1) + (i & 1)];
-}
-
-// stream state before rejection iteration j (draw 2j) from stream start s0
-__device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0, int j) {
-  if (WOS_REJ_JUMP_LDS > 0 && j < kRejJumpLds) return s_rej_jump[2 * j] * s0 + s_rej_jump[2 * j + 1];
-  return jump_state(prm, s0, 2 * j);
-}
-
-// floor(item / B) for item < 2048, 1 <= B <= 32, with m = ceil(2^16 / B): writing
-// item = qB + r, item*m/2^16 = q + (r + item*e/2^16)/B with e = mB - 2^16 < B, and
-// item*e < 2^16, so the floor is q.  (A runtime u32 division is ~20 VALU ops per item.)
-#ifndef WOS_FASTDIV
-#define WOS_FASTDIV 1
-#endif
-// The sampler's generation has items = nact * B with B = clamp(64 / nact, kRejBmin, kRejBcap):
-// items <= 64 when B = floor(64 / nact) or B = kRejBcap (then nact < 2), else
-// items = nact * kRejBmin <= 64 * kRejBmin.  rej_div needs items <= 2048 and B <= 32.
-constexpr int kRejBcap = 32;
-static_assert(kRejBcap <= 32, "rej_div: e = m B - 2^16 < B <= 32");
-static_assert(kWave * (WOS_REJ_BMIN2 > WOS_REJ_BMIN3 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3) <= 2048 && kWave <= 2048,
-              "rej_div: item * e < 2^16 needs items <= 2048");
-__device__ __forceinline__ int rej_div(int item, int B, uint32_t mB) {
-  if (!WOS_FASTDIV) return item / B;
-  return (int)(((uint32_t)item * mB) >> 16);
-}
-
-struct RejLDS {
-  unsigned long long s0[kWave];
-  float R[kWave], sqrtL[kWave];
-  float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
-  float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
-  float qb[kWave];                 // certain-reject bound (rej_quick_bound)
-#if WOS_REJ_COMPACT
-  uint16_t surv[kWave * 16];       // items that passed the certain-reject screen (one generation)
-#endif
-  float nrm[kWave], bound[kWave];
-  uint32_t base[kWave], acc[kWave], und[kWave];
-  uint32_t owner_of[kWave];
-};
-
-__device__ __forceinline__ float draw_float(uint64_t state) {
-  return bits_to_float((pcg_output(state) >> 9) | 0x3f800000u) - 1.0f;
-}
-
-// the two draws of rejection iteration j from stream start s0
-__device__ __forceinline__ void rej_draws(const DevParams& prm, uint64_t s0, int j, float* u, float* x) {
-  const uint64_t st = rej_state(prm, s0, j);
-  *u = draw_float(st);
-  *x = draw_float(st * kPcgMult + kPcgInc);
-}
-
-// fast decision of one iteration: 1 accept, 0 reject, -1 undecided (see sample_volume)
-__device__ __forceinline__ int rej_fast_decide(float u, float r, float sqrtL, float rho, float invNB) {
-  const float mur = r * sqrtL;
-  float k0, i0v;
-  k0i0_fast(mur, &k0, &i0v);
-  const float ip = i0v * rho;
-  const float c = r * invNB;
-  const float Tf = (k0 - ip) * c;
-  const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
-  return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
-}
-
-// 3D analogue: e = exp(-mu r) from exp_fast (<= ~3 ulp) and an approximate
-// reciprocal; the band M covers their error carried through the cancellation in
-// sinh(mu r) = (1 - e^2) / 2e and Q = e - (A0/A1) sinh, plus the rounding of the
-// exact path's float/double steps (~4 ulp of T), with a >= 4x margin.  Non-finite
-// or underflowed e leaves M non-finite: undecided.
-__device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, float rho, float invNB) {
-  const float mur = r * sqrtL;
-  const float e = exp_fast(-mur);
-  const float ie = __builtin_amdgcn_rcpf(e);
-  const float sh = (1.0f - e * e) * 0.5f * ie;
-  const float Q = e - rho * sh;
-  const float c = r * invNB;
-  const float Tf = Q * c;
-  const float ar = __builtin_fabsf(rho);
-  const float M = (2e-6f * e + ar * (3e-7f * ie + 2e-6f * e + 4e-6f * __builtin_fabsf(sh))) * c +
-                  4e-6f * __builtin_fabsf(Tf) + 1e-30f;
-  return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
-}
-
-// exact 3D Yukawa test of one iteration with an owner's ball constants: the same
-// Gfn::evaluate / pdf arithmetic as sample_volume, hence the same decision
-__device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, float sqrtL, float A0, float A1, float nrm,
-                                                 float bound) {
-  Gfn<3> h;
-  h.yukawa = true;
-  h.sqrtLambda = sqrtL;
-  h.A0 = A0;
-  h.A1 = A1;
-  h.R = R;
-  h.r = r;
-  const float p = h.evaluate() / nrm;
-  const float pdfRadius = p / pdf_sphere_uniform<3>(r);
-  return u < pdfRadius / bound ? 1 : 0;
-}
-
-// Convergent: every lane calls it.  Inactive lanes do nothing.  2D: certified float
-// decisions by any lane, undecided ones by the owner (exact); 3D: certified float
-// decisions by any lane, undecided ones by the same lane with the exact test (cheap
-// single-precision arithmetic plus one exp).
-template <int DIM>
-__device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM>& g, const float* dir,
-                                                   Pcg32& s, float* pdf, float* out, uint32_t* iters,
-                                                   bool need_pdf, RejLDS* L, int lane) {
-  bool coop = false;
-  float bound = 0.0f, nrm = 1.0f;
-  if (active && g.yukawa && !WOS_ABL_ONE_REJ &&
-      (DIM == 3 || (g.muR < 80.0f && !WOS_NO_FASTREJ))) {
-    const float R = g.R, lam = g.lambda, sl = g.sqrtLambda;
-    const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
-    bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
-                     : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
-    nrm = g.norm();
-    coop = true;
-  }
-  if (__ballot(coop) != 0) {
-    const uint64_t s0 = s.state;
-    if (coop) {
-      L->s0[lane] = s0;
-      L->R[lane] = g.R;
-      L->sqrtL[lane] = g.sqrtLambda;
-      L->qb[lane] = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, 1.0f / (nrm * bound));
-      if constexpr (DIM == 2) {
-        L->c0[lane] = g.A0 / g.A1;
-        L->c1[lane] = 1.0f / (nrm * bound);
-      } else {
-        L->c0[lane] = g.A0;
-        L->c1[lane] = g.A1;
-        L->rho3[lane] = g.A0 / g.A1;
-        L->inv3[lane] = 1.0f / (nrm * bound);
-        L->nrm[lane] = nrm;
-        L->bound[lane] = bound;
-      }
-    }
-    int j0 = 0, jacc = -1;
-    bool done = !coop;
-    DIAG_COUNT(D_RCALLS, 1);
-    DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
-    for (;;) {
-      const uint64_t pend = __ballot(!done);
-      if (pend == 0) break;
-      const int nact = __popcll(pend);
-      DIAG_COUNT(D_RGENS, 1);
-      // B consecutive iterations per unfinished lane, at least kRejBmin (fewer
-      // generations -- each costs three wave syncs and the owners' scan -- for a
-      // few iterations evaluated past an accept)
-      int B = kWave / nact;
-      B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > kRejBcap ? kRejBcap : B);
-      const int items = nact * B, per = (items + kWave - 1) / kWave;
-      // item / B as a multiply-shift (exact: item < 2048, B <= 32, see rej_div)
-      const uint32_t mB = (65536u + (uint32_t)B - 1u) / (uint32_t)B;
-      if (!done) {
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
-        L->owner_of[rank] = (uint32_t)lane;
-        L->base[lane] = (uint32_t)j0;
-        L->acc[lane] = 0u;
-        L->und[lane] = 0u;
-      }
-      wave_sync();
-#if WOS_REJ_COMPACT
-      // phase A: the certain-reject screen of every item (its first draw only);
-      // phase B: the survivors, compacted, evaluated densely by the whole wave
-      uint32_t keep = 0;
-      for (int q = 0; q < per; q++) {
-        const int item = lane * per + q;
-        const int orank = rej_div(item, B, mB), b = item - orank * B;
-        if (orank < nact) {
-          const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
-          DIAG_LANE(D_RITEMS);
-          if (j < kRejMax) {
-            if (!(draw_float(rej_state(prm, L->s0[owner], j)) > L->qb[owner])) keep |= 1u << q;
-            else DIAG_LANE(D_RQUICK);
-          }
-        }
-      }
-      {
-        const uint32_t kc = (uint32_t)__popc(keep);
-        uint32_t incl = kc;
-        for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-          const uint32_t v = __shfl_up(incl, dlt);
-          if (lane >= dlt) incl += v;
-        }
-        const uint32_t total = __shfl(incl, kWave - 1);
-        uint32_t pos = incl - kc;
-        for (uint32_t m = keep; m; m &= m - 1) L->surv[pos++] = (uint16_t)(lane * per + __builtin_ctz(m));
-        wave_sync();
-        for (uint32_t k = lane; k < total; k += kWave) {
-          const int item = (int)L->surv[k];
-          const int orank = rej_div(item, B, mB), b = item - orank * B;
-          const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
-          const uint64_t st = rej_state(prm, L->s0[owner], j);
-          const float u = draw_float(st);
-          const float x = draw_float(st * kPcgMult + kPcgInc);
-          int dcs;
-          if constexpr (DIM == 2) {
-            dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
-          } else {
-            const float rr = x * L->R[owner];
-            dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
-            if (dcs < 0)
-              dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
-                                      L->bound[owner]);
-          }
-          if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
-          else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
-        }
-      }
-#else
-      for (int q = 0; q < per; q++) {
-        const int item = lane * per + q;
-        const int orank = rej_div(item, B, mB), b = item - orank * B;
-        if (orank < nact) {
-          const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
-          if (j < kRejMax) {
-            const uint64_t st = rej_state(prm, L->s0[owner], j);
-            const float u = draw_float(st);
-            int dcs = 0;
-            DIAG_LANE(D_RITEMS);
-            if (u > L->qb[owner]) {
-              // certain reject: the radius draw is not needed
-              DIAG_LANE(D_RQUICK);
-            } else if constexpr (DIM == 2) {
-              const float x = draw_float(st * kPcgMult + kPcgInc);
-              dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
-            } else {
-              const float x = draw_float(st * kPcgMult + kPcgInc);
-              const float rr = x * L->R[owner];
-              dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
-              if (dcs < 0)
-                dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
-                                        L->bound[owner]);
-            }
-            if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
-            else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
-          }
-        }
-      }
-#endif
-      wave_sync();
-      if (!done) {
-        const uint32_t acc = L->acc[lane], und = L->und[lane];
-        int b = 0;
-        while (!done && b < B) {
-          if (j0 + b >= kRejMax) { jacc = kRejMax - 1; done = true; break; }  // limit: last radius kept
-          const uint32_t m = (acc | und) >> b;
-          if (m == 0u) { b = B; break; }
-          b += __builtin_ctz(m);
-          if (b >= B) break;
-          if (j0 + b >= kRejMax) { jacc = kRejMax - 1; done = true; break; }
-          if ((acc >> b) & 1u) { jacc = j0 + b; done = true; break; }
-          // undecided: the exact test of sample_volume, by the owner
-          float u, x;
-          rej_draws(prm, s0, j0 + b, &u, &x);
-          g.r = x * g.R;
-          const float p = g.evaluate() / nrm;
-          const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
-          if (u < pdfRadius / bound) { jacc = j0 + b; done = true; break; }
-          b++;
-        }
-        if (!done) {
-          j0 += B;
-          if (j0 >= kRejMax) { jacc = kRejMax - 1; done = true; }
-        }
-      }
-      wave_sync();
-    }
-    if (coop) {
-      float u, x;
-      rej_draws(prm, s0, jacc, &u, &x);
-      g.r = x * g.R;
-      s.state = rej_state(prm, s0, jacc + 1);
-      *iters += (uint32_t)(jacc + 1);
-      if (need_pdf) *pdf = g.evaluate() / nrm;
-      g.r = smax(Gfn<DIM>::rClamp, g.r);
-      if (g.r > g.R) g.r = g.R / 2.0f;
-      for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
-    }
-  }
-  if (active && !coop) sample_volume<DIM>(g, dir, s, pdf, out, iters, need_pdf);
-}
-
-// ---------------------------------------------------------------------------
-// walk (walk_on_stars.h:135-329)
-// ---------------------------------------------------------------------------
-template <int DIM>
-struct WalkState {
-  float pt[DIM], n[DIM], prevDir[DIM];
-  float prevDist, throughput;
-  bool onNeumann;
-  int walkLength;
-  float totalNeumann, totalSource;
-};
-
-template <int DIM>
-__device__ __forceinline__ float prim_area(const float* P) {
-  if constexpr (DIM == 2) {
-    float s[2] = {P[2], P[3]};  // record holds v = pb - pa
-    return normv<2>(s);
-  } else {
-    float v1[3], v2[3], n[3];
-    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; }
-    cross3(n, v1, v2);
-    return 0.5f * normv<3>(n);
-  }
-}
-
-// Neumann boundary sample (walk_on_stars.h:212-260).  With the reference's h == 0
-// (scene.h:176-181) the term is exactly +0 unless G or the throughput is
-// non-finite; only then the brute-force stochastic sample is evaluated.
-template <int DIM>
-__device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM>& g,
-                                          WalkState<DIM>& st, float R, const float* rn) {
-  constexpr int PS = Layout<DIM>::prim;
-  const int np = sc.n_prims;
-  const float* x = st.pt;
-  float total = 0.0f;
-  for (int p = 0; p < np; p++) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    if (d * d <= R * R) {
-      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
-      total += prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
-    }
-  }
-  if (!(total > 0.0f)) return;
-  float target = rn[0] * total, acc = 0.0f, selw = 0.0f;
-  int sel = -1;
-  for (int p = 0; p < np; p++) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    if (d * d <= R * R) {
-      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
-      float w = prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
-      acc += w; sel = p; selw = w;
-      if (target < acc) break;
-    }
-  }
-  if (sel < 0) return;
-  const float* P = prims + sel * PS;
-  float sp[DIM], sn[DIM], pdf;
-  if constexpr (DIM == 2) {
-    float s0 = P[2], s1 = P[3];  // record holds v = pb - pa
-    float sv[2] = {s0, s1};
-    float area = normv<2>(sv), u = rn[1];
-    sp[0] = P[0] + u * s0; sp[1] = P[1] + u * s1;
-    sn[0] = s1 / area; sn[1] = -s0 / area;
-    pdf = 1.0f / area;
-  } else {
-    float v1[3], v2[3];
-    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; }
-    cross3(sn, v1, v2);
-    float area = normv<3>(sn);
-    float u1 = __builtin_sqrtf(rn[1]), u2 = rn[2], u = 1.0f - u1, v = u2 * u1, w = 1.0f - u - v;
-    for (int k = 0; k < 3; k++) { sp[k] = P[k] * u + P[3 + k] * v + P[6 + k] * w; sn[k] /= area; }
-    pdf = 2.0f / area;
-  }
-  pdf *= selw / total;
-  float dts[DIM];
-  for (int k = 0; k < DIM; k++) dts[k] = sp[k] - x[k];
-  float distToSample = normv<DIM>(dts);
-  float alpha = st.onNeumann ? 2.0f : 1.0f;
-  if (pdf > 0.0f && distToSample < R) {
-    float p1[DIM], p2[DIM], mn[DIM];
-    for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
-    if (st.onNeumann) offset_point<DIM>(x, mn, p1); else for (int k = 0; k < DIM; k++) p1[k] = x[k];
-    for (int k = 0; k < DIM; k++) mn[k] = -sn[k];
-    offset_point<DIM>(sp, mn, p2);
-    float dd[DIM];
-    for (int k = 0; k < DIM; k++) dd[k] = p2[k] - p1[k];
-    float dn = normv<DIM>(dd);
-    for (int k = 0; k < DIM; k++) dd[k] /= dn;
-    if (!ray_occluded<DIM>(prims, np, p1, dd, dn)) {
-      float G = g.evaluate_xy(x, sp);
-      float hval = 0.0f;
-      st.totalNeumann += st.throughput * alpha * G * hval / pdf;
-    }
-  }
-}
-
-// One iteration of the walk loop (walk_on_stars.h:135-329), split around the
-// star-radius query so that the query can run wave-cooperatively:
-//   walk_step_begin  -- loop test (Dirichlet distance above the epsilon shell),
-//                       double-sided normal flip, whether a silhouette query is due;
-//   star_radius_wave -- (convergent, all lanes) computeStarRadius;
-//   walk_step_end    -- ball update, direction, ray, source sample, move, roulette.
-// Returns -1 while the walk continues, else its termination code.
-template <int DIM>
-__device__ __forceinline__ int walk_step_begin(const DevScene& sc, const DevParams& prm, float dirichletDist,
-                                               WalkState<DIM>& st, bool* flip, bool* query) {
-  if (!(dirichletDist > prm.epsilon_shell)) return WC_DIRICHLET;
-  *flip = false;
-  if (sc.double_sided && st.onNeumann) {
-    if (st.prevDist > 0.0f && dotv<DIM>(st.prevDir, st.n) < 0.0f) {
-      for (int k = 0; k < DIM; k++) st.n[k] *= -1.0f;
-      *flip = true;
-    }
-  }
-  *query = !(prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL);
-  return -1;
-}
-
-// ball + direction + ray origin; the ray query follows (walk_on_stars.h:169-210)
-template <int DIM>
-__device__ __forceinline__ float walk_step_mid(const DevParams& prm, float dirichletDist, Pcg32& smp, Gfn<DIM>& g,
-                                               WalkState<DIM>& st, uint32_t* steps, bool query, float starQ,
-                                               float* dir, float* org) {
-  float starRadius = dirichletDist;
-  if (query) {
-    starRadius = starQ;
-    if (prm.min_star_radius <= dirichletDist) starRadius = smax(0.99f * starRadius, prm.min_star_radius);
-  }
-  g.update_ball(st.pt, starRadius);
-  (*steps)++;
-  float u[2];
-  u[0] = smp.nextf();
-  if constexpr (DIM == 3) u[1] = smp.nextf();
-  sample_unit_sphere<DIM>(u, dir);
-  if (st.onNeumann && dotv<DIM>(st.n, dir) > 0.0f)
-    for (int k = 0; k < DIM; k++) dir[k] *= -1.0f;
-  if (st.onNeumann) {
-    float mn[DIM];
-    for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
-    offset_point<DIM>(st.pt, mn, org);
-  } else {
-    for (int k = 0; k < DIM; k++) org[k] = st.pt[k];
-  }
-  return starRadius;
-}
-
-// after the ray query: the miss point and the Neumann term (walk_on_stars.h:200-260);
-// the source sample (convergent, sample_volume_wave) and walk_step_tail follow
-template <int DIM>
-__device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
-                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, float starRadius,
-                                              const float* dir, const float* org, bool hit, Hit& ip) {
-  const int np = sc.n_prims;
-  const float* prims = G.prim;
-  if (!hit) {
-    for (int k = 0; k < DIM; k++) { ip.p[k] = org[k] + starRadius * dir[k]; ip.n[k] = 0.0f; }
-    ip.d = starRadius;
-  }
-  if (!prm.ignore_neumann) {
-    float rn[3] = {0.0f, 0.0f, 0.0f};
-    for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
-    bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
-    if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
-  }
-}
-
-// after the source sample (walk_on_stars.h:270-327)
-template <int DIM>
-__device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G, const DevParams& prm,
-                                              float& dirichletDist,
-                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, const float* dir,
-                                              bool hit, const Hit& ip, const float* sp) {
-  if (!prm.ignore_source) {
-    if (g.r <= ip.d) {
-      float contrib = g.norm() * source_value<DIM>(sc, sp);
-      st.totalSource += st.throughput * contrib;
-    }
-  }
-  if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
-  st.prevDist = ip.d;
-  for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
-  st.onNeumann = hit;
-  st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
-  if (st.throughput < prm.rr_threshold) {
-    float survival = st.throughput / prm.rr_threshold;
-    if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
-    st.throughput = prm.rr_threshold;
-  }
-  st.walkLength++;
-  if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
-  if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
-  dirichletDist = dirichlet_dist_culled<DIM>(sc, G.dprim, G.dgroup, st.pt);
-  return -1;
-}
-
-// ---------------------------------------------------------------------------
-// First ray hit (intersectWithNeumann, fcpw_scene_loader.h:458-484), wave-cooperative.
-// The sequential scan keeps the LAST primitive accepted with d <= rt (rt shrinking
-// to each accepted d): that is the minimum d, ties to the larger index.  So the
-// (lane, primitive) work spreads over the wave like the silhouette query: lanes
-// mark the primitive groups their ray segment can reach (slab test with the
-// initial tmax), the pairs are compacted, every lane evaluates items with the
-// rcp pre-filter + exact test against tmax, and accepted hits fold into the
-// owner's atomicMin on (d bits with -0 -> +0, ~index).  The owner then reruns
-// the exact test on the winner for the hit record (identical arithmetic).
-// ---------------------------------------------------------------------------
-constexpr int kRayChunk = 16;
-
-template <int DIM>
-struct RayLDS {
-  uint32_t list[kWave * kRayChunk];
-  float qo[DIM][kWave], qd[DIM][kWave];
-  float rt[kWave];
-  unsigned long long best[kWave];
-};
-
-// rcp pre-filter of one primitive against rt (certain rejections only), then the exact test
-template <int DIM>
-__device__ __forceinline__ bool ray_prim_filtered(const float* P, const float* o, const float* dir, float& rt,
-                                                  Hit* h) {
-  if constexpr (DIM == 2) {
-    const float u0 = P[0] - o[0], u1 = P[1] - o[1];
-    const float v0 = P[2], v1 = P[3];
-    const float dv = dir[0] * v1 - dir[1] * v0;
-    if (!(__builtin_fabsf(dv) > kFltEps)) return false;
-    const float ud = u0 * dir[1] - u1 * dir[0];
-    const float uv = u0 * v1 - u1 * v0;
-    const float ra = __builtin_amdgcn_rcpf(dv);
-    const float ta = ud * ra, da = uv * ra;
-    if ((ta < 0.0f && __builtin_fabsf(ud) > 1e-30f) || ta > 1.00001f ||
-        (da < 0.0f && __builtin_fabsf(uv) > 1e-30f) || da > rt * 1.00001f)
-      return false;
-  } else {
-    float v1[3], v2[3], pp[3], sv[3], q[3];
-    for (int k = 0; k < 3; k++) { v1[k] = P[3 + k] - P[k]; v2[k] = P[6 + k] - P[k]; sv[k] = o[k] - P[k]; }
-    cross3(pp, dir, v2);
-    const float det = dotv<3>(v1, pp);
-    if (!(__builtin_fabsf(det) > kFltEps)) return false;
-    const float ra = __builtin_amdgcn_rcpf(det);
-    const float vn = dotv<3>(sv, pp), va = vn * ra;
-    if ((va < 0.0f && __builtin_fabsf(vn) > 1e-30f) || va > 1.00001f) return false;
-    cross3(q, sv, v1);
-    const float wn = dotv<3>(dir, q), dn = dotv<3>(v2, q);
-    const float wa = wn * ra, da = dn * ra;
-    if ((wa < 0.0f && __builtin_fabsf(wn) > 1e-30f) || va + wa > 1.00002f ||
-        (da < 0.0f && __builtin_fabsf(dn) > 1e-30f) || da > rt * 1.00001f)
-      return false;
-  }
-  return ray_prim_exact<DIM>(P, o, dir, rt, h);
-}
-
-// Convergent: every lane of the wave calls it; lanes with active == false get false.
-template <int DIM>
-__device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc, bool active, const float* o,
-                                             const float* dir, float tmax, Hit* h, RayLDS<DIM>* L, int lane) {
-  constexpr int PS = Layout<DIM>::prim;
-  const int np = sc.n_prims, ng = sc.n_pgroups;
-  const bool need = active && np > 0;
-  if (__ballot(need) == 0) return false;
-  float inv[DIM];
-  for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
-  if (need) {
-    for (int k = 0; k < DIM; k++) { L->qo[k][lane] = o[k]; L->qd[k][lane] = dir[k]; }
-    L->rt[lane] = tmax;
-    L->best[lane] = ~0ull;
-  }
-  for (int g0 = 0; g0 < ng; g0 += kRayChunk) {
-    uint32_t mask = 0;
-    if (need) {
-      const int gn = (ng - g0) < kRayChunk ? (ng - g0) : kRayChunk;
-      for (int j = 0; j < gn; j++)
-        if (ray_box_maybe<DIM>(G.pgroup + (g0 + j) * kGroupStride, o, inv, tmax)) mask |= 1u << j;
-    }
-    const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
-    uint32_t pos = incl - cnt;
-    for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
-    wave_sync();
-    const uint32_t items = total * kGroup;
-    for (uint32_t k = lane; k < items; k += kWave) {
-      const uint32_t e = L->list[k / kGroup];
-      const int owner = (int)(e >> 26);
-      const int p = (int)(e & 0x3FFFFFFu) * kGroup + (int)(k % kGroup);
-      if (p >= np) continue;
-      float oo[DIM], dd[DIM];
-      for (int q = 0; q < DIM; q++) { oo[q] = L->qo[q][owner]; dd[q] = L->qd[q][owner]; }
-      float rt = L->rt[owner];
-      Hit hh;
-      if (ray_prim_filtered<DIM>(G.prim + p * PS, oo, dd, rt, &hh))
-        atomicMin(&L->best[owner],
-                  ((unsigned long long)__float_as_uint(hh.d + 0.0f) << 32) | (0xFFFFFFFFu - (uint32_t)p));
-    }
-    wave_sync();
-  }
-  bool found = false;
-  if (need) {
-    const unsigned long long key = L->best[lane];
-    if (key != ~0ull) {
-      const int p = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
-      float rt = tmax;
-      found = ray_prim_exact<DIM>(G.prim + p * PS, o, dir, rt, h);
-      if (found) normalize_rcp<DIM>(h->n);
-    }
-  }
-  wave_sync();
-  return found;
-}
-
-// ---------------------------------------------------------------------------
-// computeStarRadius (fcpw_scene_loader.h:621-641), wave-cooperative.
-//
-// The sequential query visits the silhouette candidates in index order, accepts
-// a candidate when it is a silhouette with d^2 <= r2 (r2 = the current best,
-// initially maxR^2), and stops at the first accepted candidate with d^2 <= minR^2.
-// Its result is therefore order-free: the d of the first (lowest-index) accepted
-// candidate with d^2 <= minR^2 if there is one, else the d of the candidate with
-// the minimum d^2, ties to the larger index -- each candidate judged against
-// maxR^2 alone.  So the (lane, candidate) work can be spread over the wave:
-//   1. each querying lane marks the silhouette groups it must visit (padded-box
-//      distance within maxR, normal cone not certainly front/back facing);
-//   2. the (lane, group) pairs are compacted into an LDS list (wave prefix sum);
-//   3. all 64 lanes evaluate the candidate items of the list with the exact
-//      per-candidate test and fold accepted ones into the owner's LDS slots with
-//      atomicMin on (d^2 bits, ~index) and on the index (for the minR break);
-//   4. the owner recomputes d of the winning candidate.
-// The lane-divergent group loops of the sequential form (the wave paid for the
-// union of every lane's groups) become ~(total work)/64 wave iterations.
-// ---------------------------------------------------------------------------
-constexpr int kStarChunk = 16;  // groups per compaction round: at most 64 * 16 list entries
-
-template <int DIM>
-struct StarLDS {
-  uint32_t list[kWave * kStarChunk];
-  float qx[DIM][kWave];
-  float r2[kWave], minR2[kWave];
-  uint32_t flip[kWave];
-  uint32_t brk[kWave];
-  unsigned long long best[kWave];
-};
-
-template <int DIM>
-__host__ __device__ constexpr size_t walk_scratch_bytes() {
-  constexpr size_t a = sizeof(StarLDS<DIM>), b = sizeof(RayLDS<DIM>), c = sizeof(RejLDS);
-  return ((a > b ? (a > c ? a : c) : (b > c ? b : c)) + 15) & ~size_t(15);
-}
-
-// Exact per-candidate test of the sequential loop against r2 (see star_radius).
-template <int DIM>
-__device__ __forceinline__ bool star_candidate(const LGeom& G, int s, const float* x, float r2, bool flip,
-                                               float prec, float* d2out, float* dout = nullptr) {
-  constexpr int SS = Layout<DIM>::sil;
-  const float* S = G.sil + s * SS;
-  const float miss = DIM == 2 ? S[6] : S[12];
-  float view[DIM], d;
-  int cls = 2;
-  if constexpr (DIM == 2) {
-    view[0] = x[0] - S[0]; view[1] = x[1] - S[1];
-    const float d2raw = view[0] * view[0] + view[1] * view[1];
-    if (d2raw > r2 * 1.000001f) return false;  // certain: fl(fl(sqrt(q))^2) >= q(1 - 2^-22)
-    cls = miss != 0.0f ? 1 : silhouette_class2(S, view, d2raw, flip, prec);
-    if (cls == 0) return false;
-    d = __builtin_sqrtf(d2raw);
-  } else {
-    float e[3], hl[3];
-    for (int k = 0; k < 3; k++) { e[k] = x[k] - 0.5f * (S[k] + S[3 + k]); hl[k] = 0.5f * (S[3 + k] - S[k]); }
-    const float dm = __builtin_amdgcn_sqrtf(dotv<3>(e, e)), hr = __builtin_amdgcn_sqrtf(dotv<3>(hl, hl));
-    const float lo = dm - hr;
-    if (lo > 0.0f && lo * lo > r2 * 1.0001f + 1e-6f * dm * dm) return false;
-    float pt[3], t;
-    d = cp_segment<3>(S, S + 3, x, pt, &t);
-    for (int k = 0; k < 3; k++) view[k] = x[k] - pt[k];
-    if (miss != 0.0f) cls = 1;
-  }
-  const float d2 = d * d;
-  if (!(d2 <= r2)) return false;
-  if (cls != 1 && !is_silhouette<DIM>(S, view, d, flip, prec)) return false;
-  *d2out = d2;
-  if (dout) *dout = d;
-  return true;
-}
-
-// Cell of the star-radius grid holding x (cell = (iz * ny + iy) * nx + ix), or -1
-// when there is no grid or x lies outside it.  The host built every cell's list for
-// the cell enlarged well beyond the rounding of this index arithmetic.
-template <int DIM>
-__device__ __forceinline__ int star_cell(const DevScene& sc, const float* x) {
-  int c = 0;
-  for (int k = DIM - 1; k >= 0; k--) {
-    const int nk = sc.sgrid_n[k];
-    const float v = (x[k] - sc.sgrid_min[k]) * sc.sgrid_inv[k];
-    if (!(v >= 0.0f && v < (float)nk)) return -1;
-    int i = (int)v;
-    if (i > nk - 1) i = nk - 1;
-    c = c * nk + i;
-  }
-  return c;
-}
-
-// computeStarRadius for one lane from its cell's candidate list: the sequential
-// scan of star_radius (candidates in index order, r2 shrinking, minR break) over
-// the only candidates that can decide it (wos_host_scene.h StarGrid), hence the
-// full scan's result.
-template <int DIM>
-__device__ __forceinline__ float star_radius_cell(const LGeom& G, int cell, const float* x, float r2, float minR2,
-                                                  float minR, float dflt, bool flip, float prec) {
-  const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
-  const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
-  const int e1 = off[cell + 1];
-  bool found = false;
-  float best = 0.0f;
-  for (int e = off[cell]; e < e1; e++) {
-    float d2, d;
-    if (star_candidate<DIM>(G, (int)lst[e], x, r2, flip, prec, &d2, &d)) {
-      r2 = d2;
-      best = d;
-      found = true;
-      if (minR2 >= r2) break;
-    }
-  }
-  return found ? smax(best, minR) : dflt;
-}
-
-template <int DIM>
-__device__ __forceinline__ float star_candidate_dist(const LGeom& G, int s, const float* x) {
-  constexpr int SS = Layout<DIM>::sil;
-  const float* S = G.sil + s * SS;
-  if constexpr (DIM == 2) {
-    const float v0 = x[0] - S[0], v1 = x[1] - S[1];
-    return __builtin_sqrtf(v0 * v0 + v1 * v1);
-  } else {
-    float pt[3], t;
-    return cp_segment<3>(S, S + 3, x, pt, &t);
-  }
-}
-
-// Convergent: every lane of the wave calls it.  Lanes with query == false get 0.
-template <int DIM>
-__device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene& sc, const DevParams& prm,
-                                                  bool query, const float* x, float maxR, bool flipOrient,
-                                                  StarLDS<DIM>* L, int lane) {
-  const float minR = prm.min_star_radius, prec = prm.silhouette_precision;
-  float result = 0.0f, r2 = 0.0f, minR2 = 0.0f;
-  bool need = false;
-  if (query) {
-    if (minR > maxR) {
-      result = maxR;
-    } else {
-      result = smax(maxR, minR);
-      if (sc.n_prims > 0) {
-        r2 = maxR < kFltMax ? maxR * maxR : kFltMax;
-        minR2 = minR * minR;
-        need = !(minR2 >= r2);
-      }
-    }
-  }
-  // lanes inside the star grid take their cell's short candidate list; the rest
-  // (no grid, outside it) share the wave-cooperative group scan below
-  int c_beg = 0, c_end = 0;
-  bool use_cell = false;
-  if (need && G.sgrid != nullptr) {
-    const int cell = star_cell<DIM>(sc, x);
-    if (cell >= 0) {
-      if (!WOS_CELL_COOP) {
-        result = star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
-        need = false;
-      } else {
-        const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
-        c_beg = off[cell];
-        c_end = off[cell + 1];
-        use_cell = true;
-      }
-    }
-  }
-  if (__ballot(need) == 0) return result;
-  if (need) {
-    for (int k = 0; k < DIM; k++) L->qx[k][lane] = x[k];
-    L->r2[lane] = r2;
-    L->minR2[lane] = minR2;
-    L->flip[lane] = flipOrient ? 0u : 1u;  // computeStarRadius passes !flipNormalOrientation
-    L->brk[lane] = 0xFFFFFFFFu;
-    L->best[lane] = ~0ull;
-  }
-  if (WOS_CELL_COOP && __ballot(use_cell) != 0) {
-    // the (lane, candidate) pairs of all cell lists, spread over the wave in windows
-    // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
-    // the longest list; accepted candidates fold into the owner like the group scan
-    const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
-    const uint32_t cnt = use_cell ? (uint32_t)(c_end - c_beg) : 0u;
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
-    const uint32_t first = incl - cnt;
-    constexpr uint32_t kWin = kWave * kStarChunk;
-    for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
-      for (uint32_t i = 0; i < cnt; i++) {
-        const uint32_t q = first + i;
-        if (q >= w0 && q < w0 + kWin) L->list[q - w0] = ((uint32_t)lane << 26) | (uint32_t)lst[c_beg + i];
-      }
-      wave_sync();
-      const uint32_t items = (total - w0) < kWin ? (total - w0) : kWin;
-      for (uint32_t k = lane; k < items; k += kWave) {
-        const uint32_t e = L->list[k];
-        const int owner = (int)(e >> 26);
-        const int sidx = (int)(e & 0x3FFFFFFu);
-        float xo[DIM];
-        for (int q = 0; q < DIM; q++) xo[q] = L->qx[q][owner];
-        float d2;
-        if (star_candidate<DIM>(G, sidx, xo, L->r2[owner], L->flip[owner] != 0u, prec, &d2)) {
-          atomicMin(&L->best[owner], ((unsigned long long)__float_as_uint(d2) << 32) | (0xFFFFFFFFu - (uint32_t)sidx));
-          if (d2 <= L->minR2[owner]) atomicMin(&L->brk[owner], (uint32_t)sidx);
-        }
-      }
-      wave_sync();
-    }
-  }
-  const bool scan_groups = need && !use_cell;
-  const int nsg = sc.n_sgroups, ns = sc.n_sil;
-  for (int g0 = 0; g0 < nsg && __ballot(scan_groups) != 0; g0 += kStarChunk) {
-    uint32_t mask = 0;
-    if (scan_groups) {
-      const int gn = (nsg - g0) < kStarChunk ? (nsg - g0) : kStarChunk;
-      for (int j = 0; j < gn; j++) {
-        const float* B = G.sgroup + (g0 + j) * kSGroupStride;
-        if (ball_box_maybe<DIM>(B, x, r2) && !cone_culled<DIM>(B, x, prec)) mask |= 1u << j;
-      }
-    }
-    const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
-    uint32_t pos = incl - cnt;
-    for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
-    wave_sync();
-    const uint32_t items = total * kGroup;
-    for (uint32_t k = lane; k < items; k += kWave) {
-      const uint32_t e = L->list[k / kGroup];
-      const int owner = (int)(e >> 26);
-      const int s = (int)(e & 0x3FFFFFFu) * kGroup + (int)(k % kGroup);
-      if (s >= ns) continue;
-      float xo[DIM];
-      for (int q = 0; q < DIM; q++) xo[q] = L->qx[q][owner];
-      float d2;
-      if (star_candidate<DIM>(G, s, xo, L->r2[owner], L->flip[owner] != 0u, prec, &d2)) {
-        atomicMin(&L->best[owner], ((unsigned long long)__float_as_uint(d2) << 32) | (0xFFFFFFFFu - (uint32_t)s));
-        if (d2 <= L->minR2[owner]) atomicMin(&L->brk[owner], (uint32_t)s);
-      }
-    }
-    wave_sync();
-  }
-  if (need) {
-    const uint32_t b = L->brk[lane];
-    const unsigned long long key = L->best[lane];
-    int s = -1;
-    if (b != 0xFFFFFFFFu) s = (int)b;
-    else if (key != ~0ull) s = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
-    if (s >= 0) result = smax(star_candidate_dist<DIM>(G, s, x), minR);
-  }
-  wave_sync();
-  return result;
-}
-
-// ---------------------------------------------------------------------------
-// the solve: three kernels over one batch of points
-// ---------------------------------------------------------------------------
-//   1. wos_first_ball_kernel  -- one wave per query point (atomic point queue):
-//      closest-point setup + inside test, the per-point stratified samples (all
-//      lanes at once from a PCG32 jump-ahead table; only the Fisher-Yates swaps
-//      are serial), then lane = antithetic pair: source sample + boundary
-//      direction of the first ball for both members (walk_on_stars.h:494-575).
-//      Each member becomes a walk task in HBM (start state + its record fields).
-//   2. wos_walk_kernel        -- persistent: every lane runs one walk task at a
-//      time, one step per loop iteration; a lane whose walk ends takes the next
-//      task from its wave's window of the global task queue at the next
-//      iteration, so lanes never idle behind the longest walk of a point.
-//   3. wos_fold_kernel        -- one lane per point: the statistics in walk order
-//      (Welford means with sequential control variates, walk_on_stars.h:500-506,
-//      583-614, 744-877) and the masked outputs (grid.h:155-179, 207-237).
-// The three stages touch HBM only for the task records (~48 B per walk in 2D),
-// which is negligible next to the walk arithmetic.
-
-// stratifiedSample (sampling.h:435-457) on the per-point stream, drawn in parallel:
-// draw k of the stream is pcg_output(A_k * s0 + C_k).  Diagonal draws k < n*sd;
-// the shuffle's bounded draws follow in order (k = n*sd + i*n + j) unless one of
-// them hits PCG's rejection threshold, in which case lane 0 replays the shuffle
-// draws sequentially from the true stream.
-
-// The shuffle `for j: swap(a[j], a[partner[j]])` (partner[j] >= j), wave-parallel
-// and exact.  Position j is final after step j and receives the value position
-// q = partner[j] holds just before step j.  Let V(k) be the original index held by
-// position k just before step k: V(k) = V(link(k)) where link(k) = the last step
-// m < k with partner[m] = k (it moved V(m) into k and nothing wrote k since), or k
-// itself if no step wrote k.  Then the final a'[j] = a[P(j)] with P(j) = V(j) when
-// q = j, else V(pred(j)) with pred(j) = the last step m < j with partner[m] = q,
-// or q if none.  link is an atomicMax; V resolves by pointer jumping (chains are
-// short for random partners); pred is the predecessor among equal targets, found
-// chunk by chunk (64 steps) with a lane mask per target plus the running last
-// writer of earlier chunks.  Scratch: 7 words per stratum (fb_union_bytes).
-__device__ __forceinline__ void lhs_permute(float* strat, const int* partner, int nstrat, int sd, int dimi,
-                                            char* scratch, int lane) {
-  int* link = reinterpret_cast<int*>(scratch);
-  int* val = link + nstrat;
-  int* last = val + nstrat;
-  int* perm = last + nstrat;
-  float* tmp = reinterpret_cast<float*>(perm + nstrat);
-  unsigned long long* cmask = reinterpret_cast<unsigned long long*>(tmp + nstrat + (nstrat & 1));
-  const int* pd = partner + dimi * nstrat;
-  for (int j = lane; j < nstrat; j += kWave) { link[j] = -1; last[j] = -1; cmask[j] = 0ull; }
-  wave_sync();
-  for (int j = lane; j < nstrat; j += kWave) {
-    const int q = pd[j];
-    if (q != j) atomicMax(&link[q], j);
-  }
-  wave_sync();
-  for (int j = lane; j < nstrat; j += kWave) val[j] = j;
-  wave_sync();
-  // pointer jumping: link[j] >= 0 means "V(j) = V(link[j])", unresolved
-  for (;;) {
-    bool pending = false;
-    int nl[4], nv[4];
-    for (int c = 0, j = lane; j < nstrat; j += kWave, c++) {
-      const int p = link[j];
-      nl[c] = p;
-      nv[c] = val[j];
-      if (p >= 0) {
-        const int pp = link[p];
-        if (pp < 0) { nv[c] = val[p]; nl[c] = -1; } else { nl[c] = pp; pending = true; }
-      }
-    }
-    wave_sync();
-    for (int c = 0, j = lane; j < nstrat; j += kWave, c++) { link[j] = nl[c]; val[j] = nv[c]; }
-    wave_sync();
-    if (!__any(pending)) break;
-  }
-  // predecessor among steps with the same target, 64 steps at a time
-  for (int c0 = 0; c0 < nstrat; c0 += kWave) {
-    const int j = c0 + lane;
-    const int q = j < nstrat ? pd[j] : j;
-    const bool mover = j < nstrat && q != j;
-    if (mover) atomicOr(&cmask[q], 1ull << lane);
-    wave_sync();
-    int P = 0;
-    if (j < nstrat) {
-      if (!mover) {
-        P = val[j];
-      } else {
-        const unsigned long long below = cmask[q] & ((1ull << lane) - 1ull);
-        const int pred = below ? c0 + 63 - __builtin_clzll(below) : last[q];
-        P = pred >= 0 ? val[pred] : q;
-      }
-      perm[j] = P;
-    }
-    wave_sync();
-    if (mover) { atomicMax(&last[q], j); cmask[q] = 0ull; }
-    wave_sync();
-  }
-  for (int j = lane; j < nstrat; j += kWave) tmp[j] = strat[sd * perm[j] + dimi];
-  wave_sync();
-  for (int j = lane; j < nstrat; j += kWave) strat[sd * j + dimi] = tmp[j];
-  wave_sync();
-}
-
-// per-wave first-ball scratch after the stratified samples and partners: the
-// rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute
-__host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
-  const size_t a = sizeof(RejLDS), b = (size_t)28 * lhs_floats + 64;
-  return ((a > b ? a : b) + 15) & ~size_t(15);
-}
-
-template <int DIM>
-__device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
-                                          char* scratch, int lane) {
-  constexpr int sd = DIM - 1;
-  const int nstrat = 2 * prm.n_pairs;
-  const int nd = nstrat * sd;
-  Pcg32 ps;
-  ps.seed(seed32(prm.seed, (uint64_t)gidx, 0, 0));
-  const uint64_t s0 = ps.state;
-  const float ome = 1.0f - kFltEps;
-  const float inv = 1.0f / (float)nstrat;
-  for (int idx = lane; idx < nd; idx += kWave) {
-    const int i = sd == 1 ? idx : idx / sd;
-    const uint32_t r = pcg_output(jump_state(prm, s0, idx));
-    const float u = bits_to_float((r >> 9) | 0x3f800000u) - 1.0f;
-    strat[idx] = smin(((float)i + u) * inv, ome);
-  }
-  bool rej = false;
-  for (int idx = lane; idx < nd; idx += kWave) {
-    const int j = sd == 1 ? idx : idx % nstrat;
-    const uint32_t bound = (uint32_t)(nstrat - j);
-    const uint32_t th = (~bound + 1u) % bound;
-    const uint32_t r = pcg_output(jump_state(prm, s0, nd + idx));
-    rej |= r < th;
-    partner[idx] = j + (int)(r % bound);
-  }
-  const bool any_rej = __any(rej);
-  wave_sync();
-  if (any_rej) {  // exact replay of the sequential stream (rare: P ~ n^2 / 2^32)
-    if (lane == 0) {
-      Pcg32 q;
-      q.state = jump_state(prm, s0, nd);
-      for (int i = 0; i < sd; ++i)
-        for (int j = 0; j < nstrat; ++j) partner[i * nstrat + j] = j + (int)q.bounded((uint32_t)(nstrat - j));
-    }
-    wave_sync();
-  }
-  if (nstrat <= 4 * kWave) {
-    for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);
-    return;
-  }
-  if (lane == 0) {  // more strata than lhs_permute's per-lane registers: the serial shuffle
-    for (int i = 0; i < sd; ++i)
-      for (int j = 0; j < nstrat; ++j) {
-        const int other = partner[i * nstrat + j];
-        const float t = strat[sd * j + i];
-        strat[sd * j + i] = strat[sd * other + i];
-        strat[sd * other + i] = t;
-      }
-  }
-  wave_sync();
-}
-
-// The first ball of pair w, both antithetic members (walk_on_stars.h:510-575);
-// member a becomes task t0 + a.
-// Called by every lane of the wave (the 3D source sample is wave-cooperative;
-// 2D keeps the per-lane loop: measured faster for first balls, r1d);
-// lanes with active == false run pair 0's arithmetic for nothing (helping the
-// cooperative sampler) and write and count nothing.
-template <int DIM>
-__device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
-                                            const float* x, float firstR, const float* strat, int64_t gidx,
-                                            bool active, int w, int64_t t0, bool yuk0, uint32_t* iters,
-                                            RejLDS* rejL, int lane) {
-  constexpr int sd = DIM - 1;
-  if (DIM == 2 && !active) return;
-  if (!active) w = 0;
-  uint32_t dummy_iters = 0;
-  if (!active) iters = &dummy_iters;
-  const int64_t T = tk.T;
-  float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[DIM], sourcePt[DIM];
-  for (int k = 0; k < DIM; k++) { boundaryPt[k] = 0.0f; sourcePt[k] = 0.0f; }
-  Pcg32 fs;
-  fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
-  // the first ball (centre x, radius firstR) is the same for both members: its
-  // Bessel constants are evaluated once (identical values either way)
-  Gfn<DIM> g0;
-  g0.init(yuk0, sc.absorption);
-#if WOS_ABL_FB == 1
-  { const bool y = g0.yukawa; g0.yukawa = false; g0.update_ball(x, firstR); g0.yukawa = y;
-    g0.muR = firstR * g0.sqrtLambda; g0.A0 = 0.5f; g0.A1 = 1.5f; g0.B0 = 0.3f; g0.B1 = 0.7f; }
-#else
-  g0.update_ball(x, firstR);
-#endif
-  for (int a = 0; a < prm.n_anti; a++) {
-    const int64_t t = t0 + a;
-    Gfn<DIM> g = g0;
-    float throughput = 1.0f, totalSource = 0.0f, firstSource = 0.0f;
-    float sdir[DIM], bdir[DIM];
-    for (int k = 0; k < DIM; k++) sdir[k] = 0.0f;
-    if (!prm.ignore_source) {
-      if (a == 0) {
-        float dir[DIM];
-        sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-        if constexpr (DIM == 3)
-          sample_volume_wave<DIM>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
-        else
-          sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, iters, true);
-      } else {
-        float sdv[DIM];
-        for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - x[k];
-        for (int k = 0; k < DIM; k++) g.yVol[k] = x[k] - sdv[k];
-        g.r = normv<DIM>(sdv);
-      }
-      float gnorm = g.norm();
-      float contrib = gnorm * source_value<DIM>(sc, g.yVol);
-      totalSource += throughput * contrib;
-      firstSource = contrib;
-      float gr[DIM];
-#if WOS_ABL_FB == 2
-      for (int k = 0; k < DIM; k++) gr[k] = (g.yVol[k] - g.c[k]) * 0.5f;
-#else
-      g.gradient(gr);
-#endif
-      float den = sourcePdf * gnorm;
-      for (int k = 0; k < DIM; k++) sdir[k] = gr[k] / den;
-    }
-    if (a == 0) {
-      const float* u = &strat[sd * (2 * w + 1)];
-      float bd[DIM];
-      if (prm.use_cosine) {
-        if constexpr (DIM == 2) {
-          float u1 = 2.0f * u[0] - 1.0f;
-          bd[0] = u1; bd[1] = __builtin_sqrtf(smax(0.0f, 1.0f - u1 * u1));
-        } else {
-          float u1 = 2.0f * u[0] - 1.0f, u2 = 2.0f * u[1] - 1.0f, dx = 0.0f, dy = 0.0f;
-          if (!(u1 == 0 && u2 == 0)) {
-            float theta, rr;
-            if (__builtin_fabsf(u1) > __builtin_fabsf(u2)) { rr = u1; theta = (float)(0.25 * kPi * (double)(u2 / u1)); }
-            else { rr = u2; theta = (float)(0.5 * kPi * (double)(1.0f - 0.5f * (u1 / u2))); }
-            float sn, cs;
-            fsincos(theta, &sn, &cs);
-            dx = rr * cs; dy = rr * sn;
-          }
-          bd[0] = dx; bd[1] = dy; bd[2] = __builtin_sqrtf(smax(0.0f, 1.0f - (dx * dx + dy * dy)));
-        }
-        if (fs.nextf() < 0.5f) bd[DIM - 1] *= -1.0f;
-        float ct = __builtin_fabsf(bd[DIM - 1]);
-        float pdfc = DIM == 2 ? ct / 2.0f : (float)((double)ct / kPi);
-        boundaryPdf = 0.5f * pdfc;
-        // transformCoordinates (sampling.h:176-203) with n = (1,0[,0])
-        if constexpr (DIM == 2) {
-          const float n0 = 1.0f, n1 = 0.0f;
-          float s0 = n1, s1 = -n0;
-          float q0 = bd[0] * s0 + bd[1] * n0, q1 = bd[0] * s1 + bd[1] * n1;
-          bd[0] = q0; bd[1] = q1;
-        } else {
-          const float n[3] = {1.0f, 0.0f, 0.0f};
-          float sign = __builtin_copysignf(1.0f, n[2]);
-          const float aa = -1.0f / (sign + n[2]);
-          const float b = n[0] * n[1] * aa;
-          float b1[3] = {1.0f + sign * n[0] * n[0] * aa, sign * b, -sign * n[0]};
-          float b2[3] = {b, sign + n[1] * n[1] * aa, -n[1]};
-          float q[3];
-          for (int k = 0; k < 3; k++) q[k] = bd[0] * b1[k] + bd[1] * b2[k] + bd[2] * n[k];
-          for (int k = 0; k < 3; k++) bd[k] = q[k];
-        }
-      } else {
-        sample_unit_sphere<DIM>(u, bd);
-        boundaryPdf = pdf_sphere_uniform<DIM>(1.0f);
-      }
-      for (int k = 0; k < DIM; k++) { g.ySurf[k] = g.c[k] + g.R * bd[k]; boundaryPt[k] = g.ySurf[k]; }
-    } else {
-      float bd[DIM];
-      for (int k = 0; k < DIM; k++) bd[k] = boundaryPt[k] - x[k];
-      for (int k = 0; k < DIM; k++) g.ySurf[k] = x[k] - bd[k];
-    }
-    throughput *= g.poisson_kernel() / boundaryPdf;
-    {
-      float pg[DIM];
-      g.poisson_kernel_gradient(pg);
-      float den = boundaryPdf * throughput;
-      for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
-    }
-    if (!active) continue;
-#if WOS_ABL_FB == 5
-    if (firstSource == 12345.0f) tk.first[t] = throughput + totalSource + bdir[0] + sdir[0];
-    continue;
-#endif
-    tk.first[t] = firstSource;
-    for (int k = 0; k < DIM; k++) {
-      tk.bdir[k * T + t] = bdir[k];
-      tk.sdir[k * T + t] = sdir[k];
-      tk.pt[k * T + t] = g.ySurf[k];
-    }
-    tk.thr[t] = throughput;
-    tk.tsrc[t] = totalSource;
-    tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
-  }
-}
-
-// LDS image: prims | silhouettes | prim groups | silhouette groups (each block 16-B aligned)
-template <int DIM, bool GG>
-__device__ __forceinline__ LGeom geometry_view(const DevScene& sc, float* smem, bool with_sil, bool copy) {
-  constexpr int PS = Layout<DIM>::prim, SS = Layout<DIM>::sil;
-  const int primN = sc.n_prims * PS, silN = sc.n_sil * SS;
-  const int primAl = (primN + 3) & ~3, silAl = (silN + 3) & ~3;
-  const int pgN = sc.n_pgroups * kGroupStride, sgN = sc.n_sgroups * kSGroupStride;
-  LGeom G;
-  if constexpr (GG) {  // too large for LDS: the same records, read through L2
-    G.prim = sc.prim;
-    G.sil = sc.sil;
-    G.pgroup = sc.pgroup;
-    G.sgroup = sc.sgroup;
-    G.sgrid = with_sil ? sc.sgrid : nullptr;
-    G.sgrid_off_words = sc.sgrid_off_words;
-    G.dprim = sc.dprim;
-    G.dgroup = sc.dgroup;
-    return G;
-  }
-  G.prim = smem;
-  G.sil = smem + primAl;
-  G.pgroup = smem + primAl + silAl;
-  G.sgroup = G.pgroup + pgN;
-  uint32_t* gw = reinterpret_cast<uint32_t*>(smem + primAl + silAl + pgN + sgN);
-  G.sgrid = (with_sil && sc.sgrid != nullptr) ? gw : nullptr;
-  G.sgrid_off_words = sc.sgrid_off_words;
-  const int sgridAl = sc.sgrid != nullptr ? ((sc.sgrid_words + 3) & ~3) : 0;
-  const int dpN = sc.n_dprims * PS, dpAl = (dpN + 3) & ~3, dgN = sc.n_dgroups * kGroupStride;
-  float* dbase = smem + primAl + silAl + pgN + sgN + sgridAl;
-  G.dprim = with_sil ? dbase : sc.dprim;
-  G.dgroup = with_sil ? dbase + dpAl : sc.dgroup;
-  if (!copy) return G;
-  for (int i = threadIdx.x; i < primN; i += kBlock) smem[i] = sc.prim[i];
-  if (with_sil) {
-    for (int i = threadIdx.x; i < silN; i += kBlock) smem[primAl + i] = sc.sil[i];
-    for (int i = threadIdx.x; i < pgN; i += kBlock) smem[primAl + silAl + i] = sc.pgroup[i];
-    for (int i = threadIdx.x; i < sgN; i += kBlock) smem[primAl + silAl + pgN + i] = sc.sgroup[i];
-    if (sc.sgrid != nullptr)
-      for (int i = threadIdx.x; i < sc.sgrid_words; i += kBlock) gw[i] = sc.sgrid[i];
-    for (int i = threadIdx.x; i < dpN; i += kBlock) dbase[i] = sc.dprim[i];
-    for (int i = threadIdx.x; i < dgN; i += kBlock) dbase[dpAl + i] = sc.dgroup[i];
-  }
-  return G;
-}
-
-template <int DIM, bool GG>
-__device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem, bool with_sil) {
-  return geometry_view<DIM, GG>(sc, smem, with_sil, true);
-}
-
-// Kernel parameters re-read inside a loop: the view goes through an opaque copy of
-// the pointer to the kernarg block, so every use in an iteration is a scalar load
-// (scalar-cache hit) instead of a value held in SGPRs for the whole kernel.  The
-// walk kernel's loop-invariant scene / parameter / task fields and the constants
-// hoisted next to them otherwise overflow the SGPR file, whose spills into VGPR
-// lanes then push the VGPRs into scratch.
-#ifndef WOS_KVIEW
-#define WOS_KVIEW 1
-#endif
-// The walk kernel's parameters as they lie in the kernarg segment (the ABI lays the
-// arguments out like the members of this struct: declaration order, natural alignment).
-struct WalkKernArgs {
-  DevScene sc;
-  DevParams prm;
-  DevTasks tk;
-};
-using KernArgsPtr = const __attribute__((address_space(4))) WalkKernArgs*;
-__device__ __forceinline__ KernArgsPtr kernargs_opaque() {
-  KernArgsPtr q = (KernArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
-  if (WOS_KVIEW) asm volatile("" : "+s"(q));
-  return q;
-}
-
-__device__ __forceinline__ void flush_counter(unsigned long long* counters, int slot, uint32_t v, int lane) {
-  unsigned long long s = v;
-  for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  if (lane == 0 && s) atomicAdd(&counters[slot], s);
-}
-
-// per-point state bits written by the first-ball kernel
-enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
-
-// ---- kernel 1: point setup + first balls ----------------------------------
-#ifndef WOS_PT_GRAB
-#define WOS_PT_GRAB 2
-#endif
-constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the first-ball kernel
-#ifndef WOS_FB_WAVES_PER_EU
-#define WOS_FB_WAVES_PER_EU 1
-#endif
-template <int DIM, bool GG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
-    const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
-    const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
-    int lhs_floats) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ uint32_t s_hist[kCostBuckets];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-  const LGeom Gfb = stage_geometry<DIM, GG>(sc, smem, false);
-  stage_rej_jump(prm);
-  if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
-#endif
-  __syncthreads();
-  const float* Lprim = Gfb.prim;
-  float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
-  int* partner = (int*)(strat + lhs_floats);
-  RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);
-
-  uint32_t c_iters = 0, c_pts = 0;
-  const int npairs = prm.n_pairs;
-  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
-
-  // point queue, one point ahead: the next index is taken (and its coordinates
-  // loaded) while the current point is processed, so neither the queue atomic nor
-  // the point load sits on a point's critical path
-  // Points are taken kPtGrab at a time (one queue atomic per chunk: a single-address
-  // atomic per point serialises at ~13 ns, which had bounded the whole kernel);
-  // kPtGrab = 0: static round-robin over the waves of the grid.
-  const unsigned int nwaves = gridDim.x * (kBlock / kWave);
-  const unsigned int wave_id = blockIdx.x * (kBlock / kWave) + wave;
-  unsigned int idx = 0, cend = 0;
-  if (kPtGrab == 0) {
-    idx = wave_id;
-  } else {
-    if (lane == 0) idx = atomicAdd(work, kPtGrab);
-    idx = __shfl(idx, 0);
-    cend = idx + kPtGrab;
-  }
-  float xn[DIM];
-  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
-  for (;;) {
-    if ((int64_t)idx >= n) break;
-    const int64_t gidx = base + (int64_t)idx * stride;
-    float x[DIM];
-    for (int k = 0; k < DIM; k++) x[k] = xn[k];
-    const bool grab = kPtGrab != 0 && idx + 1 >= cend;  // wave-uniform
-    unsigned int nidx_l0 = 0;
-    if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
-
-    // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
-    DIAG_T0(t_fb0);
-    float nDist = kFltMax, nSigned = kFltMax;
-    if (sc.n_prims > 0) {
-      Closest c = closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
-      nDist = c.d;
-      nSigned = signed_dist<DIM>(sc.paux, c, x);
-    }
-    float dDist, dSigned;
-    if (sc.n_dprims > 0) {
-      Closest c = closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
-      dDist = c.d;
-      dSigned = signed_dist<DIM>(sc.dpaux, c, x);
-    } else {
-      dDist = dSigned = bbox_far_dist<DIM>(sc, x);
-    }
-    const bool inside = !sc.watertight ? true
-                        : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
-    const bool estimate = inside || sc.double_sided;
-    if (lane == 0) {
-      // masked outputs (grid.h:155-179, 207-237)
-      const float mask = prm.boundary_distance_mask;
-      const bool maskP = __builtin_fabsf(nDist) < mask;
-      const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
-      // cost bucket for the walk-queue order: walks from points close to the boundary
-      // (small first ball) run longest, so they are queued first (longest-first
-      // scheduling shortens the tail of the persistent walk kernel)
-      const float bd = smin(dDist, nDist);
-      int bucket = 0;
-      if (estimate) {
-        const float l2 = __builtin_amdgcn_logf(smax(bd, 1e-9f));  // log2
-        bucket = (int)sclamp((int)(-2.0f * l2) + 8, 1, kCostBuckets - 1);
-      }
-      tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
-      atomicAdd(&s_hist[bucket], 1u);
-    }
-    // the next point: its index (the atomic has returned by now) and coordinates
-    unsigned int nidx, ncend = cend;
-    if (kPtGrab == 0) {
-      nidx = idx + nwaves;
-    } else if (grab) {
-      nidx = (unsigned int)__shfl((int)nidx_l0, 0);
-      ncend = nidx + kPtGrab;
-    } else {
-      nidx = idx + 1;
-    }
-    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
-    if (!estimate) { idx = nidx; cend = ncend; continue; }
-    c_pts += lane == 0;
-    DIAG_ADD(D_FB_SETUP, t_fb0);
-    DIAG_COUNT(D_FB_PTS, 1);
-    DIAG_T0(t_fb1);
-#if WOS_ABL_FB == 3
-    for (int i = lane; i < 2 * npairs * (DIM - 1); i += kWave) strat[i] = (i + 0.5f) / (2 * npairs * (DIM - 1));
-    wave_sync();
-#else
-    build_lhs<DIM>(prm, gidx, strat, partner, reinterpret_cast<char*>(rejL), lane);
-#endif
-    DIAG_ADD(D_FB_LHS, t_fb1);
-    DIAG_T0(t_fb2);
-    const float firstR = 0.99f * smin(dDist, nDist);
-    for (int w0 = 0; w0 < npairs; w0 += kWave) {
-      const int w = w0 + lane;
-      first_balls<DIM>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
-                       (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
-    }
-    DIAG_ADD(D_FB_BALLS, t_fb2);
-    DIAG_ADD(D_FB_TOTAL, t_fb0);
-    DIAG_MAX(D_FB_MAX, __builtin_amdgcn_s_memtime() - t_fb0);
-    wave_sync();
-    idx = nidx;
-    cend = ncend;
-  }
-  flush_counter(counters, C_ITERS, c_iters, lane);
-  flush_counter(counters, C_PTS, c_pts, lane);
-  __syncthreads();
-  if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) {
-    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-  }
-#endif
-}
 
 // ---- walk-queue order: bucket offsets (descending cost) and the permutation ---
 __global__ void wos_lpt_offsets_kernel(uint32_t* __restrict__ hist) {
@@ -2597,351 +35,6 @@ __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk,
     base[threadIdx.x] = atomicAdd(&tk.hist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
   __syncthreads();
   if (i < n) tk.perm[base[b] + local] = (uint32_t)i;
-}
-
-// ---- kernel 2: walks ---------------------------------------------------------
-#ifndef WOS_TASK_GRAB
-#define WOS_TASK_GRAB 128
-#endif
-constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
-
-// experiments (0 = off): WOS_PRIO=n raises the wave priority with the age of its
-// oldest walk (steps / n); WOS_DRAIN=n stops handing tasks to a wave whose oldest
-// walk is n steps old, so the long walks run in light waves
-#ifndef WOS_PRIO
-#define WOS_PRIO 0
-#endif
-// 1: the staged ring also carries each task's record (pt, throughput, source total,
-// Dirichlet distance), loaded one iteration ahead; 0 (default, measured faster on
-// every config: the staged records cost registers the step needs): only the task
-// index and its point's state are staged, the record is loaded at hand-out
-#ifndef WOS_TASK_RING
-#define WOS_TASK_RING 0
-#endif
-#ifndef WOS_DRAIN
-#define WOS_DRAIN 0
-#endif
-// 4 waves per SIMD (<= 128 VGPRs): latency hiding for the walk's long dependent chains
-#ifndef WOS_WALK_WAVES_PER_EU
-#define WOS_WALK_WAVES_PER_EU 4
-#endif
-template <int DIM, bool GG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK_WAVES_PER_EU))) void wos_walk_kernel(
-    const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
-    unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ unsigned int s_ctr[C_NUM];
-  const DevScene& sc = sc_arg;
-  const DevParams& prm = prm_arg;
-  const DevTasks& tk = tk_arg;
-  const int lane = threadIdx.x & (kWave - 1);
-  const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
-  stage_rej_jump(prm);
-  // per-wave scratch shared by the star and ray queries (used one after the other)
-  const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // wave-uniform: SGPR address
-  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();
-  StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
-  RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
-  RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
-  (void)rayL;
-  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
-#endif
-  __syncthreads();
-
-  const uint32_t T = (uint32_t)tk.T;
-  const uint32_t wpp = (uint32_t)tk.wpp;
-  // x / wpp as a shift when walks-per-point is a power of two (every shipped config)
-  const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
-  auto divw = [&](uint32_t x) -> uint32_t { return wsh >= 0 ? x >> wsh : x / wpp; };
-  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
-  uint32_t c_iters = 0;
-
-  DIAG_T0(t_wave);
-  // ---- task supply: a window [wq, we) of the global queue (wave-uniform; lane i
-  // holds perm[wp0 + i]) feeds a 64-slot ring of staged tasks, one per lane: ring
-  // position (lane - head) & 63, positions [0, S) valid.  The ring is refilled at
-  // the end of every iteration, so the loads of a staged task (its record and its
-  // point's state) are in flight during a whole step and a lane that finishes a
-  // walk starts the next one from registers (cross-lane shuffles) instead of a
-  // chain of dependent global loads.
-  const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;  // <= 64 points per window
-  uint32_t wq = 0, we = 0, wp0 = 0, wperm = 0;
-  bool exhausted = false;
-  int head = 0, S = 0;
-  uint32_t s_t = 0, s_ok = 0;  // staged task index, its point is estimated
-  float s_pt[DIM], s_thr = 0.0f, s_tsrc = 0.0f, s_dd = 0.0f;
-  for (int k = 0; k < DIM; k++) s_pt[k] = 0.0f;
-  auto refill = [&](const DevTasks& tk) {
-    while (S < kWave && !exhausted) {
-      if (wq >= we) {
-        unsigned int c = 0;
-        if (lane == 0) c = atomicAdd(tqueue, G_win);
-        c = __shfl(c, 0);
-        if (c >= T) { exhausted = true; break; }
-        wq = c;
-        we = (T - c) < G_win ? T : c + G_win;
-        wp0 = divw(c);
-        const uint32_t np = divw(we - 1) - wp0 + 1;
-        wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
-      }
-      const int avail = (int)(we - wq);
-      const int take = (kWave - S) < avail ? (kWave - S) : avail;
-      const int pos = ((lane - head) & (kWave - 1)) - S;
-      const bool mine = pos >= 0 && pos < take;
-      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = divw(q);
-      const uint32_t pidx = (uint32_t)__shfl((int)wperm, (int)(qp - wp0));  // queue position -> permuted point
-      if (mine) {
-        s_t = pidx * wpp + (q - qp * wpp);
-        s_ok = tk.pstate[pidx] & kPtEstimate;
-        if (WOS_TASK_RING) {
-          for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
-          s_thr = tk.thr[s_t];
-          s_tsrc = tk.tsrc[s_t];
-          s_dd = tk.dd[s_t];
-        }
-      }
-      S += take;
-      wq += (uint32_t)take;
-    }
-  };
-  refill(tk);
-  int64_t t = -1;           // this lane's task
-  int wmax = 0;             // longest live walk of the wave (steps), wave-uniform
-  WalkState<DIM> st;
-  Gfn<DIM> g;
-  Pcg32 ws;
-  float ddist = 0.0f;
-  uint32_t wsteps = 0;
-
-  for (;;) {
-    DIAG_T0(t_loop);
-    // per-iteration views of the kernel parameters and of the staged geometry (see kview)
-    KernArgsPtr ka = kernargs_opaque();
-    const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
-    const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
-    const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
-    const LGeom G = WOS_KVIEW ? geometry_view<DIM, GG>(sc, smem, true, false) : G0;
-    // ---- hand staged tasks to idle lanes (uniform control flow)
-    {
-      const uint64_t need = __ballot(t < 0);
-      if (need != 0 && S > 0 && (WOS_DRAIN == 0 || wmax < WOS_DRAIN)) {
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-        const int k = __popcll(need);
-        const int take = k < S ? k : S;
-        const int src = (head + (rank < take ? rank : 0)) & (kWave - 1);
-        const uint32_t v_t = (uint32_t)__shfl((int)s_t, src);
-        const uint32_t v_ok = (uint32_t)__shfl((int)s_ok, src);
-        float v_pt[DIM], v_thr = 0.0f, v_tsrc = 0.0f, v_dd = 0.0f;
-        if (WOS_TASK_RING) {
-          for (int kk = 0; kk < DIM; kk++) v_pt[kk] = __shfl(s_pt[kk], src);
-          v_thr = __shfl(s_thr, src);
-          v_tsrc = __shfl(s_tsrc, src);
-          v_dd = __shfl(s_dd, src);
-        } else if (t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
-          for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];
-          v_thr = tk.thr[v_t];
-          v_tsrc = tk.tsrc[v_t];
-          v_dd = tk.dd[v_t];
-        }
-        if (t < 0 && rank < take) {
-          t = (int64_t)v_t;
-          if (!v_ok) {  // point outside the domain: no walks
-            tk.code[t] = 0u;
-            t = -1;
-          } else {
-            const uint32_t pidx = divw(v_t);
-            const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
-            for (int kk = 0; kk < DIM; kk++) { st.pt[kk] = v_pt[kk]; st.n[kk] = 0.0f; st.prevDir[kk] = 0.0f; }
-            // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
-            // and every step rewrites them before that can happen
-            st.prevDist = 0.0f;
-            st.throughput = v_thr;
-            st.onNeumann = false;
-            st.walkLength = 0;
-            st.totalNeumann = 0.0f;
-            st.totalSource = v_tsrc;
-            ddist = v_dd;
-            g.init(yuk0, sc.absorption);
-            ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
-            wsteps = 1;  // the first ball
-          }
-        }
-        head = (head + take) & (kWave - 1);
-        S -= take;
-      }
-    }
-    if (__ballot(t >= 0) == 0) {
-      if (S == 0 && exhausted) break;  // queue drained and every lane idle
-      refill(tk);
-      continue;
-    }
-#if WOS_PRIO || WOS_DRAIN
-    {
-      int wl = t >= 0 ? st.walkLength : 0;
-      for (int off = kWave / 2; off > 0; off >>= 1) wl = smax(wl, __shfl_xor(wl, off));
-      wmax = __builtin_amdgcn_readfirstlane(wl);
-    }
-#endif
-#if WOS_PRIO
-    if (wmax >= 3 * WOS_PRIO) __builtin_amdgcn_s_setprio(3);
-    else if (wmax >= 2 * WOS_PRIO) __builtin_amdgcn_s_setprio(2);
-    else if (wmax >= WOS_PRIO) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#endif
-
-    DIAG_COUNT(D_ITERS, 1);
-    DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
-    DIAG_T0(t_step);
-    int code = -1;
-    bool flip = false, query = false;
-    if (t >= 0) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query);
-    DIAG_T0(t_star);
-    const float starQ = star_radius_wave<DIM>(G, sc, prm, t >= 0 && code < 0 && query, st.pt, ddist, flip,
-                                              starL, lane);
-    DIAG_ADD(D_STAR, t_star);
-    const bool live = t >= 0 && code < 0;
-    float dir[DIM], org[DIM], starR = 0.0f;
-    for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
-    DIAG_T0(t_mid);
-    if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org);
-    DIAG_ADD(D_MID, t_mid);
-    Hit ip;
-    DIAG_T0(t_ray);
-#if WOS_RAY_WAVE
-    const bool hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM>(G, sc, live, org, dir, starR, &ip, rayL, lane);
-#else
-    const bool hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 &&
-                     ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
-#endif
-    DIAG_ADD(D_RAY, t_ray);
-    DIAG_T0(t_end);
-    if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
-    DIAG_ADD(D_END, t_end);
-    float sp[DIM], pdf_unused;
-    for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
-    DIAG_T0(t_smp);
-    if (!prm.ignore_source)
-      sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, &c_iters, false, rejL, lane);
-    DIAG_ADD(D_SAMPLE, t_smp);
-    DIAG_T0(t_tail);
-    if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
-    DIAG_ADD(D_TAIL, t_tail);
-    DIAG_ADD(D_STEP, t_step);
-    if (t >= 0 && code >= 0) {
-      const bool recorded = code == WC_DIRICHLET || code == WC_RR;
-      if (recorded) {
-        const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
-        tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
-      }
-      tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
-      DIAG_MAX(D_WMAXLEN, wsteps);
-      atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
-      atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL],
-                1u);
-      t = -1;
-    }
-    refill(tk);
-    DIAG_ADD(D_LOOP, t_loop);
-  }
-
-  DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
-  flush_counter(counters, C_ITERS, c_iters, lane);
-  __syncthreads();
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) {
-    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-  }
-#endif
-  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
-    unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
-    if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
-  }
-}
-
-// ---- kernel 3: statistics + outputs ----------------------------------------
-// One thread per point, kFoldPoints points per block.  The records of the
-// block's points are contiguous (point-major tasks), so they are staged through
-// LDS in chunks of kFoldChunk records per point with coalesced 64-B loads, then
-// every thread folds its own point's chunk in walk order.
-constexpr int kFoldPoints = 128, kFoldChunk = 16;
-
-template <int DIM>
-__global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
-                                                               float* __restrict__ p_out,
-                                                               float* __restrict__ g_out,
-                                                               int32_t* __restrict__ nest_out,
-                                                               int32_t* __restrict__ steps_out) {
-  constexpr int NF = 3 + 2 * DIM;  // code | total | first | bdir[DIM] | sdir[DIM]
-  constexpr int LD = kFoldChunk + 1;
-  __shared__ float lds[NF][kFoldPoints][LD];
-  const int tid = threadIdx.x;
-  const int64_t p0 = (int64_t)blockIdx.x * kFoldPoints;
-  const int nb = (int)((n - p0) < kFoldPoints ? (n - p0) : kFoldPoints);
-  const int64_t i = p0 + tid;
-  const int64_t T = tk.T;
-  const int wpp = tk.wpp;
-  const int ps = tid < nb ? tk.pstate[i] : 0;
-  const bool estimate = ps & kPtEstimate;
-  float mean[DIM + 1];
-  for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
-  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
-  int sN = 0;
-  uint32_t steps = 0;
-  for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
-    const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
-    for (int e = tid; e < nb * kFoldChunk; e += kFoldPoints) {
-      const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
-      if (j >= cnt) continue;
-      const int64_t t = (p0 + pp) * wpp + c0 + j;
-      lds[0][pp][j] = __uint_as_float(tk.code[t]);
-      lds[1][pp][j] = tk.total[t];
-      lds[2][pp][j] = tk.first[t];
-      for (int k = 0; k < DIM; k++) {
-        lds[3 + k][pp][j] = tk.bdir[k * T + t];
-        lds[3 + DIM + k][pp][j] = tk.sdir[k * T + t];
-      }
-    }
-    __syncthreads();
-    if (estimate) {
-      for (int j = 0; j < cnt; j++) {
-        const int r = c0 + j;
-        if (r % prm.n_anti == 0) {  // a new antithetic pair: control variates from the walks before it
-          cvb = mean[0];
-          cvs = sFirst / (float)(sN > 1 ? sN : 1);
-          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
-        }
-        const uint32_t code = __float_as_uint(lds[0][tid][j]);
-        steps += code >> 1;
-        if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
-        const float total = lds[1][tid][j];
-        const float first = lds[2][tid][j];
-        sN += 1;
-        const float fN = (float)sN;
-        {
-          const float delta = total - mean[0];
-          mean[0] += delta / fN;
-        }
-        for (int k = 0; k < DIM; k++) {
-          const float be = (total - first - cvb) * lds[3 + k][tid][j];
-          const float se = (first - cvs) * lds[3 + DIM + k][tid][j];
-          const float delta = (be + se) - mean[k + 1];
-          mean[k + 1] += delta / fN;
-        }
-        sFirst += first;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid >= nb) return;
-  const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
-  p_out[i] = maskP ? 0.0f : mean[0];
-  for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];
-  if (nest_out) nest_out[i] = sN;
-  if (steps_out) steps_out[i] = (int32_t)steps;
 }
 
 template __global__ void wos_first_ball_kernel<2, false>(const DevScene, const DevParams, const float*, int64_t,
@@ -3120,3 +213,4 @@ hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t
 }
 
 }  // namespace wos
+

@@ -32,4 +32,18 @@ size_t walk_wave_lds_bytes(int dim);
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
+
+// boundary value caching (wos_bvc.hip), 2D
+hipError_t launch_bvc_point_info(const DevScene& sc, const float* pts, int64_t n, float* dd, float* nd,
+                                 int32_t* inside, float* src, hipStream_t s);
+hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const float* bpt, const float* bnrm,
+                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, hipStream_t s);
+hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
+                               int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
+                               size_t shmem, int geom_floats, hipStream_t s);
+hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks);
+hipError_t launch_bvc_fold(const DevTasks& tk, int64_t nb, float* sol, int32_t* nest, hipStream_t s);
+hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const float* edd, const float* end_,
+                            const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
+                            float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s);
 }  // namespace wos

@@ -119,6 +119,13 @@ struct DevTasks {
   uint32_t* hist;   // [2 * kCostBuckets] bucket counts, then running bucket offsets
   int64_t T;
   int32_t wpp;      // walks per point = n_pairs * n_anti
+  // Boundary-start walks (estimateSolution, walk_on_stars.h:353-464; boundary value
+  // caching): per task the start normal [DIM][T], the first sphere radius [T] and
+  // bit 0 "starts on the Neumann boundary" [T].  They alias the first-ball record
+  // arrays (bdir, first, sdir), which such walks do not use; nullptr otherwise.
+  float* n0;
+  float* r0;
+  uint32_t* sflags;
 };
 
 constexpr int task_floats(int dim) { return 3 * dim + 6; }

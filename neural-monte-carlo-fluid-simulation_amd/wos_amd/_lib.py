@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 4  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 5  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
@@ -58,6 +58,14 @@ class SolverParams(C.Structure):
     ]
 
 
+class BvcParams(C.Structure):
+    _fields_ = [("n_walks_solution", C.c_int32), ("n_walks_gradient", C.c_int32),
+                ("boundary_cache_size", C.c_int32), ("domain_cache_size", C.c_int32),
+                ("grid_res", C.c_int32), ("use_finite_differences", C.c_int32),
+                ("normal_offset", C.c_float), ("radius_clamp", C.c_float),
+                ("kernel_regularization", C.c_float)]
+
+
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped", "walks_max_length",
@@ -74,7 +82,7 @@ class Stats(C.Structure):
 EXPORTS = (
     "wos_load_obj", "wos_mesh_free", "wos_scene_create", "wos_scene_destroy",
     "wos_scene_get_info", "wos_scene_set_source", "wos_release_caches", "wos_default_params", "wos_solve",
-    "wos_solve_stats",
+    "wos_solve_stats", "wos_default_bvc_params", "wos_bvc",
     "wos_selftest_math", "wos_last_error", "wos_abi_version", "wos_device_count",
 )
 
@@ -111,6 +119,11 @@ def load():
                             C.POINTER(Stats), C.c_void_p, C.c_uint32]
     L.wos_solve_stats.restype = C.c_int
     L.wos_solve_stats.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(Stats)]
+    L.wos_default_bvc_params.restype = None
+    L.wos_default_bvc_params.argtypes = [C.POINTER(BvcParams)]
+    L.wos_bvc.restype = C.c_int
+    L.wos_bvc.argtypes = [C.c_void_p, C.POINTER(SolverParams), C.POINTER(BvcParams), C.c_void_p, C.c_void_p,
+                          C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(Stats)]
     L.wos_selftest_math.restype = C.c_int
     L.wos_selftest_math.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
     L.wos_last_error.restype = C.c_char_p

@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import SceneDesc, SceneInfo, SolverParams, Stats, WosError, check
+from ._lib import BvcParams, SceneDesc, SceneInfo, SolverParams, Stats, WosError, check
 
 _DEFAULT_SEED = 0x5EED0001
 
@@ -63,6 +63,28 @@ def solver_params(solver=None, output=None, seed=None):
     p.ignore_source = int(bool(s.get("ignoreSource", False)))
     p.seed = int(seed if seed is not None else s.get("seed", _DEFAULT_SEED)) & 0xFFFFFFFFFFFFFFFF
     return p
+
+
+def bvc_params(solver=None, output=None):
+    """The boundary-value-caching keys runBoundaryValueCaching reads (demo.cpp:269-290):
+    same names and defaults; output.gridRes is required."""
+    s = dict(solver or {})
+    o = dict(output or {})
+    if "gridRes" not in o:
+        raise KeyError("Missing required setting: gridRes")
+    b = BvcParams()
+    _lib.load().wos_default_bvc_params(C.byref(b))
+    eps = _get_opt(s, "epsilonShell", 1e-3, float)
+    b.n_walks_solution = _get_opt(s, "nWalksForCachedSolutionEstimates", 128, int)
+    b.n_walks_gradient = _get_opt(s, "nWalksForCachedGradientEstimates", 640, int)
+    b.boundary_cache_size = _get_opt(s, "boundaryCacheSize", 1024, int)
+    b.domain_cache_size = _get_opt(s, "domainCacheSize", 1024, int)
+    b.grid_res = int(o["gridRes"])
+    b.use_finite_differences = int(bool(s.get("useFiniteDifferencesForBoundaryDerivatives", False)))
+    b.normal_offset = _get_opt(s, "normalOffsetForCachedDirichletSamples", 5.0 * eps, float)
+    b.radius_clamp = _get_opt(s, "radiusClampForKernels", 1e-3, float)
+    b.kernel_regularization = _get_opt(s, "regularizationForKernels", 0.0, float)
+    return b
 
 
 def _is_torch(x):
@@ -221,6 +243,34 @@ class WosScene:
         if counts:
             out = out + (ne, sp)
         return out
+
+    def bvc(self, params=None, bvc=None, samples=True):
+        """Boundary value caching (wos_bvc; the reference's bvc, demo.cpp:265-363) on this
+        2D all-Neumann scene.  Returns (solution [g, g], grad [g, g, 2], info) on the
+        evaluation grid (index [i, j] = point (i/g, j/g) of the bounding box, masked as
+        saveEvaluationGrid masks); info holds the sample counts, the cached samples
+        ([k, 8]: x y nx ny pdf value normalDerivative kind) and the stats."""
+        L = _lib.load()
+        params = params if params is not None else solver_params()
+        if bvc is None:
+            raise WosError("bvc parameters required (engine.bvc_params(solver, output))")
+        g = int(bvc.grid_res)
+        sol = np.empty(g * g, np.float32)
+        grad = np.empty(g * g * 2, np.float32)
+        counts = np.zeros(4, np.int64)
+        st = Stats()
+        cap = 0
+        buf = None
+        if samples:
+            cap = 2 * int(bvc.boundary_cache_size) + 4 * int(bvc.domain_cache_size) + 16
+            buf = np.empty(cap * 8, np.float32)
+        check(L.wos_bvc(self._h, C.byref(params), C.byref(bvc), sol.ctypes.data, grad.ctypes.data,
+                        buf.ctypes.data if samples else None, cap, counts.ctypes.data, C.byref(st)), "wos_bvc")
+        info = {"counts": {"boundary": int(counts[0]), "boundary_aligned": int(counts[1]), "domain": int(counts[2]),
+                           "total": int(counts[3])}, "stats": st.as_dict()}
+        if samples:
+            info["samples"] = buf[:int(counts[3]) * 8].reshape(-1, 8).copy()
+        return sol.reshape(g, g), grad.reshape(g, g, 2), info
 
     def solve_stats(self, ticket):
         """Statistics of an enqueued solve (wos_solve_stats); blocks until it has finished."""

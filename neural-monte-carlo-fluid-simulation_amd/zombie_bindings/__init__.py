@@ -14,6 +14,8 @@ Differences, all deliberate (DESIGN.md "Boundary"):
 Like the reference, 2D and 3D wost solve at the query points they are given
 (createSolutionGrid(..., pts), zombie/demo/grid.h:69-102; createSolutionGrid_3d,
 zombie3d/demo/grid.h:105-146 iterates the passed points).
+bvc (boundary value caching) runs on the GPU too (2D all-Neumann scenes, the only
+kind the reference builds).
 Extensions: numpy / torch inputs are accepted without nested-list conversion, a
 torch CUDA tensor of points stays on the GPU; optional scene key
 "dirichletBoundary" (OBJ) + "dirichletValue" adds Dirichlet geometry.
@@ -116,7 +118,51 @@ def wost(scene, solverConfig, outputConfig, pts, return_numpy=False):
     return x.tolist(), p.tolist(), g.tolist()
 
 
-def bvc(scene, solverConfig, outputConfig):
-    """Boundary value caching (demo.cpp:265-363) is exported by the reference but never
-    called by the time-stepper; it is out of scope for this engine (SURVEY.md §2 #7)."""
-    raise NotImplementedError("bvc is not provided by the MI355X engine (unused by src/2d, src/3d)")
+def _write_image(path, img):
+    """Image<3>::write (image.h:97-103, 173-216) of a gray image replicated over three
+    channels: .pfm little-endian 'PF' with the rows written bottom to top, anything else
+    PNG (8-bit, clamp(int(v * 255), 0, 255)).  Parent directories are created as
+    writeSolution does (grid.h:16-17)."""
+    import struct
+    import zlib
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    h, w = img.shape
+    rgb = np.repeat(np.asarray(img, np.float32)[..., None], 3, axis=2)
+    if path.lower().endswith(".pfm"):
+        with open(path, "wb") as f:
+            f.write(b"PF\n%d %d\n-1\n" % (w, h))
+            f.write(np.ascontiguousarray(rgb[::-1], "<f4").tobytes())
+        return
+    v = np.clip((rgb * 255.0).astype(np.int64), 0, 255).astype(np.uint8)
+    raw = b"".join(b"\x00" + v[r].tobytes() for r in range(h))
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)) +
+                chunk(b"IDAT", zlib.compress(raw)) + chunk(b"IEND", b""))
+
+
+def bvc(scene, solverConfig, outputConfig, return_arrays=False):
+    """runBoundaryValueCaching (demo.cpp:265-363): boundary and domain samples, walk-on-stars
+    estimates at the boundary samples, splatted onto the gridRes x gridRes evaluation grid
+    (GPU: libwos_hip.so wos_bvc), then saveEvaluationGrid (grid.h:370-414): the masked
+    solution is written to output["solutionFile"] (default "solution.pfm").  Returns None
+    like the reference; return_arrays=True (extension) returns (solution [g, g] indexed
+    [i, j] for grid point (i, j), grad [g, g, 2], info with the cached samples and stats).
+    The colormapped and debug images of writeSolution are not written."""
+    _required(outputConfig, "gridRes")
+    if scene.dim != 2:
+        raise ValueError("bvc is 2D (the reference's zombie3d module exports no bvc)")
+    params = _engine.solver_params(solverConfig, outputConfig)
+    bp = _engine.bvc_params(solverConfig, outputConfig)
+    sol, grad, info = scene._scene.bvc(params, bp)
+    scene.last_stats = info["stats"]
+    # Image<3> solution(gridRes, gridRes), solution->get(j, i) = point (i, j) (grid.h:384-409)
+    _write_image(outputConfig.get("solutionFile", "solution.pfm"), sol.T)
+    if return_arrays:
+        return sol, grad, info
+    return None

@@ -1085,13 +1085,19 @@ static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float 
     }
 }
 
-static int walk(const scene_t *sc, const oracle_params *prm, float dirichletDist,
+/* walk() (walk_on_stars.h:135-329); first_r > 0: the first step's sphere radius is
+ * given (firstSphereRadius of estimateSolution, :148-150) -- no flip, no query */
+static int walk(const scene_t *sc, const oracle_params *prm, float dirichletDist, float first_r,
                 pcg_t *smp, gfn_t *g, wstate_t *st, wcount_t *cnt)
 {
     const int dim = sc->dim;
+    int firstStep = 1;
     while (dirichletDist > prm->epsilon_shell) {
         float starRadius;
         int flip = 0;
+        if (firstStep && first_r > 0.0f) {
+            starRadius = first_r;
+        } else {
         if (sc->double_sided && st->onNeumann) {
             float dp = 0.0f; for (int k = 0; k < dim; k++) dp += st->prevDir[k] * st->n[k];
             if (st->prevDist > 0.0f && dp < 0.0f) { for (int k = 0; k < dim; k++) st->n[k] *= -1.0f; flip = 1; }
@@ -1103,6 +1109,7 @@ static int walk(const scene_t *sc, const oracle_params *prm, float dirichletDist
                                      prm->silhouette_precision, flip);
             if (prm->min_star_radius <= dirichletDist)
                 starRadius = smaxf(0.99f * starRadius, prm->min_star_radius);
+        }
         }
         gfn_update_ball(g, st->pt, starRadius);
         cnt->steps++;
@@ -1160,6 +1167,7 @@ static int walk(const scene_t *sc, const oracle_params *prm, float dirichletDist
             gfn_init(g, dim, 1, sc->absorption);
         }
         dirichletDist = dist_dirichlet(sc, st->pt, 0);
+        firstStep = 0;
     }
     return WC_DIRICHLET;
 }
@@ -1297,7 +1305,7 @@ static void estimate_point(const scene_t *sc, const oracle_params *prm, const fl
             float dd = dist_dirichlet(sc, st.pt, 0);
             pcg_t ws; pcg_seed(&ws, wseed, 1u);
             wcount_t wc = {0, 0};
-            int code = walk(sc, prm, dd, &ws, &g, &st, &wc);
+            int code = walk(sc, prm, dd, 0.0f, &ws, &g, &st, &wc);
             pc->iters += wc.iters;
             uint64_t total_steps = stepsBefore + wc.steps;
             if (code == WC_DIRICHLET || code == WC_RR) {
@@ -1463,4 +1471,324 @@ double oracle_math(int which, double x, int math_mode)
     case 14: return m_cbrtf((float)x);
     default: return NAN;
     }
+}
+
+/* ========================================================================= */
+/* Boundary value caching: runBoundaryValueCaching (demo.cpp:265-363) over    */
+/* boundary_value_caching/{boundary_sampler,domain_sampler,splatter}.h, 2D,   */
+/* all-Neumann scenes (scene.h:39,68).                                        */
+/* RNG (documented deviation): boundary sampler stream seed32(key,0,0,4),     */
+/* domain sampler seed32(key,0,0,5), walk w of boundary sample i             */
+/* seed32(key,i,w,6); sampled segments visited in ascending order (the        */
+/* reference: clock seeds, std::unordered_map order, boundary_sampler.h:335). */
+/* ========================================================================= */
+
+/* CDFTable (sampling.h:261-314) */
+static float cdf_build(float *table, const float *w, int n)
+{
+    if (n <= 0) return 0.0f;
+    table[0] = 0.0f;
+    for (int i = 1; i < n + 1; i++) table[i] = table[i - 1] + w[i - 1];
+    float total = table[n];
+    if (total == 0.0f) { for (int i = 1; i < n + 1; i++) table[i] = (float)i / (float)n; }
+    else { for (int i = 1; i < n + 1; i++) table[i] /= total; }
+    return total;
+}
+
+static int cdf_sample(const float *table, int size, float u)
+{
+    int first = 0, len = size;
+    while (len > 0) {
+        int half = len >> 1, middle = first + half;
+        if (table[middle] <= u) { first = middle + 1; len -= half + 1; }
+        else len = half;
+    }
+    return sclampi(first - 1, 0, size - 2);
+}
+
+/* buildCDFTable (boundary_sampler.h:291-331), every segment on the Neumann boundary */
+static float bvc_table(const geom_t *g, const scene_t *sc, float offset, float *table)
+{
+    float *w = calloc((size_t)g->np + 1, sizeof(float));
+    for (int i = 0; i < g->np; i++) {
+        const float *pa = g->v[g->ix[i][0]], *pb = g->v[g->ix[i][1]];
+        float pm[2] = {(pa[0] + pb[0]) / 2.0f, (pa[1] + pb[1]) / 2.0f};
+        float s0 = pb[0] - pa[0], s1 = pb[1] - pa[1];
+        float n[2] = {s1, -s0};
+        float z = n[0] * n[0] + n[1] * n[1];
+        if (z > 0.0f) { float r = sqrtf(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+        float q[2] = {pm[0] + offset * n[0], pm[1] + offset * n[1]};
+        int in = q[0] >= sc->pmin[0] && q[1] >= sc->pmin[1] && q[0] <= sc->pmax[0] && q[1] <= sc->pmax[1];
+        if (in) w[i] = sqrtf(s1 * s1 + (-s0) * (-s0));
+    }
+    float total = cdf_build(table, w, g->np);
+    free(w);
+    return total;
+}
+
+typedef struct { float *rec; int n, cap; } recbuf_t;
+static void rec_push(recbuf_t *b, const float *r)
+{
+    if (b->n == b->cap) { b->cap = b->cap ? 2 * b->cap : 256; b->rec = realloc(b->rec, sizeof(float) * 8 * (size_t)b->cap); }
+    memcpy(b->rec + 8 * (size_t)b->n, r, sizeof(float) * 8); b->n++;
+}
+
+/* generateSamples (boundary_sampler.h:333-402) */
+static void bvc_gen_boundary(const geom_t *g, const float *table, int n, float total, int aligned, pcg_t *rng,
+                             recbuf_t *out, float pdf)
+{
+    if (!(total > 0.0f) || n <= 0) return;
+    float *strat = malloc(sizeof(float) * (size_t)n);
+    gen_stratified(strat, n, 1, rng);
+    int *count = calloc((size_t)g->np, sizeof(int));
+    for (int i = 0; i < n; i++) count[cdf_sample(table, g->np + 1, strat[i])]++;
+    for (int f = 0; f < g->np; f++) {
+        int c = count[f];
+        if (!c) continue;
+        float *u = malloc(sizeof(float) * (size_t)c);
+        if (c == 1) u[0] = pcg_float(rng); else gen_stratified(u, c, 1, rng);
+        const float *pa = g->v[g->ix[f][0]], *pb = g->v[g->ix[f][1]];
+        float s0 = pb[0] - pa[0], s1 = pb[1] - pa[1];
+        for (int i = 0; i < c; i++) {
+            float nn[2] = {s1, -s0};
+            float norm = sqrtf(nn[0] * nn[0] + nn[1] * nn[1]);
+            float r[8] = {pa[0] + u[i] * s0, pa[1] + u[i] * s1, nn[0] / norm, nn[1] / norm, pdf, 0.0f, 0.0f,
+                          aligned ? 1.0f : 0.0f};
+            rec_push(out, r);
+        }
+        free(u);
+    }
+    free(count); free(strat);
+}
+
+/* estimateSolution (walk_on_stars.h:353-464) at a boundary sample */
+static float bvc_estimate(const scene_t *sc, const oracle_params *prm, const float *pt, const float *nrm, int aligned,
+                          int nWalks, uint64_t sidx, pcount_t *pc)
+{
+    float x[3] = {pt[0], pt[1], 0.0f};
+    float dDist = dist_dirichlet(sc, x, 0);
+    if (dDist <= prm->epsilon_shell) nWalks = 1;
+    float cn[3] = {nrm[0], nrm[1], 0.0f};
+    int flip = 0;
+    if (sc->double_sided && aligned) { cn[0] *= -1.0f; cn[1] *= -1.0f; flip = 1; }
+    float firstR;
+    if (dDist > prm->epsilon_shell && prm->steps_before_maximal_spheres != 0) {
+        firstR = star_radius(&sc->neu, x, prm->min_star_radius, dDist, prm->silhouette_precision, flip);
+        if (prm->min_star_radius <= dDist) firstR = smaxf(0.99f * firstR, prm->min_star_radius);
+    } else {
+        firstR = dDist;
+    }
+    int yuk0 = sc->absorption > 0.0f && prm->steps_before_tikhonov == 0;
+    float mean = 0.0f; int N = 0;
+    for (int w = 0; w < nWalks; w++) {
+        gfn_t g; gfn_init(&g, 2, yuk0, sc->absorption);
+        wstate_t st; memset(&st, 0, sizeof(st));
+        memcpy(st.pt, x, 12); memcpy(st.n, cn, 12); memcpy(st.prevDir, cn, 12);
+        st.prevDist = FLT_MAX; st.throughput = 1.0f; st.onNeumann = 1;
+        pcg_t ws; pcg_seed(&ws, oracle_seed32(prm->seed, sidx, (uint64_t)w, 6), 1u);
+        wcount_t wc = {0, 0};
+        int code = walk(sc, prm, dDist, firstR, &ws, &g, &st, &wc);
+        pc->iters += wc.iters;
+        if (code == WC_DIRICHLET || code == WC_RR) {
+            float term = (code == WC_DIRICHLET && !prm->ignore_dirichlet) ? sc->g_dirichlet : 0.0f;
+            float total = st.throughput * term + st.totalNeumann + st.totalSource;
+            N += 1;
+            float delta = total - mean;
+            mean += delta / (float)N;
+            pc->steps += wc.steps; pc->rec++;
+            if (code == WC_RR) pc->rr++; else pc->dir++;
+        } else {
+            pc->wasted += wc.steps;
+            if (code == WC_ESCAPED) pc->esc++; else pc->maxl++;
+        }
+    }
+    return mean;
+}
+
+/* free-space Green's functions, 2D (distributions.h:85-119, 168-219) */
+typedef struct { int yukawa; float lambda, sqrtLambda; } fs2_t;
+
+static void fs2_k(float mur, float *K0, float *K1, float *K2)
+{
+    double k0 = bessk0((double)mur), k1 = bessk1((double)mur);
+    *K0 = (float)k0; *K1 = (float)k1;
+    double tox = 2.0 / (double)mur;                /* bessel::bessk(2, x), bessel.hpp:584-608 */
+    *K2 = (float)(k0 + (1.0 * tox) * k1);
+}
+
+typedef struct { float mean, g[2]; int n; } sstat_t;
+static void sstat_add(sstat_t *s, float est, const float *ge)
+{
+    s->n += 1;
+    float fN = (float)s->n;
+    s->mean += (est - s->mean) / fN;
+    for (int k = 0; k < 2; k++) s->g[k] += (ge[k] - s->g[k]) / fN;
+}
+
+/* Splatter::splat of every cached sample onto one evaluation point (splatter.h:43-301) */
+static void bvc_splat_point(const fs2_t *gf, const float *x, const recbuf_t *rb, float radius_clamp, float reg,
+                            float *sol, float *grad)
+{
+    sstat_t st[3]; memset(st, 0, sizeof(st));
+    for (int j = 0; j < rb->n; j++) {
+        const float *R = rb->rec + 8 * (size_t)j;
+        int kind = (int)R[7];
+        float pdf = R[4], value = R[5];
+        float yx[2] = {R[0] - x[0], R[1] - x[1]}, xy[2] = {x[0] - R[0], x[1] - R[1]};
+        float r = smaxf(radius_clamp, sqrtf(yx[0] * yx[0] + yx[1] * yx[1]));
+        float K0 = 0, K1 = 0, K2 = 0;
+        if (gf->yukawa) fs2_k(r * gf->sqrtLambda, &K0, &K1, &K2);
+        float G, dG[2];
+        if (!gf->yukawa) {
+            G = (float)((double)(-m_logf(r)) / TWO_PI_D);
+            float s = (float)(TWO_PI_D * (double)(r * r));
+            for (int k = 0; k < 2; k++) dG[k] = (-xy[k]) / s;
+        } else {
+            G = (float)((double)K0 / TWO_PI_D);
+            float Qr = gf->sqrtLambda * K1;
+            float s = (float)(TWO_PI_D * (double)r);
+            for (int k = 0; k < 2; k++) dG[k] = ((-xy[k]) * Qr) / s;
+        }
+        float dGNorm = sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
+        float est, ge[2];
+        if (kind != 2) {
+            float sg = kind == 1 ? -1.0f : 1.0f;
+            float n[2] = {R[2] * sg, R[3] * sg};
+            float nd = n[0] * xy[0] + n[1] * xy[1];
+            float P, dP[2];
+            float r2 = r * r;
+            if (!gf->yukawa) {
+                P = (float)((double)nd / (TWO_PI_D * (double)r2));
+                float c = 2.0f * (nd / r2);
+                float s = (float)(TWO_PI_D * (double)r2);
+                for (int k = 0; k < 2; k++) dP[k] = (n[k] - c * xy[k]) / s;
+            } else {
+                float Qr = gf->sqrtLambda * K1;
+                P = (float)((double)(nd * Qr) / (TWO_PI_D * (double)r));
+                float Qr1 = gf->sqrtLambda * K1;
+                float Qr2 = gf->lambda * (K0 + K2) / 2.0f;
+                float c = (nd / r2) * (Qr1 + r * Qr2);
+                float s = (float)(TWO_PI_D * (double)r);
+                for (int k = 0; k < 2; k++) dP[k] = (n[k] * Qr1 - c * xy[k]) / s;
+            }
+            float dPNorm = sqrtf(dP[0] * dP[0] + dP[1] * dP[1]);
+            if (!(isfinite(G) && isfinite(P) && isfinite(dGNorm) && isfinite(dPNorm))) continue;
+            if (reg > 0.0f) { r /= reg; P *= 1.0f - m_expf(-r * r); }
+            float ndv = R[6];
+            est = (G * ndv - P * value) / pdf;
+            for (int k = 0; k < 2; k++) ge[k] = (dG[k] * ndv - dP[k] * value) / pdf;
+        } else {
+            if (!(isfinite(G) && isfinite(dGNorm))) continue;
+            est = (G * value) / pdf;
+            for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
+        }
+        sstat_add(&st[kind], est, ge);
+    }
+    float v = st[0].mean; v += st[1].mean; v += st[2].mean;
+    *sol = v;
+    for (int k = 0; k < 2; k++) { float a = st[0].g[k]; a += st[1].g[k]; a += st[2].g[k]; grad[k] = a; }
+}
+
+int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const oracle_bvc_params *bp,
+               float *solution, float *grad, float *samples, int64_t samples_capacity, int64_t *counts,
+               oracle_stats *stats)
+{
+    if (!scene || !prm || !bp || !solution || !grad) return -1;
+    if (scene->dim != 2 || scene->n_dprims > 0 || scene->n_prims <= 0 || bp->grid_res < 1 ||
+        bp->n_walks_solution < 1) return -2;
+    scene_t sc;
+    g_libm = prm->math_mode == 1;
+    if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
+    const geom_t *g = &sc.neu;
+    recbuf_t rb = {0};
+    /* ---- boundary samples */
+    pcg_t bs; pcg_seed(&bs, oracle_seed32(prm->seed, 0, 0, 4), 1u);
+    float *t_main = malloc(sizeof(float) * ((size_t)g->np + 1)), *t_al = malloc(sizeof(float) * ((size_t)g->np + 1));
+    float a_main = bvc_table(g, &sc, -1.0f * bp->normal_offset, t_main);
+    int nb_main, nb_al = 0;
+    if (sc.double_sided) {
+        float a_al = bvc_table(g, &sc, bp->normal_offset, t_al);
+        float total = a_main + a_al;
+        int n_main = (int)ceilf((float)bp->boundary_cache_size * a_main / total);
+        int n_al = (int)ceilf((float)bp->boundary_cache_size * a_al / total);
+        bvc_gen_boundary(g, t_main, n_main, a_main, 0, &bs, &rb, 1.0f / a_main);
+        nb_main = rb.n;
+        bvc_gen_boundary(g, t_al, n_al, a_al, 1, &bs, &rb, 1.0f / a_al);
+        nb_al = rb.n - nb_main;
+    } else {
+        bvc_gen_boundary(g, t_main, bp->boundary_cache_size, a_main, 0, &bs, &rb, 1.0f / a_main);
+        nb_main = rb.n;
+    }
+    free(t_main); free(t_al);
+    /* ---- estimates at the boundary samples (BoundarySampler::computeEstimates) */
+    pcount_t pc; memset(&pc, 0, sizeof(pc));
+    for (int i = 0; i < rb.n; i++) {
+        float *R = rb.rec + 8 * (size_t)i;
+        R[5] = bvc_estimate(&sc, prm, R, R + 2, R[7] == 1.0f, bp->n_walks_solution, (uint64_t)i, &pc);
+        R[6] = 0.0f;  /* pde.neumann == 0 (scene.h:176-181) */
+    }
+    /* ---- domain samples (DomainSampler::generateSamples) */
+    int nd_kept = 0;
+    if (!prm->ignore_source && bp->domain_cache_size > 0) {
+        float ext[2] = {sc.pmax[0] - sc.pmin[0], sc.pmax[1] - sc.pmin[1]};
+        float vol;
+        if (sc.double_sided) vol = ext[0] * ext[1];
+        else {
+            float sv = 0.0f;
+            for (int p = 0; p < g->np; p++) {
+                const float *pa = g->v[g->ix[p][0]], *pb = g->v[g->ix[p][1]];
+                sv += 0.5f * (pa[0] * pb[1] - pa[1] * pb[0]);
+            }
+            vol = fabsf(sv);
+        }
+        float pdf = 1.0f / vol;
+        int nstrat = bp->domain_cache_size;
+        if (vol > 0.0f) nstrat = (int)((float)nstrat * (ext[0] * ext[1] * pdf));
+        if (nstrat > 0) {
+            pcg_t ds; pcg_seed(&ds, oracle_seed32(prm->seed, 0, 0, 5), 1u);
+            float *strat = malloc(sizeof(float) * 2 * (size_t)nstrat);
+            gen_stratified(strat, nstrat, 2, &ds);
+            for (int i = 0; i < nstrat; i++) {
+                float x[3] = {sc.pmin[0] + ext[0] * strat[2 * i], sc.pmin[1] + ext[1] * strat[2 * i + 1], 0.0f};
+                int keep = sc.double_sided ? !outside_bbox(&sc, x) : inside_domain(&sc, x);
+                if (!keep) continue;
+                float r[8] = {x[0], x[1], 0.0f, 0.0f, pdf, source_value(&sc, x), 0.0f, 2.0f};
+                rec_push(&rb, r);
+                nd_kept++;
+            }
+            free(strat);
+        }
+    }
+    /* ---- splat onto the evaluation grid (createEvaluationGrid grid.h:352-368, saveEvaluationGrid 370-414) */
+    fs2_t gf = {sc.absorption > 0.0f, sc.absorption, sqrtf(sc.absorption)};
+    const int res = bp->grid_res;
+    float ext[2] = {sc.pmax[0] - sc.pmin[0], sc.pmax[1] - sc.pmin[1]};
+    for (int i = 0; i < res; i++) for (int j = 0; j < res; j++) {
+        size_t q = (size_t)i * res + j;
+        float x[3] = {((float)i / (float)res) * ext[0] + sc.pmin[0], ((float)j / (float)res) * ext[1] + sc.pmin[1], 0.0f};
+        float dDist = dist_dirichlet(&sc, x, 0), nDist = dist_neumann(&sc, x, 0);
+        float v = 0.0f, gv[2] = {0.0f, 0.0f};
+        if (!(dDist < bp->normal_offset)) bvc_splat_point(&gf, x, &rb, bp->radius_clamp, bp->kernel_regularization, &v, gv);
+        int in = inside_domain(&sc, x);
+        int masked = (!in && !sc.double_sided) || sminf(fabsf(dDist), fabsf(nDist)) < prm->boundary_distance_mask;
+        solution[q] = masked ? 0.0f : v;
+        grad[2 * q] = masked ? 0.0f : gv[0];
+        grad[2 * q + 1] = masked ? 0.0f : gv[1];
+    }
+    if (counts) { counts[0] = nb_main; counts[1] = nb_al; counts[2] = nd_kept; counts[3] = rb.n; }
+    int rc = 0;
+    if (samples) {
+        if (samples_capacity < rb.n) rc = -4;
+        else memcpy(samples, rb.rec, sizeof(float) * 8 * (size_t)rb.n);
+    }
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->walk_steps = pc.steps; stats->wasted_steps = pc.wasted; stats->walks_recorded = pc.rec;
+        stats->walks_escaped = pc.esc; stats->walks_max_length = pc.maxl; stats->walks_rr = pc.rr;
+        stats->walks_dirichlet = pc.dir; stats->points_estimated = (uint64_t)(nb_main + nb_al);
+        stats->rejection_iters = pc.iters;
+    }
+    free(rb.rec);
+    scene_free(&sc);
+    return rc;
 }

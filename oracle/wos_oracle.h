@@ -84,6 +84,18 @@ int oracle_solve(const oracle_scene_desc *scene, const oracle_params *prm,
                  float *p, float *grad, int32_t *n_est, int32_t *steps,
                  oracle_stats *stats);
 
+/* Boundary value caching: runBoundaryValueCaching (bindings/zombie/demo/demo.cpp:
+ * 265-363), 2D all-Neumann scenes.  Outputs as wos_bvc (include/wos.h). */
+typedef struct oracle_bvc_params {
+    int32_t n_walks_solution, n_walks_gradient, boundary_cache_size, domain_cache_size, grid_res;
+    int32_t use_finite_differences;
+    float normal_offset, radius_clamp, kernel_regularization;
+} oracle_bvc_params;
+
+int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const oracle_bvc_params *bvc,
+               float *solution, float *grad, float *samples, int64_t samples_capacity, int64_t *counts,
+               oracle_stats *stats);
+
 /* Geometry helpers exposed for unit tests. */
 int oracle_point_info(const oracle_scene_desc *scene, const float *pt,
                       float *dirichlet_dist, float *neumann_dist,

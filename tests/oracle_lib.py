@@ -41,6 +41,14 @@ class Params(C.Structure):
     ]
 
 
+class BvcParams(C.Structure):
+    _fields_ = [("n_walks_solution", C.c_int32), ("n_walks_gradient", C.c_int32),
+                ("boundary_cache_size", C.c_int32), ("domain_cache_size", C.c_int32),
+                ("grid_res", C.c_int32), ("use_finite_differences", C.c_int32),
+                ("normal_offset", C.c_float), ("radius_clamp", C.c_float),
+                ("kernel_regularization", C.c_float)]
+
+
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "walk_steps", "wasted_steps", "walks_recorded", "walks_escaped",
@@ -76,6 +84,9 @@ def lib():
         L.oracle_math.argtypes = [C.c_int, C.c_double, C.c_int]
         L.oracle_seed32.restype = C.c_uint32
         L.oracle_seed32.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.oracle_bvc.restype = C.c_int
+        L.oracle_bvc.argtypes = [C.POINTER(SceneDesc), C.POINTER(Params), C.POINTER(BvcParams), C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(Stats)]
         L.oracle_lhs.restype = C.c_int
         L.oracle_lhs.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_void_p]
         _lib = L
@@ -190,3 +201,38 @@ def lhs(seed, n, dims):
 
 def seed32(key, idx, pair, tag):
     return int(lib().oracle_seed32(key, idx, pair, tag))
+
+
+def bvc_params(solver=None, output=None):
+    """Oracle copy of the BVC keys (demo.cpp:269-290), same defaults as the product's."""
+    s = dict(solver or {})
+    o = dict(output or {})
+    b = BvcParams()
+    eps = float(s.get("epsilonShell", 1e-3))
+    b.n_walks_solution = int(s.get("nWalksForCachedSolutionEstimates", 128))
+    b.n_walks_gradient = int(s.get("nWalksForCachedGradientEstimates", 640))
+    b.boundary_cache_size = int(s.get("boundaryCacheSize", 1024))
+    b.domain_cache_size = int(s.get("domainCacheSize", 1024))
+    b.grid_res = int(o["gridRes"])
+    b.use_finite_differences = int(bool(s.get("useFiniteDifferencesForBoundaryDerivatives", False)))
+    b.normal_offset = float(s.get("normalOffsetForCachedDirichletSamples", 5.0 * eps))
+    b.radius_clamp = float(s.get("radiusClampForKernels", 1e-3))
+    b.kernel_regularization = float(s.get("regularizationForKernels", 0.0))
+    return b
+
+
+def bvc(scene: OracleScene, params: Params, bp: BvcParams):
+    """oracle_bvc: (solution [g, g], grad [g, g, 2], samples [k, 8], counts, stats)."""
+    g = int(bp.grid_res)
+    sol = np.zeros(g * g, np.float32)
+    grad = np.zeros(g * g * 2, np.float32)
+    cap = 2 * int(bp.boundary_cache_size) + 4 * int(bp.domain_cache_size) + 16
+    samples = np.zeros(cap * 8, np.float32)
+    counts = np.zeros(4, np.int64)
+    st = Stats()
+    rc = lib().oracle_bvc(C.byref(scene.desc), C.byref(params), C.byref(bp), sol.ctypes.data, grad.ctypes.data,
+                          samples.ctypes.data, cap, counts.ctypes.data, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_bvc failed rc={rc}")
+    return (sol.reshape(g, g), grad.reshape(g, g, 2), samples[:int(counts[3]) * 8].reshape(-1, 8).copy(),
+            counts, st.as_dict())

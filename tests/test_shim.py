@@ -33,9 +33,30 @@ def test_missing_required_keys_raise():
         zombie_bindings.wost(None, solver, {}, np.zeros((1, 2), np.float32))
 
 
-def test_bvc_not_provided():
-    with pytest.raises(NotImplementedError):
+def test_bvc_requires_grid_res():
+    """bvc reads output.gridRes as required (demo.cpp:281 getRequired)."""
+    with pytest.raises(KeyError, match="gridRes"):
         zombie_bindings.bvc(None, {}, {})
+
+
+def test_solution_image_writers(tmp_path):
+    """saveEvaluationGrid's Image<3>::write: PFM 'PF' rows bottom-to-top, PNG 8-bit RGB."""
+    import zlib
+    img = (np.arange(12, dtype=np.float32).reshape(3, 4) / 12.0)
+    pfm = tmp_path / "a" / "s.pfm"
+    zombie_bindings._write_image(str(pfm), img)
+    raw = pfm.read_bytes()
+    assert raw.startswith(b"PF\n4 3\n-1\n")
+    body = np.frombuffer(raw[len(b"PF\n4 3\n-1\n"):], "<f4").reshape(3, 4, 3)
+    np.testing.assert_array_equal(body[::-1, :, 1], img)
+    png = tmp_path / "s.png"
+    zombie_bindings._write_image(str(png), img)
+    data = png.read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    idat = data[data.index(b"IDAT") + 4:data.index(b"IEND") - 8]
+    rows = zlib.decompress(idat)
+    px = np.frombuffer(rows, np.uint8).reshape(3, 1 + 4 * 3)[:, 1:].reshape(3, 4, 3)
+    np.testing.assert_array_equal(px[..., 0], np.clip((img * 255).astype(int), 0, 255))
 
 
 def test_pfm_reader_roundtrip(tmp_path):

@@ -138,10 +138,14 @@ void ctx_free(DevCtx& c) {
 // the rejection bound tables (host, computed once per process)
 const std::vector<float>& rejection_tables() {
   static std::once_flag once;
-  static std::vector<float> t(2 * wos::kRejTabBins);
+  // [2D bound | 3D bound | 2D envelope | 3D envelope] (DevParams::rej_tab, rej_env)
+  constexpr size_t kEnv = (size_t)wos::kRejTabBins * wos::kRejEnvX * 2;
+  static std::vector<float> t(2 * wos::kRejTabBins + 2 * kEnv);
   std::call_once(once, [] {
     wos::rejection_bound_table(2, t.data());
     wos::rejection_bound_table(3, t.data() + wos::kRejTabBins);
+    wos::rejection_envelope_table(2, t.data() + 2 * wos::kRejTabBins);
+    wos::rejection_envelope_table(3, t.data() + 2 * wos::kRejTabBins + kEnv);
   });
   return t;
 }
@@ -757,6 +761,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     dp.n_jump = c.n_jump;
     const char* rt = std::getenv("WOS_REJ_TABLE");  // "0": the scene-independent bound only (A/B)
     dp.rej_tab = (rt && rt[0] == '0') ? nullptr : c.d_rejtab;
+    const char* re = std::getenv("WOS_REJ_ENV");  // "0": no two-sided envelope (A/B)
+    dp.rej_env = (re && re[0] == '0') ? nullptr : c.d_rejtab + 2 * wos::kRejTabBins;
   }
 
   // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
@@ -1049,6 +1055,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     dp.jump = c.d_jump;
     dp.n_jump = c.n_jump;
     dp.rej_tab = c.d_rejtab;
+    dp.rej_env = c.d_rejtab + 2 * wos::kRejTabBins;
   }
   WalkLayout wl;
   {

@@ -733,6 +733,11 @@ __device__ __forceinline__ float k1_fast(float x);
 // ---------------------------------------------------------------------------
 // Green's functions on balls (distributions.h:273-832)
 // ---------------------------------------------------------------------------
+// 1: the direction-sampled Poisson kernel reuses the ball update's K1(mu R), I1(mu R)
+// when the point's distance from the centre rounds to R (bit-identical values)
+#ifndef WOS_PK_REUSE
+#define WOS_PK_REUSE 0
+#endif
 template <int DIM>
 struct Gfn {
   bool yukawa;
@@ -868,10 +873,18 @@ struct Gfn {
 #if WOS_ABL_FAST_BESSEL
       float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
 #else
-      double i1, k1;
-      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
-      float K1mur = (float)k1;
-      float I1mur = (float)i1;
+      float K1mur, I1mur;
+      if (WOS_PK_REUSE && rr == R) {
+        // |y - c| rounds to R (about half the sphere points): mu r is mu R, whose K1 and I1
+        // the ball update already evaluated -- the same double values, rounded the same
+        K1mur = B0;
+        I1mur = B1;
+      } else {
+        double i1, k1;
+        bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
+        K1mur = (float)k1;
+        I1mur = (float)i1;
+      }
 #endif
       float Q = K1mur + I1mur * A0 / A1;
       return mur * Q;
@@ -1071,11 +1084,39 @@ __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, 
   return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
 }
 
+// Offset of a ball's row of the two-sided rejection envelope (DevParams::rej_env,
+// wos_host_scene.h rejection_envelope_table), or -1 when there is none: no table, the
+// s -> 0 bin, mu R beyond the table, or a non-positive / non-finite R / (norm bound).
+// (default off: the per-item table gather measured slower than the arithmetic it saves,
+// karman walk +4.5 %, cube +21 %: the load latency sits inside every generation)
+#ifndef WOS_REJ_ENV
+#define WOS_REJ_ENV 0
+#endif
+template <int DIM>
+__device__ __forceinline__ int rej_env_row(const DevParams& prm, float muR, float cR) {
+  if (!WOS_REJ_ENV || prm.rej_env == nullptr || !(muR >= 0.0f) || !(cR > 0.0f && cR < 3.0e38f)) return -1;
+  const int k = (int)(kRejTabScale * __builtin_sqrtf(muR));
+  if (k < 1 || k >= kRejTabBins) return -1;
+  return ((DIM == 3 ? kRejTabBins : 0) + k) * kRejEnvX * 2;
+}
+
+// Envelope decision of one iteration: 1 accept (u < lo R / (norm bound)), 0 reject
+// (u > hi R / (norm bound)), -1 the exact test (or its certified fast path) decides.
+__device__ __forceinline__ int rej_env_decide(const DevParams& prm, int row, float cR, float u, float x) {
+  if (row < 0) return -1;
+  const int j = (int)(x * (float)kRejEnvX);
+  const float* e = prm.rej_env + row + 2 * j;
+  const float hi = e[0], lo = e[1];
+  if (u > hi * cR) return 0;
+  if (u < lo * cR) return 1;
+  return -1;
+}
+
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM>
-__device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg32& s, float* pdf, float* out,
-                                              uint32_t* iters, bool need_pdf) {
+__device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM>& g, const float* dir, Pcg32& s,
+                                              float* pdf, float* out, uint32_t* iters, bool need_pdf) {
   const float R = g.R;
   if (DIM == 3 && !g.yukawa) {
     float u1 = s.nextf(), u2 = s.nextf();
@@ -1103,15 +1144,19 @@ __device__ __forceinline__ void sample_volume(Gfn<DIM>& g, const float* dir, Pcg
   const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
   const float rho = g.A0 / g.A1;
   const float invNB = 1.0f / (nrm * bound);
-  const float quick = g.yukawa ? rej_quick_bound<DIM>(DevParams{}, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
+  const float quick = g.yukawa ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
+  const float cR = R * invNB;
+  const int env = (g.yukawa && (fast || DIM == 3)) ? rej_env_row<DIM>(prm, g.muR, cR) : -1;
   int iter = 0;
   do {
     float u = s.nextf();
-    g.r = s.nextf() * R;
+    const float xd = s.nextf();
+    g.r = xd * R;
     iter++;
     int decided = -1;  // 1 accept, 0 reject, -1 undecided
     if (u > quick) {
       decided = 0;
+    } else if ((decided = rej_env_decide(prm, env, cR, u, xd)) >= 0) {
     } else if (fast) {
       const float mur = g.r * g.sqrtLambda;
       float k0, i0v;
@@ -1219,6 +1264,10 @@ struct RejLDS {
   float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
   float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
   float qb[kWave];                 // certain-reject bound (rej_quick_bound)
+#if WOS_REJ_ENV
+  float cR[kWave];                 // R / (norm bound): scale of the envelope (rej_env_decide)
+  int env[kWave];                  // the ball's envelope row (rej_env_row), -1: none
+#endif
 #if WOS_REJ_COMPACT
   uint16_t surv[kWave * 16];       // items that passed the certain-reject screen (one generation)
 #endif
@@ -1310,7 +1359,12 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
-      L->qb[lane] = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, 1.0f / (nrm * bound));
+      const float invNB = 1.0f / (nrm * bound);
+      L->qb[lane] = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB);
+#if WOS_REJ_ENV
+      L->cR[lane] = g.R * invNB;
+      L->env[lane] = rej_env_row<DIM>(prm, g.muR, g.R * invNB);
+#endif
       if constexpr (DIM == 2) {
         L->c0[lane] = g.A0 / g.A1;
         L->c1[lane] = 1.0f / (nrm * bound);
@@ -1414,16 +1468,24 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
             if (u > L->qb[owner]) {
               // certain reject: the radius draw is not needed
               DIAG_LANE(D_RQUICK);
-            } else if constexpr (DIM == 2) {
-              const float x = draw_float(st * kPcgMult + kPcgInc);
-              dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
             } else {
               const float x = draw_float(st * kPcgMult + kPcgInc);
-              const float rr = x * L->R[owner];
-              dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
-              if (dcs < 0)
-                dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
-                                        L->bound[owner]);
+#if WOS_REJ_ENV
+              dcs = rej_env_decide(prm, L->env[owner], L->cR[owner], u, x);
+#else
+              dcs = -1;
+#endif
+              if (dcs < 0) {
+                if constexpr (DIM == 2) {
+                  dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
+                } else {
+                  const float rr = x * L->R[owner];
+                  dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
+                  if (dcs < 0)
+                    dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner],
+                                            L->nrm[owner], L->bound[owner]);
+                }
+              }
             }
             if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
             else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
@@ -1471,7 +1533,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
     }
   }
-  if (active && !coop) sample_volume<DIM>(g, dir, s, pdf, out, iters, need_pdf);
+  if (active && !coop) sample_volume<DIM>(prm, g, dir, s, pdf, out, iters, need_pdf);
 }
 
 // ---------------------------------------------------------------------------
@@ -2257,7 +2319,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
         if constexpr (DIM == 3)
           sample_volume_wave<DIM>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
         else
-          sample_volume<DIM>(g, dir, fs, &sourcePdf, sourcePt, iters, true);
+          sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, true);
       } else {
         float sdv[DIM];
         for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - x[k];

@@ -95,11 +95,16 @@ struct DevParams {
   // certain-reject bounds of the Yukawa rejection threshold by bin of s = mu R
   // (wos_host_scene.h rejection_bound_table), kRejTabBins floats; nullptr: none
   const float* rej_tab;
+  // two-sided envelope of the accept threshold, [2D | 3D][kRejTabBins][kRejEnvX][hi, lo]
+  // (wos_host_scene.h rejection_envelope_table); nullptr: none
+  const float* rej_env;
 };
 
 // bins of the rejection bound table: bin = floor(kRejTabScale * sqrt(mu R))
 constexpr int kRejTabBins = 96;
 constexpr float kRejTabScale = 8.0f;
+// x-bins of the two-sided rejection envelope (wos_host_scene.h rejection_envelope_table)
+constexpr int kRejEnvX = 32;
 
 // Walk-task workspace of one batch of points, SoA over T = n_points * wpp tasks
 // (task t = point * wpp + pair * n_anti + member).  Written by the first-ball

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 5
+#define WOS_ABI_VERSION 6
 
 enum {
     WOS_OK = 0,
@@ -120,6 +120,11 @@ typedef struct wos_solver_params {
     int32_t ignore_neumann;
     int32_t ignore_source;
     uint64_t seed;                          /* RNG key */
+    int32_t robust_float;                   /* 0 (default): the reference's float Bessel members, which
+                                               overflow to NaN for 2D Yukawa balls with mu R > ~92
+                                               (distributions.h:585-587,695); 1: balls with mu R > 80 use
+                                               exponentially scaled Bessels and ratios (finite, correct) --
+                                               identical to mode 0 on every ball with mu R <= 80 */
 } wos_solver_params;
 
 void wos_default_params(wos_solver_params *p);

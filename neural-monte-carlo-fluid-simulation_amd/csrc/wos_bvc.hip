@@ -330,6 +330,8 @@ hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const floa
 hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                                int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                                size_t shmem, int geom_floats, hipStream_t s) {
+  if (prm.robust)
+    return launch_walks_rb(2, true, sc, prm, tk, base, stride, counters, tqueue, grid, shmem, geom_floats, s);
   if (sc.geom_global)
     hipLaunchKernelGGL((wos_walk_kernel<2, true, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride,
                        counters, tqueue, geom_floats);
@@ -339,7 +341,8 @@ hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const D
   return hipGetLastError();
 }
 
-hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks) {
+hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks, bool robust) {
+  if (robust) return occupancy_rb(2, 2, geom_global, shmem, blocks);
   return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, true, true>, kBlock, shmem)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, false, true>, kBlock, shmem);
 }

@@ -719,6 +719,7 @@ wos::DevParams dev_params(const wos_solver_params* prm) {
   dp.ignore_dirichlet = prm->ignore_dirichlet;
   dp.ignore_neumann = prm->ignore_neumann;
   dp.ignore_source = prm->ignore_source;
+  dp.robust = prm->robust_float != 0;
   dp.seed = prm->seed;
   return dp;
 }
@@ -832,10 +833,10 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (n > 0) {
     int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb));
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb, dp.robust != 0));
     grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
-    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk));
+    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk, dp.robust != 0));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
   const uint64_t ticket = c.next_ticket++;
@@ -1081,7 +1082,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     HIP_TRY(wos::launch_bvc_start(dsc, dp, d_bpt, d_bnrm, d_al, d_bdd, nb, tk, st));
     HIP_TRY(hipEventRecord(q.bev[1], st));
     int bpc = 0;
-    HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc));
+    HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc, dp.robust != 0));
     const int grid = (int)std::min<int64_t>((int64_t)std::max(1, bpc) * std::max(1, c.num_cus), (tk.T + 63) / 64);
     unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kNumCounters + 1);
     HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, 0, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,

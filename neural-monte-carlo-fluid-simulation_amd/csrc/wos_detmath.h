@@ -310,6 +310,42 @@ WOS_HD void bessel_ik(double x, double* i0, double* k0, double* i1, double* k1) 
   if (N1) *i1 = vi1;
 }
 
+// Robust float semantics (wos_solver_params.robust_float): exponentially scaled A&S
+// functions ie_v(x) = e^-x I_v(x), ke_v(x) = e^x K_v(x), x > 0 -- the polynomials above
+// without the exponential (large x) or times the compensating exponential (small x),
+// so nothing overflows.  Operation for operation as oracle/wos_oracle.c bess_scaled.
+WOS_HD void bessel_scaled(double x, double* ie0, double* ke0, double* ie1, double* ke1) {
+  if (x < 3.75) {
+    const double e = dexp(-x);
+    *ie0 = bessi0(x) * e;
+    *ie1 = bessi1(x) * e;
+  } else {
+    const double y = 3.75 / x, sx = __builtin_sqrt(x);
+    *ie0 = (0.39894228 + y * (0.1328592e-1 + y * (0.225319e-2 + y * (-0.157565e-2 + y * (0.916281e-2 +
+           y * (-0.2057706e-1 + y * (0.2635537e-1 + y * (-0.1647633e-1 + y * 0.392377e-2)))))))) / sx;
+    double a = 0.2282967e-1 + y * (-0.2895312e-1 + y * (0.1787654e-1 - y * 0.420059e-2));
+    a = 0.39894228 + y * (-0.3988024e-1 + y * (-0.362018e-2 + y * (0.163801e-2 + y * (-0.1031555e-1 + y * a))));
+    *ie1 = a / sx;
+  }
+  if (x <= 2.0) {
+    const double e = dexp(x);
+    *ke0 = bessk0(x) * e;
+    *ke1 = bessk1(x) * e;
+  } else {
+    const double y = 2.0 / x, sx = __builtin_sqrt(x);
+    *ke0 = (1.25331414 + y * (-0.7832358e-1 + y * (0.2189568e-1 + y * (-0.1062446e-1 + y * (0.587872e-2 +
+           y * (-0.251540e-2 + y * 0.53208e-3)))))) / sx;
+    *ke1 = (1.25331414 + y * (0.23498619 + y * (-0.3655620e-1 + y * (0.1504268e-1 + y * (-0.780353e-2 +
+           y * (0.325614e-2 + y * (-0.68245e-3))))))) / sx;
+  }
+}
+
+// 3D robust member: (cosh x - sinh x / x) e^-x
+WOS_HD double i32_scaled(double x) {
+  const double e2 = dexp(-2.0 * x);
+  return 0.5 * ((1.0 + e2) - (1.0 - e2) / x);
+}
+
 // ---------------------------------------------------------------------------
 // PCG32 (pcg32.h) + counter-based seeding
 // ---------------------------------------------------------------------------

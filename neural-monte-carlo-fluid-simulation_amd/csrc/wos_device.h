@@ -738,9 +738,88 @@ __device__ __forceinline__ float k1_fast(float x);
 #ifndef WOS_PK_REUSE
 #define WOS_PK_REUSE 0
 #endif
+// ---------------------------------------------------------------------------
+// Robust float semantics (Gfn::yukawa == kYukScaled): the reference's Yukawa members
+// rewritten with exponentially scaled Bessels (bessel_scaled) and e^{2(mu r - mu R)} <= 1,
+// in double, rounded where the reference rounds its result -- operation for operation
+// as oracle/wos_oracle.c (scaled_q0 and the g->scaled branches).  Out of line: the
+// reference-semantics path keeps its registers.
+// ---------------------------------------------------------------------------
+#define WOS_COLD __device__ __attribute__((noinline))
+// 2D K0(mur) - I0(mur) K0(muR)/I0(muR) (a0 = ke0(muR), a1 = ie0(muR));
+// 3D e^-mur - e^-muR sinh(mur)/sinh(muR)
 template <int DIM>
+WOS_COLD double scaled_q0(float mur, float muR, float a0, float a1) {
+  const double x = (double)mur, X = (double)muR;
+  if constexpr (DIM == 2) {
+    double ie0, ke0, ie1, ke1;
+    bessel_scaled(x, &ie0, &ke0, &ie1, &ke1);
+    return dexp(-x) * (ke0 - ie0 * ((double)a0 / (double)a1) * dexp(2.0 * (x - X)));
+  } else {
+    return dexp(-x) - dexp(x - 2.0 * X) * (1.0 - dexp(-2.0 * x)) / (1.0 - dexp(-2.0 * X));
+  }
+}
+
+template <int DIM>
+WOS_COLD void scaled_members(float muR, float* a0, float* a1, float* b0, float* b1) {
+  double ie0, ke0, ie1, ke1;
+  bessel_scaled((double)muR, &ie0, &ke0, &ie1, &ke1);
+  *a0 = (float)ke0; *a1 = (float)ie0; *b0 = (float)ke1; *b1 = (float)ie1;
+}
+
+template <int DIM>
+WOS_COLD float scaled_poisson_kernel(float muR, float a1) {
+  const double X = (double)muR;
+  if constexpr (DIM == 2) return (float)(dexp(-X) / (kTwoPi * (double)a1));
+  else return (float)(X * 2.0 * dexp(-X) / (kFourPi * (1.0 - dexp(-2.0 * X))));
+}
+
+template <int DIM>
+WOS_COLD float scaled_gradient_norm(float r, float sqrtL, float muR, float b0, float b1) {
+  const float mur = r * sqrtL;
+  const double x = (double)mur, X = (double)muR, t = dexp(2.0 * (x - X));
+  if constexpr (DIM == 2) {
+    double ie0, ke0, ie1, ke1;
+    bessel_scaled(x, &ie0, &ke0, &ie1, &ke1);
+    const double q = dexp(-x) * (ke1 - ie1 * ((double)b0 / (double)b1) * t);
+    return (float)((double)sqrtL * q / (kTwoPi * (double)r));
+  } else {
+    const double q = dexp(-x) * ((1.0 + 1.0 / x) - i32_scaled(x) * ((1.0 + 1.0 / X) / i32_scaled(X)) * t);
+    return (float)((double)sqrtL * q / (kFourPi * (double)(r * r)));
+  }
+}
+
+// QR of the Poisson kernel gradient
+template <int DIM>
+WOS_COLD float scaled_pk_gradient(float muR, float sqrtL, float lambda, float R, float b1) {
+  const double X = (double)muR;
+  if constexpr (DIM == 2) return (float)((double)sqrtL * dexp(-X) / ((double)R * (double)b1));
+  else return (float)((double)lambda * dexp(-X) / i32_scaled(X));
+}
+
+template <int DIM>
+WOS_COLD float scaled_dir_poisson_kernel(float mur, float muR, float a0, float a1) {
+  const double x = (double)mur, X = (double)muR, t = dexp(2.0 * (x - X));
+  double q;
+  if constexpr (DIM == 2) {
+    double ie0, ke0, ie1, ke1;
+    bessel_scaled(x, &ie0, &ke0, &ie1, &ke1);
+    q = ke1 + ie1 * ((double)a0 / (double)a1) * t;
+  } else {
+    q = (1.0 + 1.0 / x) + i32_scaled(x) * (2.0 / (1.0 - dexp(-2.0 * X))) * t;
+  }
+  return (float)(x * dexp(-x) * q);
+}
+
+// Robust float semantics (DevParams::robust): Yukawa balls with mu R above this use
+// exponentially scaled members (Gfn::yukawa == kYukScaled); below it the reference's
+// float members are finite and are kept, so the two modes agree there bit for bit.
+constexpr float kRobustMuR = 80.0f;
+constexpr int kYukScaled = 2;
+
+template <int DIM, bool RB = false>
 struct Gfn {
-  bool yukawa;
+  int yukawa;  // 0 harmonic, 1 Yukawa, kYukScaled Yukawa with scaled members (robust mode)
   float c[DIM], yVol[DIM], ySurf[DIM];
   float R, r;
   float lambda, sqrtLambda;
@@ -748,14 +827,22 @@ struct Gfn {
   static constexpr float rClamp = 1e-4f;
 
   __device__ __forceinline__ void init(bool yuk, float lam) {
-    yukawa = yuk; lambda = lam; sqrtLambda = __builtin_sqrtf(lam);
+    yukawa = yuk ? 1 : 0; lambda = lam; sqrtLambda = __builtin_sqrtf(lam);
   }
 
-  __device__ __forceinline__ void update_ball(const float* cc, float RR) {
+  // RB: the instantiation of the robust kernels; elsewhere the scaled branches are dead code
+  __device__ __forceinline__ bool scaled() const { return RB && yukawa == kYukScaled; }
+
+  __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust) {
     for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
     R = RR; r = 0.0f;
     if (!yukawa) return;
     muR = R * sqrtLambda;
+    if constexpr (RB) yukawa = (robust && muR > kRobustMuR) ? kYukScaled : 1;
+    if (scaled()) {  // 3D scaled balls evaluate everything from mu R
+      if constexpr (DIM == 2) scaled_members<DIM>(muR, &A0, &A1, &B0, &B1);
+      return;
+    }
     if constexpr (DIM == 2) {
 #if WOS_ABL_FAST_BESSEL
       A0 = k0_fast(muR); A1 = i0_fast(muR); B0 = k1_fast(muR); B1 = i1_fast(muR);
@@ -780,6 +867,11 @@ struct Gfn {
 
   // G(r) for the current r (evaluate())
   __device__ __forceinline__ float evaluate() const {
+    if (scaled()) {
+      const double q = scaled_q0<DIM>(r * sqrtLambda, muR, A0, A1);
+      if constexpr (DIM == 2) return (float)(q / kTwoPi);
+      else return (float)(q / (kFourPi * (double)r));
+    }
     if (!yukawa) {
       if constexpr (DIM == 2) return (float)((double)flog(R / r) / kTwoPi);
       else return (float)((double)(1.0f / r - 1.0f / R) / kFourPi);
@@ -800,6 +892,7 @@ struct Gfn {
 
   __device__ __forceinline__ float poisson_kernel() const {
     if (!yukawa) return DIM == 2 ? (float)(1.0 / kTwoPi) : (float)(1.0 / kFourPi);
+    if (scaled()) return scaled_poisson_kernel<DIM>(muR, A1);
     if constexpr (DIM == 2) return (float)(1.0 / (kTwoPi * (double)A1));
     else return (float)((double)muR / (kFourPi * (double)A1));
   }
@@ -816,6 +909,7 @@ struct Gfn {
       else { float r3 = r * r * r; return (float)((double)(1.0f / r3 - 1.0f / (R * R * R)) / kFourPi); }
     }
     float mur = r * sqrtLambda;
+    if (scaled()) return scaled_gradient_norm<DIM>(r, sqrtLambda, muR, B0, B1);
     if constexpr (DIM == 2) {
       double i1, k1;
       bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
@@ -854,6 +948,11 @@ struct Gfn {
       }
       return;
     }
+    if (scaled()) {
+      const float QR = scaled_pk_gradient<DIM>(muR, sqrtLambda, lambda, R, B1);
+      for (int k = 0; k < DIM; k++) out[k] = (d[k] * QR) / (float)(DIM == 2 ? kTwoPi : kFourPi);
+      return;
+    }
     if constexpr (DIM == 2) {
       float QR = sqrtLambda / (R * B1);
       for (int k = 0; k < 2; k++) out[k] = (d[k] * QR) / (float)kTwoPi;
@@ -869,6 +968,7 @@ struct Gfn {
     for (int k = 0; k < DIM; k++) d[k] = y[k] - c[k];
     float rr = smax(rClamp, normv<DIM>(d));
     float mur = rr * sqrtLambda;
+    if (scaled()) return scaled_dir_poisson_kernel<DIM>(mur, muR, A0, A1);
     if constexpr (DIM == 2) {
 #if WOS_ABL_FAST_BESSEL
       float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
@@ -912,6 +1012,11 @@ struct Gfn {
     float r1 = smax(rClamp, normv<DIM>(yx));
     float r2 = (R * R - dotv<DIM>(xc, yc)) / R;
     float mur1 = r1 * sqrtLambda, mur2 = r2 * sqrtLambda;
+    if (scaled()) {
+      const double q1 = scaled_q0<DIM>(mur1, muR, A0, A1), q2 = scaled_q0<DIM>(mur2, muR, A0, A1);
+      if constexpr (DIM == 2) return (float)((q1 - q2) / kTwoPi);
+      else return (float)((q1 / (double)r1 - q2 / (double)r2) / kFourPi);
+    }
     if constexpr (DIM == 2) {
       float K0mur1 = (float)bessk0((double)mur1), K0mur2 = (float)bessk0((double)mur2);
       float I0mur1 = (float)bessi0((double)mur1), I0mur2 = (float)bessi0((double)mur2);
@@ -1114,8 +1219,8 @@ __device__ __forceinline__ int rej_env_decide(const DevParams& prm, int row, flo
 
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
-template <int DIM>
-__device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM>& g, const float* dir, Pcg32& s,
+template <int DIM, bool RB>
+__device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>& g, const float* dir, Pcg32& s,
                                               float* pdf, float* out, uint32_t* iters, bool need_pdf) {
   const float R = g.R;
   if (DIM == 3 && !g.yukawa) {
@@ -1199,21 +1304,40 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM>& g,
 constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
 // minimum iterations per unfinished lane and generation of the cooperative sampler
 // (2D acceptance ~21 %, 3D ~7 % on the shipped scenes)
+// (A/B on MI355X, tools/ab.sh: 2D 3 beats 1 by 2-4 % on karman / C; 3D 8 in the first-ball
+// kernel beats 16 by 8 %, while the walk kernel keeps 16)
 #ifndef WOS_REJ_BMIN2
-#define WOS_REJ_BMIN2 1
+#define WOS_REJ_BMIN2 3
 #endif
 #ifndef WOS_REJ_BMIN3
 #define WOS_REJ_BMIN3 16
 #endif
-template <int DIM>
-constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3;
-static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16, "RejLDS::surv holds 64 * 16 items");
+#ifndef WOS_REJ_BMIN3_FB
+#define WOS_REJ_BMIN3_FB 8
+#endif
+template <int DIM, bool FB>
+constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : (FB ? WOS_REJ_BMIN3_FB : WOS_REJ_BMIN3);
+static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 16, "RejLDS::surv holds 64 * 16 items");
 // 1: screen a generation's items with the certain-reject bound, then evaluate the
 // survivors compacted over the wave; 0 (default): every lane evaluates its own
 // items (the screen + compaction measured 15-20 % slower on karman / cube / C)
 #ifndef WOS_REJ_COMPACT
 #define WOS_REJ_COMPACT 0
 #endif
+// Self phase: while more than this many lanes of the wave are unfinished, a
+// generation would give each owner B = 1 item (2D) anyway, so every unfinished lane
+// evaluates its own next iteration from its own stream in registers -- no LDS
+// staging, no owner scan, no wave syncs; the cooperative generations start when at
+// most this many lanes remain.  64 disables the phase (the default: with the block
+// sizes above it measured no faster than the cooperative generations, within noise).
+#ifndef WOS_REJ_SELF2
+#define WOS_REJ_SELF2 64
+#endif
+#ifndef WOS_REJ_SELF3
+#define WOS_REJ_SELF3 64
+#endif
+template <int DIM>
+constexpr int kRejSelf = DIM == 2 ? WOS_REJ_SELF2 : WOS_REJ_SELF3;
 
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
@@ -1323,7 +1447,7 @@ __device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, f
 __device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, float sqrtL, float A0, float A1, float nrm,
                                                  float bound) {
   Gfn<3> h;
-  h.yukawa = true;
+  h.yukawa = 1;
   h.sqrtLambda = sqrtL;
   h.A0 = A0;
   h.A1 = A1;
@@ -1338,14 +1462,14 @@ __device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, floa
 // decisions by any lane, undecided ones by the owner (exact); 3D: certified float
 // decisions by any lane, undecided ones by the same lane with the exact test (cheap
 // single-precision arithmetic plus one exp).
-template <int DIM>
-__device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM>& g, const float* dir,
+template <int DIM, bool RB, bool FB = false>
+__device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool active, Gfn<DIM, RB>& g, const float* dir,
                                                    Pcg32& s, float* pdf, float* out, uint32_t* iters,
                                                    bool need_pdf, RejLDS* L, int lane) {
   bool coop = false;
   float bound = 0.0f, nrm = 1.0f;
   if (active && g.yukawa && !WOS_ABL_ONE_REJ &&
-      (DIM == 3 || (g.muR < 80.0f && !WOS_NO_FASTREJ))) {
+      (DIM == 3 ? !g.scaled() : (g.muR < 80.0f && !WOS_NO_FASTREJ))) {
     const float R = g.R, lam = g.lambda, sl = g.sqrtLambda;
     const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
     bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
@@ -1355,7 +1479,43 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
   }
   if (__ballot(coop) != 0) {
     const uint64_t s0 = s.state;
-    if (coop) {
+    int j0 = 0, jacc = -1;
+    bool done = !coop;
+    DIAG_COUNT(D_RCALLS, 1);
+    DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
+    if (kRejSelf<DIM> < kWave) {
+      // self phase (see kRejSelf): iteration j0 of every unfinished lane, sequential draws
+      const float invNB = coop ? 1.0f / (nrm * bound) : 0.0f;
+      const float qb = coop ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 0.0f;
+      const float rho = coop ? g.A0 / g.A1 : 0.0f;
+      // s advances past the self draws; the end of the call resets it from s0
+      while (__popcll(__ballot(!done)) > kRejSelf<DIM>) {
+        DIAG_COUNT(D_RGENS, 1);
+        if (!done) {
+          const float u = s.nextf();
+          const float x = s.nextf();
+          int dcs = 0;
+          DIAG_LANE(D_RITEMS);
+          if (u > qb) {
+            DIAG_LANE(D_RQUICK);
+          } else {
+            const float rr = x * g.R;
+            if constexpr (DIM == 2) dcs = rej_fast_decide(u, rr, g.sqrtLambda, rho, invNB);
+            else dcs = rej_fast_decide3(u, rr, g.sqrtLambda, rho, invNB);
+            if (dcs < 0) {
+              DIAG_LANE(D_RUND);
+              g.r = rr;
+              const float p = g.evaluate() / nrm;
+              const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
+              dcs = u < pdfRadius / bound ? 1 : 0;
+            }
+          }
+          if (dcs == 1) { jacc = j0; done = true; }
+          else if (++j0 >= kRejMax) { jacc = kRejMax - 1; done = true; }  // limit: last radius kept
+        }
+      }
+    }
+    if (!done) {
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
@@ -1377,10 +1537,6 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         L->bound[lane] = bound;
       }
     }
-    int j0 = 0, jacc = -1;
-    bool done = !coop;
-    DIAG_COUNT(D_RCALLS, 1);
-    DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
     for (;;) {
       const uint64_t pend = __ballot(!done);
       if (pend == 0) break;
@@ -1390,7 +1546,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       // generations -- each costs three wave syncs and the owners' scan -- for a
       // few iterations evaluated past an accept)
       int B = kWave / nact;
-      B = B < kRejBmin<DIM> ? kRejBmin<DIM> : (B > kRejBcap ? kRejBcap : B);
+      B = B < kRejBmin<DIM, FB> ? kRejBmin<DIM, FB> : (B > kRejBcap ? kRejBcap : B);
       const int items = nact * B, per = (items + kWave - 1) / kWave;
       // item / B as a multiply-shift (exact: item < 2048, B <= 32, see rej_div)
       const uint32_t mB = (65536u + (uint32_t)B - 1u) / (uint32_t)B;
@@ -1564,8 +1720,8 @@ __device__ __forceinline__ float prim_area(const float* P) {
 // Neumann boundary sample (walk_on_stars.h:212-260).  With the reference's h == 0
 // (scene.h:176-181) the term is exactly +0 unless G or the throughput is
 // non-finite; only then the brute-force stochastic sample is evaluated.
-template <int DIM>
-__device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM>& g,
+template <int DIM, bool RB>
+__device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM, RB>& g,
                                           WalkState<DIM>& st, float R, const float* rn) {
   constexpr int PS = Layout<DIM>::prim;
   const int np = sc.n_prims;
@@ -1660,8 +1816,8 @@ __device__ __forceinline__ int walk_step_begin(const DevScene& sc, const DevPara
 }
 
 // ball + direction + ray origin; the ray query follows (walk_on_stars.h:169-210)
-template <int DIM>
-__device__ __forceinline__ float walk_step_mid(const DevParams& prm, float dirichletDist, Pcg32& smp, Gfn<DIM>& g,
+template <int DIM, bool RB>
+__device__ __forceinline__ float walk_step_mid(const DevParams& prm, float dirichletDist, Pcg32& smp, Gfn<DIM, RB>& g,
                                                WalkState<DIM>& st, uint32_t* steps, bool query, float starQ,
                                                float* dir, float* org, float firstR = 0.0f) {
   float starRadius = dirichletDist;
@@ -1671,7 +1827,7 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
     starRadius = starQ;
     if (prm.min_star_radius <= dirichletDist) starRadius = smax(0.99f * starRadius, prm.min_star_radius);
   }
-  g.update_ball(st.pt, starRadius);
+  g.update_ball(st.pt, starRadius, prm.robust != 0);
   (*steps)++;
   float u[2];
   u[0] = smp.nextf();
@@ -1691,9 +1847,9 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
 
 // after the ray query: the miss point and the Neumann term (walk_on_stars.h:200-260);
 // the source sample (convergent, sample_volume_wave) and walk_step_tail follow
-template <int DIM>
+template <int DIM, bool RB>
 __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
-                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, float starRadius,
+                                              Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, float starRadius,
                                               const float* dir, const float* org, bool hit, Hit& ip) {
   const int np = sc.n_prims;
   const float* prims = G.prim;
@@ -1704,16 +1860,16 @@ __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParam
   if (!prm.ignore_neumann) {
     float rn[3] = {0.0f, 0.0f, 0.0f};
     for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
-    bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa && g.muR > 85.0f);
+    bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa == 1 && g.muR > 85.0f);
     if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
   }
 }
 
 // after the source sample (walk_on_stars.h:270-327)
-template <int DIM>
+template <int DIM, bool RB>
 __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G, const DevParams& prm,
                                               float& dirichletDist,
-                                              Pcg32& smp, Gfn<DIM>& g, WalkState<DIM>& st, const float* dir,
+                                              Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, const float* dir,
                                               bool hit, const Hit& ip, const float* sp) {
   if (!prm.ignore_source) {
     if (g.r <= ip.d) {
@@ -2281,7 +2437,7 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 // 2D keeps the per-lane loop: measured faster for first balls, r1d);
 // lanes with active == false run pair 0's arithmetic for nothing (helping the
 // cooperative sampler) and write and count nothing.
-template <int DIM>
+template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
                                             bool active, int w, int64_t t0, bool yuk0, uint32_t* iters,
@@ -2298,17 +2454,17 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
   // the first ball (centre x, radius firstR) is the same for both members: its
   // Bessel constants are evaluated once (identical values either way)
-  Gfn<DIM> g0;
+  Gfn<DIM, RB> g0;
   g0.init(yuk0, sc.absorption);
 #if WOS_ABL_FB == 1
-  { const bool y = g0.yukawa; g0.yukawa = false; g0.update_ball(x, firstR); g0.yukawa = y;
+  { const int y = g0.yukawa; g0.yukawa = 0; g0.update_ball(x, firstR, false); g0.yukawa = y;
     g0.muR = firstR * g0.sqrtLambda; g0.A0 = 0.5f; g0.A1 = 1.5f; g0.B0 = 0.3f; g0.B1 = 0.7f; }
 #else
-  g0.update_ball(x, firstR);
+  g0.update_ball(x, firstR, prm.robust != 0);
 #endif
   for (int a = 0; a < prm.n_anti; a++) {
     const int64_t t = t0 + a;
-    Gfn<DIM> g = g0;
+    Gfn<DIM, RB> g = g0;
     float throughput = 1.0f, totalSource = 0.0f, firstSource = 0.0f;
     float sdir[DIM], bdir[DIM];
     for (int k = 0; k < DIM; k++) sdir[k] = 0.0f;
@@ -2317,7 +2473,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
         float dir[DIM];
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
         if constexpr (DIM == 3)
-          sample_volume_wave<DIM>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
+          sample_volume_wave<DIM, RB, true>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
         else
           sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, true);
       } else {
@@ -2503,7 +2659,9 @@ constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the
 #ifndef WOS_FB_WAVES_PER_EU
 #define WOS_FB_WAVES_PER_EU 1
 #endif
-template <int DIM, bool GG>
+// RB: robust float semantics (DevParams::robust; Gfn::scaled) -- separate instantiations
+// (wos_robust.hip), so the reference-semantics kernels carry none of its code
+template <int DIM, bool GG, bool RB = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
@@ -2618,7 +2776,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
     const float firstR = 0.99f * smin(dDist, nDist);
     for (int w0 = 0; w0 < npairs; w0 += kWave) {
       const int w = w0 + lane;
-      first_balls<DIM>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
+      first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
                        (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
     }
     DIAG_ADD(D_FB_BALLS, t_fb2);
@@ -2669,7 +2827,7 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // BSTART: the tasks are boundary-start walks (estimateSolution, walk_on_stars.h:353-464:
 // start normal, first sphere radius, on-Neumann flag from DevTasks::n0/r0/sflags, no
 // first ball, walk stream tag 6) -- boundary value caching (wos_bvc.hip).
-template <int DIM, bool GG, bool BSTART = false>
+template <int DIM, bool GG, bool BSTART = false, bool RB = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK_WAVES_PER_EU))) void wos_walk_kernel(
     const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
@@ -2754,7 +2912,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_WALK
   int64_t t = -1;           // this lane's task
   int wmax = 0;             // longest live walk of the wave (steps), wave-uniform
   WalkState<DIM> st;
-  Gfn<DIM> g;
+  Gfn<DIM, RB> g;
   Pcg32 ws;
   float ddist = 0.0f;
   uint32_t wsteps = 0;

@@ -5,6 +5,7 @@
 // order (wos_lpt_*), the persistent wos_walk_kernel and wos_fold_kernel (statistics
 // + masked outputs), all on the caller's stream.
 #include "wos_device.h"
+#include "wos_launch.h"
 
 namespace wos {
 
@@ -109,6 +110,9 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                               unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
                               hipStream_t s) {
+  if (prm.robust)
+    return launch_first_balls_rb(dim, sc, prm, pts, n, base, stride, tk, counters, work, grid, shmem, geom_floats,
+                                 lhs_floats, s);
 #define WOS_LAUNCH_FB(D, G)                                                                                  \
   hipLaunchKernelGGL((wos_first_ball_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, \
                      tk, counters, work, geom_floats, lhs_floats)
@@ -131,6 +135,8 @@ hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s) {
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                         int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
                         int geom_floats, hipStream_t s) {
+  if (prm.robust)
+    return launch_walks_rb(dim, false, sc, prm, tk, base, stride, counters, tqueue, grid, shmem, geom_floats, s);
 #define WOS_LAUNCH_WALK(D, G)                                                                                   \
   hipLaunchKernelGGL((wos_walk_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters, \
                      tqueue, geom_floats)
@@ -160,7 +166,8 @@ size_t first_ball_wave_lds_bytes(int lhs_floats) {
 
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
-hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks) {
+hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks, bool robust) {
+  if (robust) return occupancy_rb(which, dim, geom_global, shmem, blocks);
   if (which == 0) {
     if (dim == 2)
       return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, true>, kBlock, shmem)

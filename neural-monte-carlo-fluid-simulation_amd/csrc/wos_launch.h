@@ -28,8 +28,10 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
 size_t first_ball_wave_lds_bytes(int lhs_floats);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
-// which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry)
-hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks);
+// which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry);
+// robust: the robust-float instantiations (wos_robust.hip)
+hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks,
+                                   bool robust = false);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
 
@@ -41,9 +43,20 @@ hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const floa
 hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                                int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                                size_t shmem, int geom_floats, hipStream_t s);
-hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks);
+hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks, bool robust = false);
 hipError_t launch_bvc_fold(const DevTasks& tk, int64_t nb, float* sol, int32_t* nest, hipStream_t s);
 hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const float* edd, const float* end_,
                             const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
                             float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s);
+// robust float semantics (wos_robust.hip): the same launches with Gfn<DIM, true>;
+// the launchers above dispatch here when prm.robust is set
+hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                                 int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
+                                 unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
+                                 hipStream_t s);
+hipError_t launch_walks_rb(int dim, bool bstart, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
+                           int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
+                           size_t shmem, int geom_floats, hipStream_t s);
+// which: 0 first-ball, 1 walk, 2 boundary-start walk
+hipError_t occupancy_rb(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 }  // namespace wos

@@ -86,6 +86,7 @@ struct DevParams {
   int32_t ignore_dirichlet;
   int32_t ignore_neumann;
   int32_t ignore_source;
+  int32_t robust;           // wos_solver_params.robust_float (Gfn::scaled)
   uint64_t seed;
   // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
   // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the

@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 5  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 6  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
@@ -55,6 +55,7 @@ class SolverParams(C.Structure):
         ("use_cosine_sampling", C.c_int32), ("ignore_dirichlet", C.c_int32),
         ("ignore_neumann", C.c_int32), ("ignore_source", C.c_int32),
         ("seed", C.c_uint64),
+        ("robust_float", C.c_int32),
     ]
 
 

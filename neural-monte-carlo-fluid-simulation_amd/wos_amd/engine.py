@@ -62,6 +62,8 @@ def solver_params(solver=None, output=None, seed=None):
     p.ignore_neumann = int(bool(s.get("ignoreNeumann", False)))
     p.ignore_source = int(bool(s.get("ignoreSource", False)))
     p.seed = int(seed if seed is not None else s.get("seed", _DEFAULT_SEED)) & 0xFFFFFFFFFFFFFFFF
+    # extension key (no reference analogue): robust float semantics, SURVEY.md 7.2 hard part 4
+    p.robust_float = int(bool(s.get("robustFloatSemantics", False)))
     return p
 
 

@@ -56,6 +56,10 @@
 /* math mode                                                                 */
 /* ------------------------------------------------------------------------- */
 static __thread int g_libm = 0;
+/* robust float semantics (oracle_params.robust_float): Yukawa balls with mu R > ROBUST_MUR
+ * use exponentially scaled Bessels and ratios (SURVEY.md section 7.2 hard part 4) */
+static __thread int g_robust = 0;
+#define ROBUST_MUR 80.0f
 
 static inline double m_exp(double x) { return g_libm ? exp(x) : dm_exp(x); }
 static inline double m_log(double x) { return g_libm ? log(x) : dm_log(x); }
@@ -152,6 +156,43 @@ static double bessk1(double x)
               + y * (0.325614e-2 + y * (-0.68245e-3)))))));
     }
     return ans;
+}
+
+/* Robust mode: exponentially scaled A&S functions ie_v(x) = e^-x I_v(x), ke_v(x) =
+ * e^x K_v(x), x > 0 -- the polynomials above without the exponential (large x) or
+ * times the compensating exponential (small x), so nothing overflows for any x. */
+static void bess_scaled(double x, double *ie0, double *ke0, double *ie1, double *ke1)
+{
+    if (x < 3.75) {
+        double e = m_exp(-x);
+        *ie0 = bessi0(x) * e;
+        *ie1 = bessi1(x) * e;
+    } else {
+        double y = 3.75 / x, sx = sqrt(x);
+        *ie0 = (0.39894228 + y * (0.1328592e-1 + y * (0.225319e-2 + y * (-0.157565e-2 + y * (0.916281e-2
+               + y * (-0.2057706e-1 + y * (0.2635537e-1 + y * (-0.1647633e-1 + y * 0.392377e-2)))))))) / sx;
+        double a = 0.2282967e-1 + y * (-0.2895312e-1 + y * (0.1787654e-1 - y * 0.420059e-2));
+        a = 0.39894228 + y * (-0.3988024e-1 + y * (-0.362018e-2 + y * (0.163801e-2 + y * (-0.1031555e-1 + y * a))));
+        *ie1 = a / sx;
+    }
+    if (x <= 2.0) {
+        double e = m_exp(x);
+        *ke0 = bessk0(x) * e;
+        *ke1 = bessk1(x) * e;
+    } else {
+        double y = 2.0 / x, sx = sqrt(x);
+        *ke0 = (1.25331414 + y * (-0.7832358e-1 + y * (0.2189568e-1 + y * (-0.1062446e-1 + y * (0.587872e-2
+               + y * (-0.251540e-2 + y * 0.53208e-3)))))) / sx;
+        *ke1 = (1.25331414 + y * (0.23498619 + y * (-0.3655620e-1 + y * (0.1504268e-1 + y * (-0.780353e-2
+               + y * (0.325614e-2 + y * (-0.68245e-3))))))) / sx;
+    }
+}
+
+/* 3D: e^-x I_{3/2}-like member scaled: (cosh x - sinh x / x) e^-x */
+static inline double i32s(double x)
+{
+    double e2 = m_exp(-2.0 * x);
+    return 0.5 * ((1.0 + e2) - (1.0 - e2) / x);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -764,6 +805,7 @@ typedef struct {
     float lambda, sqrtLambda;
     float muR, K0muR, I0muR, K1muR, I1muR;       /* 2D */
     float expmuR, sinhmuR, K32muR, I32muR;       /* 3D */
+    int scaled;  /* robust mode, mu R > ROBUST_MUR: 2D members hold ke0 ie0 ke1 ie1 of mu R */
 } gfn_t;
 
 static void gfn_init(gfn_t *g, int dim, int yukawa, float lambda)
@@ -780,6 +822,15 @@ static void gfn_update_ball(gfn_t *g, const float *c, float R)
     g->R = R; g->r = 0.0f; g->rClamp = 1e-4f;
     if (!g->yukawa) return;
     g->muR = R * g->sqrtLambda;
+    g->scaled = g_robust && g->muR > ROBUST_MUR;
+    if (g->scaled) {  /* 3D scaled balls evaluate everything from mu R */
+        if (g->dim == 2) {
+            double ie0, ke0, ie1, ke1;
+            bess_scaled((double)g->muR, &ie0, &ke0, &ie1, &ke1);
+            g->K0muR = (float)ke0; g->I0muR = (float)ie0; g->K1muR = (float)ke1; g->I1muR = (float)ie1;
+        }
+        return;
+    }
     if (g->dim == 2) {
         g->K0muR = (float)bessk0((double)g->muR);
         g->I0muR = (float)bessi0((double)g->muR);
@@ -795,8 +846,28 @@ static void gfn_update_ball(gfn_t *g, const float *c, float R)
     }
 }
 
+/* robust-mode forms of the members below (g->scaled): the reference's expressions
+ * rewritten with ie/ke and e^{2(mu r - mu R)} <= 1, in double, rounded where the
+ * reference rounds its result */
+static double scaled_q0(const gfn_t *g, float mur)  /* 2D K0(mur) - I0(mur) K0(muR)/I0(muR); 3D e^-mur - e^-muR sinh(mur)/sinh(muR) */
+{
+    double x = (double)mur, X = (double)g->muR;
+    if (g->dim == 2) {
+        double ie0, ke0, ie1, ke1;
+        bess_scaled(x, &ie0, &ke0, &ie1, &ke1);
+        return m_exp(-x) * (ke0 - ie0 * ((double)g->K0muR / (double)g->I0muR) * m_exp(2.0 * (x - X)));
+    }
+    return m_exp(-x) - m_exp(x - 2.0 * X) * (1.0 - m_exp(-2.0 * x)) / (1.0 - m_exp(-2.0 * X));
+}
+
 static float gfn_evaluate(const gfn_t *g)
 {
+    if (g->yukawa && g->scaled) {
+        float mur = g->r * g->sqrtLambda;
+        double q = scaled_q0(g, mur);
+        if (g->dim == 2) return (float)(q / TWO_PI_D);
+        return (float)(q / (FOUR_PI_D * (double)g->r));
+    }
     float r = g->r, R = g->R;
     if (!g->yukawa) {
         if (g->dim == 2) return (float)((double)m_logf(R / r) / TWO_PI_D);
@@ -816,6 +887,11 @@ static float gfn_evaluate(const gfn_t *g)
 static float gfn_poisson_kernel(const gfn_t *g)
 {
     if (!g->yukawa) return g->dim == 2 ? (float)(1.0 / TWO_PI_D) : (float)(1.0 / FOUR_PI_D);
+    if (g->scaled) {
+        double X = (double)g->muR;
+        if (g->dim == 2) return (float)(m_exp(-X) / (TWO_PI_D * (double)g->I0muR));
+        return (float)(X * 2.0 * m_exp(-X) / (FOUR_PI_D * (1.0 - m_exp(-2.0 * X))));
+    }
     if (g->dim == 2) return (float)(1.0 / (TWO_PI_D * (double)g->I0muR));
     return (float)((double)g->muR / (FOUR_PI_D * (double)g->sinhmuR));
 }
@@ -836,6 +912,17 @@ static float gfn_gradient_norm(const gfn_t *g)
         float r3 = r * r * r; return (float)((double)(1.0f / r3 - 1.0f / (R * R * R)) / FOUR_PI_D);
     }
     float mur = r * g->sqrtLambda;
+    if (g->scaled) {
+        double x = (double)mur, X = (double)g->muR, t = m_exp(2.0 * (x - X)), q;
+        if (g->dim == 2) {
+            double ie0, ke0, ie1, ke1;
+            bess_scaled(x, &ie0, &ke0, &ie1, &ke1);
+            q = m_exp(-x) * (ke1 - ie1 * ((double)g->K1muR / (double)g->I1muR) * t);
+            return (float)((double)g->sqrtLambda * q / (TWO_PI_D * (double)r));
+        }
+        q = m_exp(-x) * ((1.0 + 1.0 / x) - i32s(x) * ((1.0 + 1.0 / X) / i32s(X)) * t);
+        return (float)((double)g->sqrtLambda * q / (FOUR_PI_D * (double)(r * r)));
+    }
     if (g->dim == 2) {
         float K1mur = (float)bessk1((double)mur);
         float I1mur = (float)bessi1((double)mur);
@@ -872,6 +959,13 @@ static void gfn_poisson_kernel_gradient(const gfn_t *g, float *out)
         }
         return;
     }
+    if (g->scaled) {
+        double X = (double)g->muR;
+        float QR = g->dim == 2 ? (float)((double)g->sqrtLambda * m_exp(-X) / ((double)g->R * (double)g->I1muR))
+                               : (float)((double)g->lambda * m_exp(-X) / i32s(X));
+        for (int k = 0; k < g->dim; k++) out[k] = (d[k] * QR) / (float)(g->dim == 2 ? TWO_PI_D : FOUR_PI_D);
+        return;
+    }
     if (g->dim == 2) {
         float QR = g->sqrtLambda / (g->R * g->I1muR);
         for (int k = 0; k < 2; k++) out[k] = (d[k] * QR) / (float)TWO_PI_D;
@@ -887,6 +981,17 @@ static float gfn_dir_sampled_poisson_kernel(const gfn_t *g, const float *y)
     float d[3] = {0, 0, 0}; for (int k = 0; k < g->dim; k++) d[k] = y[k] - g->c[k];
     float r = smaxf(g->rClamp, norm3(d));
     float mur = r * g->sqrtLambda;
+    if (g->scaled) {
+        double x = (double)mur, X = (double)g->muR, t = m_exp(2.0 * (x - X)), q;
+        if (g->dim == 2) {
+            double ie0, ke0, ie1, ke1;
+            bess_scaled(x, &ie0, &ke0, &ie1, &ke1);
+            q = ke1 + ie1 * ((double)g->K0muR / (double)g->I0muR) * t;
+        } else {
+            q = (1.0 + 1.0 / x) + i32s(x) * (2.0 / (1.0 - m_exp(-2.0 * X))) * t;
+        }
+        return (float)(x * m_exp(-x) * q);
+    }
     if (g->dim == 2) {
         float K1mur = (float)bessk1((double)mur);
         float I1mur = (float)bessi1((double)mur);
@@ -917,6 +1022,11 @@ static float gfn_evaluate_xy(const gfn_t *g, const float *x, const float *y)
     float r1 = smaxf(g->rClamp, norm3(yx));
     float r2 = (R * R - dot3(xc, yc)) / R;
     float mur1 = r1 * g->sqrtLambda, mur2 = r2 * g->sqrtLambda;
+    if (g->scaled) {
+        double q1 = scaled_q0(g, mur1), q2 = scaled_q0(g, mur2);
+        if (g->dim == 2) return (float)((q1 - q2) / TWO_PI_D);
+        return (float)((q1 / (double)r1 - q2 / (double)r2) / FOUR_PI_D);
+    }
     if (g->dim == 2) {
         float K0mur1 = (float)bessk0((double)mur1), K0mur2 = (float)bessk0((double)mur2);
         float I0mur1 = (float)bessi0((double)mur1), I0mur2 = (float)bessi0((double)mur2);
@@ -1014,7 +1124,7 @@ typedef struct {
 static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float R, const float *rn)
 {
     const geom_t *ng = &sc->neu;
-    int nonfinite = !isfinite(st->throughput) || (g->yukawa && g->muR > 85.0f);
+    int nonfinite = !isfinite(st->throughput) || (g->yukawa && !g->scaled && g->muR > 85.0f);
     if (!nonfinite || ng->np <= 0) return;
     const float *x = st->pt;
     /* select a primitive overlapping the ball ~ area * |G_harmonic3D(max(d,1e-2))| */
@@ -1380,6 +1490,7 @@ static void *worker(void *arg)
     pcount_t pc; memset(&pc, 0, sizeof(pc));
     uint64_t nest = 0;
     g_libm = J->prm->math_mode == 1;
+    g_robust = J->prm->robust_float != 0;
     for (;;) {
         int64_t i = atomic_fetch_add(&J->next, 16);
         if (i >= J->n) break;
@@ -1404,6 +1515,7 @@ int oracle_solve(const oracle_scene_desc *scene, const oracle_params *prm,
     if (prm->n_walks < 1) return -2;
     scene_t sc;
     g_libm = prm->math_mode == 1;
+    g_robust = prm->robust_float != 0;
     if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
     job_t J; memset(&J, 0, sizeof(J));
     J.sc = &sc; J.prm = prm; J.pts = pts; J.n = n; J.base = index_base; J.stride = index_stride;
@@ -1698,6 +1810,7 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
         bp->n_walks_solution < 1) return -2;
     scene_t sc;
     g_libm = prm->math_mode == 1;
+    g_robust = prm->robust_float != 0;
     if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
     const geom_t *g = &sc.neu;
     recbuf_t rb = {0};

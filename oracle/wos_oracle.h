@@ -61,6 +61,7 @@ typedef struct oracle_params {
     uint64_t seed;            /* counter-based RNG key (replaces system_clock seeds) */
     int32_t math_mode;        /* 0 = det (matches GPU), 1 = glibc libm */
     int32_t n_threads;        /* std thread count for the CPU baseline */
+    int32_t robust_float;     /* 0 = the reference's float members (NaN for mu R > ~92), 1 = robust */
 } oracle_params;
 
 typedef struct oracle_stats {

@@ -38,6 +38,7 @@ class Params(C.Structure):
         ("use_cosine_sampling", C.c_int32), ("ignore_dirichlet", C.c_int32),
         ("ignore_neumann", C.c_int32), ("ignore_source", C.c_int32),
         ("seed", C.c_uint64), ("math_mode", C.c_int32), ("n_threads", C.c_int32),
+        ("robust_float", C.c_int32),
     ]
 
 
@@ -153,6 +154,7 @@ def make_params(solver=None, output=None, *, seed=0x5EED0001, math_mode=0, n_thr
     p.seed = int(s.get("seed", seed))
     p.math_mode = math_mode
     p.n_threads = n_threads or default_threads()
+    p.robust_float = int(bool(s.get("robustFloatSemantics", False)))
     return p
 
 

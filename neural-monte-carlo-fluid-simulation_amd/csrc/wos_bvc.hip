@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void wos_bvc_start_kernel(const DevScene sc
     if (flip) for (int k = 0; k < DIM; k++) n[k] *= -1.0f;
   }
   const bool query = valid && dd > prm.epsilon_shell && prm.steps_before_maximal_spheres != 0;
-  const float starQ = star_radius_wave<DIM>(G, sc, prm, query, x, dd, flip, starL, lane);
+  const float starQ = star_radius_wave<DIM, true>(G, sc, prm, query, x, dd, flip, starL, lane);
   if (!valid) return;
   float r0 = dd;
   if (query) r0 = prm.min_star_radius <= dd ? smax(0.99f * starQ, prm.min_star_radius) : starQ;

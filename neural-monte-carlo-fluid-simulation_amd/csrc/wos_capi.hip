@@ -192,6 +192,7 @@ struct Geom {
   wos::HostScene host;
   float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
   float *d_pgroup = nullptr, *d_sgroup = nullptr, *d_dgroup = nullptr;
+  float *d_ptree = nullptr, *d_stree = nullptr, *d_dtree = nullptr;
   std::mutex mu;  // star grids
   struct Grid {
     float prec, min_r;
@@ -204,6 +205,7 @@ struct Geom {
     hipSetDevice(device);
     hipFree(d_prim); hipFree(d_paux); hipFree(d_sil); hipFree(d_dprim); hipFree(d_dpaux);
     hipFree(d_pgroup); hipFree(d_sgroup); hipFree(d_dgroup);
+    hipFree(d_ptree); hipFree(d_stree); hipFree(d_dtree);
     for (Grid& g : grids) hipFree(g.d);
   }
 };
@@ -260,6 +262,9 @@ int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
   HIP_TRY(upload(&g->d_pgroup, g->host.pgroup));
   HIP_TRY(upload(&g->d_dgroup, g->host.dgroup));
   HIP_TRY(upload(&g->d_sgroup, g->host.sgroup));
+  HIP_TRY(upload(&g->d_ptree, g->host.ptree.node));
+  HIP_TRY(upload(&g->d_stree, g->host.stree.node));
+  HIP_TRY(upload(&g->d_dtree, g->host.dtree.node));
   {
     std::lock_guard<std::mutex> lk(g_geom_mu);
     g_geom_lru.insert(g_geom_lru.begin(), g);
@@ -422,6 +427,16 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   ds.source = s->d_source;
   ds.pgroup = geom->d_pgroup; ds.sgroup = geom->d_sgroup; ds.dgroup = geom->d_dgroup;
   ds.n_pgroups = h.n_pgroups; ds.n_sgroups = h.n_sgroups; ds.n_dgroups = h.n_dgroups;
+  auto tree = [](const wos::HostTree& ht, const float* dnode) {
+    wos::DevTree t{};
+    t.node = dnode;
+    t.levels = ht.levels;
+    for (int l = 0; l <= wos::kTreeLevels; l++) { t.n[l] = ht.n[l]; t.off[l] = ht.off[l]; }
+    return t;
+  };
+  ds.ptree = tree(h.ptree, geom->d_ptree);
+  ds.stree = tree(h.stree, geom->d_stree);
+  ds.dtree = tree(h.dtree, geom->d_dtree);
   const int nsd = d->dim == 2 ? 2 : 3;
   for (int k = 0; k < 3; k++) {
     ds.sdims[k] = d->source ? (k < nsd ? d->source_dims[k] : 1) : 0;

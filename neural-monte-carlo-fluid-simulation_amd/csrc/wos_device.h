@@ -226,6 +226,19 @@ __device__ __forceinline__ float cp_prim(const float* P, const float* x, float* 
   else return cp_triangle(P, P + 3, P + 6, x, pt, t0, t1);
 }
 
+// Squared distance from x to a padded group box: below the computed distance of
+// every member (the padding dwarfs the rounding of both), so skipping a group whose
+// bound exceeds the running minimum never skips the scan's result.
+template <int DIM>
+__device__ __forceinline__ float box_dist2(const float* B, const float* x) {
+  float d2 = 0.0f;
+  for (int k = 0; k < DIM; k++) {
+    const float e = smax(smax(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
+    d2 += e * e;
+  }
+  return d2;
+}
+
 struct Closest { float d; float p[3]; float t0, t1; int prim; };
 
 // Wave-cooperative closest point over `np` primitives (key fl(d*d), last index
@@ -239,6 +252,62 @@ __device__ Closest closest_wave(const float* prims, int np, const float* x, int 
     float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
     float d2 = d * d;
     if (d2 <= bk) { bk = d2; bi = p; }
+  }
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    float ok = __shfl_xor(bk, off);
+    int oi = __shfl_xor(bi, off);
+    if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
+  }
+  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
+  c.p[0] = c.p[1] = c.p[2] = 0.0f;
+  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
+  return c;
+}
+
+// The same query for scenes with many groups (global-memory geometry): the group of
+// the smallest box bound is evaluated first for a running minimum, then every group
+// whose bound does not exceed it (lanes take groups by stride) -- the brute-force
+// result (min fl(d*d), last index on ties).
+template <int DIM>
+__device__ Closest closest_wave_grouped(const float* prims, const float* groups, int np, int ng, const float* x,
+                                        int lane) {
+  constexpr int PS = Layout<DIM>::prim;
+  float lbm = kFltMax;
+  int gm = 0x7FFFFFFF;
+  for (int g = lane; g < ng; g += kWave) {
+    const float lb = box_dist2<DIM>(groups + g * kGroupStride, x);
+    if (lb < lbm) { lbm = lb; gm = g; }
+  }
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const float ol = __shfl_xor(lbm, off);
+    const int og = __shfl_xor(gm, off);
+    if (ol < lbm || (ol == lbm && og < gm)) { lbm = ol; gm = og; }
+  }
+  float bk = kFltMax;
+  int bi = -1;
+  if (lane < kGroup && gm != 0x7FFFFFFF) {
+    const int p = gm * kGroup + lane;
+    if (p < np) {
+      float pt[DIM], t0, t1;
+      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+      bk = d * d;
+      bi = p;
+    }
+  }
+  float sr2 = bk;
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const float o = __shfl_xor(sr2, off);
+    sr2 = o < sr2 ? o : sr2;
+  }
+  for (int g = lane; g < ng; g += kWave) {
+    if (box_dist2<DIM>(groups + g * kGroupStride, x) > sr2) continue;
+    const int p1 = (g + 1) * kGroup < np ? (g + 1) * kGroup : np;
+    for (int p = g * kGroup; p < p1; p++) {
+      float pt[DIM], t0, t1;
+      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+      const float d2 = d * d;
+      if (d2 < bk || (d2 == bk && p > bi)) { bk = d2; bi = p; }
+    }
   }
   for (int off = kWave / 2; off > 0; off >>= 1) {
     float ok = __shfl_xor(bk, off);
@@ -292,18 +361,55 @@ __device__ __forceinline__ float bbox_far_dist(const DevScene& sc, const float* 
   return __builtin_sqrtf(dotv<DIM>(m, m));
 }
 
-// per-lane (non-cooperative) closest distance to the Dirichlet boundary
-// Squared distance from x to a padded group box: below the computed distance of
-// every member (the padding dwarfs the rounding of both), so skipping a group whose
-// bound exceeds the running minimum never skips the scan's result.
-template <int DIM>
-__device__ __forceinline__ float box_dist2(const float* B, const float* x) {
-  float d2 = 0.0f;
-  for (int k = 0; k < DIM; k++) {
-    const float e = smax(smax(B[k] - x[k], x[k] - B[4 + k]), 0.0f);
-    d2 += e * e;
+// ---------------------------------------------------------------------------
+// Implicit 8-ary tree over a group array (DevTree, wos_scene.h).  A cursor (L, i)
+// walks it depth-first in increasing group order without a stack: the siblings of
+// node (L, i) are the aligned block 8 (i / 8) .. + 7 of level L, its parent is
+// (L + 1, i / 8) and its children (L - 1, 8 i ..).  L = -1: done.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int tree_count(const DevTree& t, int L) {
+  int v = t.n[0];
+#pragma unroll
+  for (int l = 1; l <= kTreeLevels; l++) v = L == l ? t.n[l] : v;
+  return v;
+}
+
+__device__ __forceinline__ const float* tree_node(const DevTree& t, int L, int i) {
+  int off = 0;
+#pragma unroll
+  for (int l = 1; l <= kTreeLevels; l++) off = L == l ? t.off[l] : off;
+  return t.node + (size_t)(off + i) * kGroupStride;
+}
+
+// the first group of node (L, i)
+__device__ __forceinline__ int tree_first(int L, int i) { return i << (3 * L); }
+
+// Advances the cursor to the next group g < limit accepted by leaf_ok(g) inside
+// subtrees whose boxes node_ok(box) accepts; returns g, or -1 with the cursor parked
+// at the first node starting at or beyond `limit` (or done).
+template <class NodeOk, class LeafOk>
+__device__ __forceinline__ int tree_next(const DevTree& t, int& L, int& i, int limit, NodeOk node_ok,
+                                         LeafOk leaf_ok) {
+  const int top = t.levels;
+  while (L >= 0) {
+    if (tree_first(L, i) >= limit) return -1;
+    const bool ok = L == 0 ? leaf_ok(i) : node_ok(tree_node(t, L, i));
+    if (ok && L > 0) { L--; i <<= 3; continue; }
+    const int found = ok ? i : -1;
+    i++;
+    while (L < top && ((i & 7) == 0 || i >= tree_count(t, L))) { i = ((i - 1) >> 3) + 1; L++; }
+    if (L == top && i >= tree_count(t, L)) L = -1;
+    if (found >= 0) return found;
   }
-  return d2;
+  return -1;
+}
+
+__device__ __forceinline__ int wave_min_int(int v) {
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const int o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
 }
 
 // computeDistToDirichlet (fcpw_scene_loader.h:299-315) over the Dirichlet
@@ -318,6 +424,46 @@ __device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, c
   if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
   constexpr int PS = Layout<DIM>::prim;
   const int ng = sc.n_dgroups;
+  if (sc.dtree.levels > 0) {
+    // hierarchy: the greedy descent to the nearest-bound leaf gives a tight running
+    // minimum, then the depth-first walk visits every group whose bound does not
+    // exceed it (re-visiting that leaf changes nothing): the same primitive
+    const DevTree& T = sc.dtree;
+    float sr2 = kFltMax, best = kFltMax;
+    int bestp = -1;
+    auto eval_group = [&](int gi) {
+      const int p1 = (gi + 1) * kGroup < sc.n_dprims ? (gi + 1) * kGroup : sc.n_dprims;
+      for (int p = gi * kGroup; p < p1; p++) {
+        float pt[DIM], t0, t1;
+        const float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
+        const float d2 = d * d;
+        if (d2 < sr2 || (d2 == sr2 && p > bestp)) { sr2 = d2; best = d; bestp = p; }
+      }
+    };
+    {
+      int L = T.levels, i0 = 0;
+      while (true) {
+        const int n = tree_count(T, L), i1 = (i0 + 8) < n ? i0 + 8 : n;
+        int bi = i0;
+        float bl = kFltMax;
+        for (int i = i0; i < i1; i++) {
+          const float lb = box_dist2<DIM>(L == 0 ? dgroup + i * kGroupStride : tree_node(T, L, i), x);
+          if (lb < bl) { bl = lb; bi = i; }
+        }
+        if (L == 0) { eval_group(bi); break; }
+        L--;
+        i0 = bi << 3;
+      }
+    }
+    int L = T.levels, i = 0;
+    while (L >= 0) {
+      const int g = tree_next(T, L, i, 0x7FFFFFFF,
+                              [&](const float* B) { return !(box_dist2<DIM>(B, x) > sr2); },
+                              [&](int gi) { return !(box_dist2<DIM>(dgroup + gi * kGroupStride, x) > sr2); });
+      if (g >= 0) eval_group(g);
+    }
+    return best;
+  }
   int g0 = 0;
   float lb0 = kFltMax;
   for (int gi = 0; gi < ng; gi++) {
@@ -2000,7 +2146,9 @@ __device__ __forceinline__ bool ray_prim_filtered(const float* P, const float* o
 }
 
 // Convergent: every lane of the wave calls it; lanes with active == false get false.
-template <int DIM>
+// TREE: the primitive-group hierarchy (sc.ptree) replaces the flat group scan when the
+// scene has one (the global-memory geometry instantiation).
+template <int DIM, bool TREE = false>
 __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc, bool active, const float* o,
                                              const float* dir, float tmax, Hit* h, RayLDS<DIM>* L, int lane) {
   constexpr int PS = Layout<DIM>::prim;
@@ -2014,12 +2162,30 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
     L->rt[lane] = tmax;
     L->best[lane] = ~0ull;
   }
-  for (int g0 = 0; g0 < ng; g0 += kRayChunk) {
+  const bool tree = TREE && sc.ptree.levels > 0;
+  int cL = (tree && need) ? sc.ptree.levels : -1, ci = 0;
+  for (int g0 = 0;; g0 += kRayChunk) {
     uint32_t mask = 0;
-    if (need) {
-      const int gn = (ng - g0) < kRayChunk ? (ng - g0) : kRayChunk;
-      for (int j = 0; j < gn; j++)
-        if (ray_box_maybe<DIM>(G.pgroup + (g0 + j) * kGroupStride, o, inv, tmax)) mask |= 1u << j;
+    if (tree) {
+      // the window of kRayChunk groups starting at the lowest cursor of the wave; each
+      // lane's cursor emits its accepted groups inside it (increasing order)
+      g0 = wave_min_int(cL >= 0 ? tree_first(cL, ci) : 0x7FFFFFFF);
+      if (g0 == 0x7FFFFFFF) break;
+      if (cL >= 0) {
+        int gi;
+        while ((gi = tree_next(
+                    sc.ptree, cL, ci, g0 + kRayChunk,
+                    [&](const float* B) { return ray_box_maybe<DIM>(B, o, inv, tmax); },
+                    [&](int q) { return ray_box_maybe<DIM>(G.pgroup + q * kGroupStride, o, inv, tmax); })) >= 0)
+          mask |= 1u << (gi - g0);
+      }
+    } else {
+      if (g0 >= ng) break;
+      if (need) {
+        const int gn = (ng - g0) < kRayChunk ? (ng - g0) : kRayChunk;
+        for (int j = 0; j < gn; j++)
+          if (ray_box_maybe<DIM>(G.pgroup + (g0 + j) * kGroupStride, o, inv, tmax)) mask |= 1u << j;
+      }
     }
     const uint32_t cnt = (uint32_t)__popc(mask);
     uint32_t incl = cnt;
@@ -2189,7 +2355,8 @@ __device__ __forceinline__ float star_candidate_dist(const LGeom& G, int s, cons
 }
 
 // Convergent: every lane of the wave calls it.  Lanes with query == false get 0.
-template <int DIM>
+// TREE: the silhouette-group hierarchy (sc.stree) replaces the flat group scan.
+template <int DIM, bool TREE = false>
 __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene& sc, const DevParams& prm,
                                                   bool query, const float* x, float maxR, bool flipOrient,
                                                   StarLDS<DIM>* L, int lane) {
@@ -2273,13 +2440,31 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
   }
   const bool scan_groups = need && !use_cell;
   const int nsg = sc.n_sgroups, ns = sc.n_sil;
-  for (int g0 = 0; g0 < nsg && __ballot(scan_groups) != 0; g0 += kStarChunk) {
+  const bool tree = TREE && sc.stree.levels > 0;
+  int cL = (tree && scan_groups) ? sc.stree.levels : -1, ci = 0;
+  for (int g0 = 0; __ballot(scan_groups) != 0; g0 += kStarChunk) {
     uint32_t mask = 0;
-    if (scan_groups) {
-      const int gn = (nsg - g0) < kStarChunk ? (nsg - g0) : kStarChunk;
-      for (int j = 0; j < gn; j++) {
-        const float* B = G.sgroup + (g0 + j) * kSGroupStride;
-        if (ball_box_maybe<DIM>(B, x, r2) && !cone_culled<DIM>(B, x, prec)) mask |= 1u << j;
+    if (tree) {
+      g0 = wave_min_int(cL >= 0 ? tree_first(cL, ci) : 0x7FFFFFFF);
+      if (g0 == 0x7FFFFFFF) break;
+      if (cL >= 0) {
+        int gi;
+        while ((gi = tree_next(
+                    sc.stree, cL, ci, g0 + kStarChunk, [&](const float* B) { return ball_box_maybe<DIM>(B, x, r2); },
+                    [&](int q) {
+                      const float* B = G.sgroup + q * kSGroupStride;
+                      return ball_box_maybe<DIM>(B, x, r2) && !cone_culled<DIM>(B, x, prec);
+                    })) >= 0)
+          mask |= 1u << (gi - g0);
+      }
+    } else {
+      if (g0 >= nsg) break;
+      if (scan_groups) {
+        const int gn = (nsg - g0) < kStarChunk ? (nsg - g0) : kStarChunk;
+        for (int j = 0; j < gn; j++) {
+          const float* B = G.sgroup + (g0 + j) * kSGroupStride;
+          if (ball_box_maybe<DIM>(B, x, r2) && !cone_culled<DIM>(B, x, prec)) mask |= 1u << j;
+        }
       }
     }
     const uint32_t cnt = (uint32_t)__popc(mask);
@@ -2766,13 +2951,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
     DIAG_T0(t_fb0);
     float nDist = kFltMax, nSigned = kFltMax;
     if (sc.n_prims > 0) {
-      Closest c = closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
+      Closest c = (GG && sc.n_pgroups > kTreeMinGroups)
+                      ? closest_wave_grouped<DIM>(Lprim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, lane)
+                      : closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
       nDist = c.d;
       nSigned = signed_dist<DIM>(sc.paux, c, x);
     }
     float dDist, dSigned;
     if (sc.n_dprims > 0) {
-      Closest c = closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
+      Closest c = sc.n_dgroups > kTreeMinGroups
+                      ? closest_wave_grouped<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, lane)
+                      : closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
       dDist = c.d;
       dSigned = signed_dist<DIM>(sc.dpaux, c, x);
     } else {
@@ -3065,7 +3254,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     bool flip = false, query = false;
     if (t >= 0) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
     DIAG_T0(t_star);
-    const float starQ = star_radius_wave<DIM>(G, sc, prm, t >= 0 && code < 0 && query, st.pt, ddist, flip,
+    const float starQ = star_radius_wave<DIM, GG>(G, sc, prm, t >= 0 && code < 0 && query, st.pt, ddist, flip,
                                               starL, lane);
     DIAG_ADD(D_STAR, t_star);
     const bool live = t >= 0 && code < 0;
@@ -3077,7 +3266,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     Hit ip;
     DIAG_T0(t_ray);
 #if WOS_RAY_WAVE
-    const bool hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM>(G, sc, live, org, dir, starR, &ip, rayL, lane);
+    const bool hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
 #else
     const bool hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 &&
                      ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);

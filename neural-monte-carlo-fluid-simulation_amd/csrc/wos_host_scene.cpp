@@ -318,7 +318,37 @@ bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
     out.sgroup.insert(out.sgroup.end(), rec, rec + kSGroupStride);
     out.n_sgroups++;
   }
+  build_group_tree(out.pgroup, kGroupStride, out.n_pgroups, out.ptree);
+  build_group_tree(out.sgroup, kSGroupStride, out.n_sgroups, out.stree);
+  build_group_tree(out.dgroup, kGroupStride, out.n_dgroups, out.dtree);
   return true;
+}
+
+void build_group_tree(const std::vector<float>& groups, int stride, int ngroups, HostTree& t) {
+  t = HostTree{};
+  t.n[0] = ngroups;
+  if (ngroups <= kTreeMinGroups) return;
+  // level L's boxes: unions of the 8 consecutive boxes of level L-1 (the padded group
+  // boxes at L = 1), so every node box contains its groups' padded boxes
+  int prev_n = ngroups, L = 0;
+  while (prev_n > 8 && L < kTreeLevels) {
+    L++;
+    const int n = (prev_n + 7) / 8;
+    const size_t base = t.node.size() / kGroupStride;
+    t.off[L] = (int)base;
+    t.n[L] = n;
+    for (int i = 0; i < n; i++) {
+      float lo[3] = {kFltMax, kFltMax, kFltMax}, hi[3] = {-kFltMax, -kFltMax, -kFltMax};
+      for (int c = 8 * i; c < std::min(prev_n, 8 * i + 8); c++) {
+        const float* B = L == 1 ? &groups[(size_t)c * stride] : &t.node[((size_t)t.off[L - 1] + c) * kGroupStride];
+        for (int k = 0; k < 3; k++) { lo[k] = smin(lo[k], B[k]); hi[k] = smax(hi[k], B[4 + k]); }
+      }
+      const float rec[kGroupStride] = {lo[0], lo[1], lo[2], 0.0f, hi[0], hi[1], hi[2], 0.0f};
+      t.node.insert(t.node.end(), rec, rec + kGroupStride);
+    }
+    prev_n = n;
+  }
+  t.levels = L;
 }
 
 // ---------------------------------------------------------------------------

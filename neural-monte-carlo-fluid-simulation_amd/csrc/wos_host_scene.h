@@ -22,12 +22,22 @@ struct HostSceneInput {
   int is_double_sided = 0;
 };
 
+struct HostTree {
+  std::vector<float> node;  // levels 1.. of the implicit 8-ary tree (wos_scene.h DevTree)
+  int levels = 0;
+  int n[kTreeLevels + 1] = {};
+  int off[kTreeLevels + 1] = {};
+};
+// the tree over `ngroups` group records of `stride` floats (box in the first 8)
+void build_group_tree(const std::vector<float>& groups, int stride, int ngroups, HostTree& out);
+
 struct HostScene {
   int dim = 2;
   int n_prims = 0, n_sil = 0, n_dprims = 0;
   std::vector<float> prim, paux, sil, dprim, dpaux;
   std::vector<float> pgroup, sgroup, dgroup;  // culling boxes (kGroupStride floats each)
   int n_pgroups = 0, n_sgroups = 0, n_dgroups = 0;
+  HostTree ptree, stree, dtree;
   float pmin[3] = {0, 0, 0}, pmax[3] = {0, 0, 0}, ext[3] = {0, 0, 0};
 };
 

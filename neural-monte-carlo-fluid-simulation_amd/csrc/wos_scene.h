@@ -31,6 +31,21 @@ constexpr int kSilStride2 = 8, kSilStride3 = 16;
 //   [min.xyz sin(alpha) | max.xyz cos(alpha) | c.xyz rho | axis.xyz nocull]
 constexpr int kGroup = 8, kGroupStride = 8, kSGroupStride = 16;
 
+// Bounding-volume hierarchy over a group array (the role of fcpw's 8-wide MBVH,
+// mbvh.inl:702-818, for meshes far beyond the reference's): an implicit 8-ary tree
+// whose level-0 nodes are the groups and whose node (L, i), L >= 1, bounds the
+// groups [i 8^L, (i+1) 8^L) with the union of their padded boxes ([min pad | max pad],
+// kGroupStride floats).  Levels are built until at most 8 nodes remain; scenes with
+// at most kTreeMinGroups groups get none (levels = 0: the flat group scan).
+constexpr int kTreeLevels = 8;
+constexpr int kTreeMinGroups = 64;
+struct DevTree {
+  const float* node;           // level L's boxes at node + off[L] * kGroupStride (L >= 1)
+  int32_t levels;              // 0: no tree
+  int32_t n[kTreeLevels + 1];  // n[0] = groups, n[L] = nodes of level L
+  int32_t off[kTreeLevels + 1];
+};
+
 template <int DIM> struct Layout;
 template <> struct Layout<2> {
   static constexpr int prim = kPrimStride2, aux = kAuxStride2, sil = kSilStride2;
@@ -52,6 +67,7 @@ struct DevScene {
   const float* sgroup;   // n_sgroups boxes over consecutive silhouette candidates
   const float* dgroup;   // n_dgroups boxes over consecutive Dirichlet primitives
   int32_t n_pgroups, n_sgroups, n_dgroups;
+  DevTree ptree, stree, dtree;  // hierarchies over pgroup / sgroup / dgroup
   // 1: the kernels read the geometry records from global memory (L2) instead of
   // staging them in LDS -- scenes too large for the LDS budget (set per solve)
   int32_t geom_global;

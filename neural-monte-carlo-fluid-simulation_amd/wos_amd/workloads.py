@@ -144,6 +144,37 @@ def box_2d(L=1.0):
     return v, ix
 
 
+def subdivided_cube(k=12, half=1.0):
+    """[-half, half]^3 with every face split into k x k quads (2 k^2 triangles per face),
+    shared vertices, wound like scenes/cube.obj (positive signed volume): a 3D mesh far
+    beyond the LDS budget for the global-memory geometry path and its group hierarchy
+    (no reference analogue: the reference's 3D meshes have 12 triangles)."""
+    axes = {0: np.eye(3)[0], 1: np.eye(3)[1], 2: np.eye(3)[2]}
+    faces = [(0, 1, 2, 1), (0, 2, 1, -1), (1, 2, 0, 1), (1, 0, 2, -1), (2, 0, 1, 1), (2, 1, 0, -1)]
+    index, verts, tris = {}, [], []
+
+    def vid(p):
+        key = tuple(int(round(c * k / half)) for c in p)
+        if key not in index:
+            index[key] = len(verts)
+            verts.append(p)
+        return index[key]
+
+    for n_ax, u_ax, v_ax, sgn in faces:
+        n, u, v = axes[n_ax] * sgn, axes[u_ax], axes[v_ax]
+        g = np.linspace(-half, half, k + 1)
+        for a in range(k):
+            for b in range(k):
+                p00 = n * half + g[a] * u + g[b] * v
+                p10 = n * half + g[a + 1] * u + g[b] * v
+                p11 = n * half + g[a + 1] * u + g[b + 1] * v
+                p01 = n * half + g[a] * u + g[b + 1] * v
+                i00, i10, i11, i01 = vid(p00), vid(p10), vid(p11), vid(p01)
+                tris.append((i00, i10, i11))
+                tris.append((i00, i11, i01))
+    return np.array(verts, np.float32), np.array(tris, np.int32)
+
+
 def circle_2d(c, r, n=64, clockwise=True):
     """Polygonal circle.  Clockwise: normals (s.y,-s.x) point into the disk, i.e. out of
     a fluid that surrounds it (obstacle); counter-clockwise: fluid inside the disk."""

@@ -172,3 +172,19 @@ extern "C" int hs_rej_table(int dim, float* out) {
   wos::rejection_bound_table(dim, out);
   return wos::kRejTabBins;
 }
+
+// ---- group hierarchy (wos_host_scene.cpp build_group_tree) ----
+// out_meta: [levels, n[0..kTreeLevels], off[0..kTreeLevels]]
+extern "C" int hs_group_tree(const float* groups, int stride, int ngroups, float* nodes, int cap, int* out_meta) {
+  std::vector<float> g(groups, groups + (size_t)stride * ngroups);
+  wos::HostTree t;
+  wos::build_group_tree(g, stride, ngroups, t);
+  if ((int)t.node.size() > cap) return -2;
+  std::copy(t.node.begin(), t.node.end(), nodes);
+  out_meta[0] = t.levels;
+  for (int l = 0; l <= wos::kTreeLevels; l++) {
+    out_meta[1 + l] = t.n[l];
+    out_meta[2 + wos::kTreeLevels + l] = t.off[l];
+  }
+  return (int)t.node.size();
+}

@@ -295,6 +295,33 @@ def test_mesh_beyond_lds_bit_exact(gpu, oracle):
     sc.close()
 
 
+def test_mesh3d_beyond_lds_tree_bit_exact(gpu, oracle):
+    """a 3072-triangle cube (subdivided faces; records far beyond the LDS budget): the
+    global-memory geometry path with the group hierarchy (ray, star radius, closest
+    point by group bounds) matches the oracle's brute-force scans"""
+    v, ix = workloads.subdivided_cube(16)
+    cfg = workloads.cube_config(res=6, n_walks=16)
+    osc = oracle.OracleScene(v, ix, cfg["source"], 350.0, watertight=True)
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    _, _, st = _compare(oracle, osc, sc, cfg, cfg["points"])
+    assert st["geom_global"] == 1 and st["points_estimated"] == cfg["points"].shape[0]
+    sc.close()
+
+
+def test_dirichlet_many_segments_tree_bit_exact(gpu, oracle):
+    """a 4096-segment Dirichlet obstacle: the Dirichlet distance through the group
+    hierarchy (nearest-bound descent + pruned depth-first walk) and the grouped closest
+    point match the oracle's sequential scans"""
+    cfg = workloads.dirichlet_obstacle_config(n_walks=16, res=16)
+    dv, dix = workloads.circle_2d((0.5, 0.35), 0.1, 4096)
+    kw = dict(dvertices=dv, dprims=dix, dirichlet_value=1.0, watertight=True)
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
+    _, _, st = _compare(oracle, osc, sc, cfg, cfg["points"])
+    assert st["walks_dirichlet"] > 0
+    sc.close()
+
+
 @pytest.mark.parametrize("which", ["C_dirichlet512", "D_cube128"])
 def test_full_size_configs_properties(gpu, oracle, which):
     """BASELINE configs C (Dirichlet obstacle, 512^2 points x 256 walks) and D (cube,

@@ -220,3 +220,92 @@ def test_cone_culling_is_sound(shim, name):
                 for flip in (True, False):
                     assert not (S[6] != 0 or silhouette_2d(S, x, 1e-3, flip)), (name, gi, x)
     assert culled > 1000  # the test culls a real share of the groups
+
+
+# ---- group hierarchy (wos_scene.h DevTree) -----------------------------------------
+KTREE_LEVELS, KTREE_MIN = 8, 64
+
+
+def _tree(shim, groups, stride):
+    groups = np.ascontiguousarray(groups, np.float32)
+    n = groups.shape[0]
+    cap = 8 * (n + 64)
+    nodes = np.zeros(cap, np.float32)
+    meta = np.zeros(1 + 2 * (KTREE_LEVELS + 1), np.int32)
+    f = C.POINTER(C.c_float)
+    rc = shim.hs_group_tree(groups.ctypes.data_as(f), stride, n, nodes.ctypes.data_as(f), cap,
+                            meta.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc >= 0
+    levels = int(meta[0])
+    cnt = meta[1:2 + KTREE_LEVELS].tolist()
+    off = meta[2 + KTREE_LEVELS:].tolist()
+    return levels, cnt, off, nodes[:rc].reshape(-1, 8)
+
+
+def _tree_next(levels, cnt, L, i, limit, node_ok, leaf_ok):
+    """Python restatement of wos_device.h tree_next (the kernel's stackless cursor)."""
+    while L >= 0:
+        if (i << (3 * L)) >= limit:
+            return -1, L, i
+        ok = leaf_ok(i) if L == 0 else node_ok(L, i)
+        if ok and L > 0:
+            L, i = L - 1, i << 3
+            continue
+        found = i if ok else -1
+        i += 1
+        while L < levels and ((i & 7) == 0 or i >= cnt[L]):
+            i, L = ((i - 1) >> 3) + 1, L + 1
+        if L == levels and i >= cnt[L]:
+            L = -1
+        if found >= 0:
+            return found, L, i
+    return -1, L, i
+
+
+@pytest.mark.parametrize("ngroups", [10, 64, 65, 200, 513, 4099])
+def test_group_tree_contains_and_traverses(shim, ngroups):
+    """node boxes contain their children; the cursor, walked window by window like
+    ray_hit_wave / star_radius_wave, emits exactly the flat scan's accepted groups in
+    increasing order (box-overlap tests: a group's ancestors contain its box)"""
+    rng = np.random.default_rng(ngroups)
+    c = np.cumsum(rng.normal(0, 1, (ngroups, 2)), 0)        # spatially coherent, like a boundary polyline
+    half = rng.uniform(0.1, 1.0, (ngroups, 2))
+    groups = np.zeros((ngroups, 16), np.float32)             # silhouette-group stride (box in the first 8)
+    groups[:, 0:2], groups[:, 4:6] = c - half, c + half
+    levels, cnt, off, nodes = _tree(shim, groups, 16)
+    assert cnt[0] == ngroups
+    if ngroups <= KTREE_MIN:
+        assert levels == 0
+        return
+    assert levels >= 1 and cnt[levels] <= 8
+
+    def box(L, i):
+        return groups[i, :8] if L == 0 else nodes[off[L] + i]
+
+    for L in range(1, levels + 1):
+        assert cnt[L] == (cnt[L - 1] + 7) // 8
+        for i in range(cnt[L]):
+            B = box(L, i)
+            for ch in range(8 * i, min(8 * i + 8, cnt[L - 1])):
+                C_ = box(L - 1, ch)
+                assert np.all(C_[0:3] >= B[0:3]) and np.all(C_[4:7] <= B[4:7])
+    for trial in range(20):
+        q = rng.uniform(c.min(0), c.max(0))
+        r = rng.uniform(0.5, 8.0)
+
+        def overlaps(B):
+            return np.all(B[0:2] <= q + r) and np.all(B[4:6] >= q - r)
+
+        want = [g for g in range(ngroups) if overlaps(groups[g, :8])]
+        got, L, i = [], levels, 0
+        while L >= 0:
+            g0 = i << (3 * L)
+            limit = g0 + 16
+            while True:
+                g, L, i = _tree_next(levels, cnt, L, i, limit, lambda L_, i_: overlaps(box(L_, i_)),
+                                     lambda i_: overlaps(groups[i_, :8]))
+                if g < 0:
+                    break
+                assert g0 <= g < limit
+                got.append(g)
+        assert got == want, trial

@@ -82,7 +82,8 @@ __device__ __forceinline__ void wave_sync() {
 // Diagnostic build only (-DWOS_DIAG=1, never shipped): per-section wave cycles
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
-       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_MID, D_END, D_TAIL, D_NUM };
+       D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_MID, D_END, D_TAIL,
+       D_XITERS, D_XLANES, D_XLOOP, D_NUM };  // X: iterations after the wave's task queue ran dry
 // slots holding maxima (folded with atomicMax)
 __host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 static __device__ unsigned long long g_diag[D_NUM];
@@ -3301,6 +3302,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     }
     refill(tk);
     DIAG_ADD(D_LOOP, t_loop);
+#if WOS_DIAG
+    if (exhausted) {
+      DIAG_COUNT(D_XITERS, 1);
+      DIAG_COUNT(D_XLANES, __popcll(__ballot(t >= 0)));
+      DIAG_ADD(D_XLOOP, t_loop);
+    }
+#endif
   }
 
   DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);

@@ -205,6 +205,9 @@ void diag_dump(const char* tag) {
   fprintf(stderr, "[diag %s] star calls %llu: groups visited/call %.2f, candidates/call %.2f, exact/call %.2f\n", tag,
           d[D_SCALLS], (double)d[D_SGVISIT] / d[D_SCALLS], (double)d[D_SCAND] / d[D_SCALLS],
           (double)d[D_SEXACT] / d[D_SCALLS]);
+  fprintf(stderr, "[diag %s] after the queue ran dry: %llu iterations (%.1f%%), lanes/iter %.2f, %.1f%% of loop cycles\n",
+          tag, d[D_XITERS], 100.0 * d[D_XITERS] / (d[D_ITERS] ? d[D_ITERS] : 1),
+          (double)d[D_XLANES] / (d[D_XITERS] ? d[D_XITERS] : 1), 100.0 * d[D_XLOOP] / (d[D_LOOP] ? d[D_LOOP] : 1));
   unsigned long long z[D_NUM] = {};
   hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
 #else

@@ -553,7 +553,7 @@ constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
 
 int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
   // sized for 3D records so either dimension fits
-  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
+  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3)) + 1;  // + rrng alignment
   if (tasks > c.task_cap) {
     hipFree(c.d_tasks);
     c.d_tasks = nullptr; c.task_cap = 0;
@@ -564,7 +564,7 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
     HIP_TRY(hipMalloc((void**)&c.d_pstate,
-                      ((size_t)2 * points + 2 * wos::kCostBuckets * wos::kMaxPipes) * sizeof(int32_t)));
+                      ((size_t)2 * points + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
@@ -575,7 +575,7 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
 wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, int64_t task_slice,
                         int64_t point_slice) {
   wos::DevTasks tk{};
-  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
+  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3)) + 1;
   float* f = c.d_tasks + (size_t)pipe * task_slice * tf;
   tk.pt = f; f += dim * T;
   tk.thr = f; f += T;
@@ -585,10 +585,21 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, in
   tk.bdir = f; f += dim * T;
   tk.sdir = f; f += dim * T;
   tk.total = f; f += T;
-  tk.code = (uint32_t*)f;
+  tk.code = (uint32_t*)f; f += T;
+  if (((uintptr_t)f & 7u) != 0) f += 1;  // (T even in practice; keep rrng 8-B aligned regardless)
+  tk.rrng = (uint64_t*)f; f += 2 * T;
+  tk.rn = f; f += dim * T;
+  tk.rpd = f; f += dim * T;
+  tk.rpdist = f; f += T;
+  tk.rtn = f; f += T;
+  tk.rwl = (uint32_t*)f; f += T;
+  tk.rsteps = (uint32_t*)f; f += T;
+  tk.surv = (uint32_t*)f;
   tk.pstate = c.d_pstate + pipe * point_slice;
   tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap + pipe * point_slice);
   tk.hist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
+  tk.shist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
+                         pipe * (2 * wos::kCostBuckets + 1));
   tk.T = T;
   tk.wpp = wpp;
   return tk;
@@ -839,6 +850,9 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   const int64_t wpp = (int64_t)dp.n_pairs * dp.n_anti;
   int pipes = 1;
   if (const char* e = std::getenv("WOS_SPLIT")) pipes = std::max(1, std::min(wos::kMaxPipes, std::atoi(e)));
+  // 2: two-phase walks (first step of every task, then the survivors); 1: one persistent pass
+  int phases = 1;
+  if (const char* e = std::getenv("WOS_PHASES")) phases = std::atoi(e) == 2 ? 2 : 1;
   const int64_t slice_tasks = kMaxBatchTasks / pipes;
   int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, slice_tasks / wpp));
   if (pipes > 1 && n > 0) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, (n + pipes - 1) / pipes));
@@ -889,11 +903,15 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     HIP_TRY(hipEventRecord(ev[0], ps));
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
                                     q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, ps));
-    HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
+    if (phases == 1) HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
     HIP_TRY(hipEventRecord(ev[1], ps));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
-    HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
-                              shmem_walk, geom_floats_walk, ps));
+    if (phases == 2)
+      HIP_TRY(wos::launch_walks_two_phase(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
+                                          shmem_walk, geom_floats_walk, ps));
+    else
+      HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
+                                shmem_walk, geom_floats_walk, ps));
     HIP_TRY(hipEventRecord(ev[2], ps));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
                              d_steps ? d_steps + b0 : nullptr, ps));

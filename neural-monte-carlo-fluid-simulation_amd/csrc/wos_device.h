@@ -3038,6 +3038,194 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_W
 }
 
 // ---- kernel 2: walks ---------------------------------------------------------
+// The state a walk task starts from (the hand-out of walk_on_stars.h:494-579 after
+// the first ball; BSTART: estimateSolution's boundary start, :437-439) ...
+template <int DIM, bool BSTART, bool RB>
+__device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t t,
+                                           uint32_t pidx, uint32_t w, const float* v_pt, float v_thr, float v_tsrc,
+                                           float v_dd, int64_t base, int64_t stride, bool yuk0, WalkState<DIM>& st,
+                                           Gfn<DIM, RB>& g, Pcg32& ws, float& ddist, uint32_t& wsteps, float& firstR) {
+  for (int kk = 0; kk < DIM; kk++) { st.pt[kk] = v_pt[kk]; st.n[kk] = 0.0f; st.prevDir[kk] = 0.0f; }
+  // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
+  // and every step rewrites them before that can happen
+  st.prevDist = 0.0f;
+  st.throughput = v_thr;
+  st.onNeumann = false;
+  st.walkLength = 0;
+  st.totalNeumann = 0.0f;
+  st.totalSource = v_tsrc;
+  ddist = v_dd;
+  g.init(yuk0, sc.absorption);
+  if constexpr (BSTART) {
+    // WalkState(pt, currentNormal, prevDirection = normal, FLT_MAX, 1, onNeumann)
+    // (walk_on_stars.h:437-439); walk w of sample pidx on its own stream
+    for (int kk = 0; kk < DIM; kk++) { st.n[kk] = tk.n0[kk * tk.T + t]; st.prevDir[kk] = st.n[kk]; }
+    st.prevDist = kFltMax;
+    st.onNeumann = (tk.sflags[t] & 1u) != 0u;
+    firstR = tk.r0[t];
+    ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 6));
+    wsteps = 0;
+  } else {
+    ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
+    wsteps = 1;  // the first ball
+  }
+}
+
+// ... the complete state of a walk that continues after its first walk-kernel step
+// (two-phase walks: DevTasks r* arrays), and its restoration.  The Green's function
+// carries nothing across steps but its kind, which follows from the walk length
+// (walk_step_tail switches to Yukawa when walkLength reaches steps_before_tikhonov).
+template <int DIM>
+__device__ __forceinline__ void walk_save(const DevTasks& tk, int64_t t, const WalkState<DIM>& st, const Pcg32& ws,
+                                          float ddist, uint32_t wsteps) {
+  const int64_t T = tk.T;
+  for (int k = 0; k < DIM; k++) {
+    tk.pt[k * T + t] = st.pt[k];
+    tk.rn[k * T + t] = st.n[k];
+    tk.rpd[k * T + t] = st.prevDir[k];
+  }
+  tk.thr[t] = st.throughput;
+  tk.tsrc[t] = st.totalSource;
+  tk.dd[t] = ddist;
+  tk.rpdist[t] = st.prevDist;
+  tk.rtn[t] = st.totalNeumann;
+  tk.rwl[t] = (uint32_t)st.walkLength | (st.onNeumann ? 0x80000000u : 0u);
+  tk.rsteps[t] = wsteps;
+  tk.rrng[t] = ws.state;
+  tk.code[t] = kInFlight;
+}
+
+template <int DIM, bool RB>
+__device__ __forceinline__ void walk_resume(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t t,
+                                            WalkState<DIM>& st, Gfn<DIM, RB>& g, Pcg32& ws, float& ddist,
+                                            uint32_t& wsteps) {
+  const int64_t T = tk.T;
+  for (int k = 0; k < DIM; k++) {
+    st.pt[k] = tk.pt[k * T + t];
+    st.n[k] = tk.rn[k * T + t];
+    st.prevDir[k] = tk.rpd[k * T + t];
+  }
+  st.throughput = tk.thr[t];
+  st.totalSource = tk.tsrc[t];
+  ddist = tk.dd[t];
+  st.prevDist = tk.rpdist[t];
+  st.totalNeumann = tk.rtn[t];
+  const uint32_t wl = tk.rwl[t];
+  st.walkLength = (int)(wl & 0x7FFFFFFFu);
+  st.onNeumann = (wl >> 31) != 0u;
+  wsteps = tk.rsteps[t];
+  ws.state = tk.rrng[t];
+  const int sbt = prm.steps_before_tikhonov;
+  g.init(sc.absorption > 0.0f && (sbt == 0 || (sbt > 0 && st.walkLength >= sbt)), sc.absorption);
+}
+
+// computeStarRadius for one lane without the wave: the lane's cell list when the star
+// grid covers it, else the sequential group scan -- star_radius_wave's result.
+template <int DIM>
+__device__ __forceinline__ float star_radius_lane(const LGeom& G, const DevScene& sc, const DevParams& prm,
+                                                  const float* x, float maxR, bool flipOrient) {
+  const float minR = prm.min_star_radius, prec = prm.silhouette_precision;
+  if (minR > maxR) return maxR;
+  const float result = smax(maxR, minR);
+  if (sc.n_prims <= 0) return result;
+  const float r2 = maxR < kFltMax ? maxR * maxR : kFltMax, minR2 = minR * minR;
+  if (minR2 >= r2) return result;
+  if (G.sgrid != nullptr) {
+    const int cell = star_cell<DIM>(sc, x);
+    if (cell >= 0) return star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
+  }
+  return star_radius<DIM>(G, sc.n_sil, sc.n_sgroups, sc.n_prims, x, minR, maxR, prec, flipOrient);
+}
+
+// Waves with at most this many live walks (the long walks of the kernel's tail, which
+// set its critical path) run the step's queries lane by lane -- the sequential star
+// radius, ray and rejection loops, the same results -- instead of the cooperative
+// forms.  Default off: measured slower at every threshold (karman walk 2.50 -> 2.90 ms
+// at 4): even for one or two live lanes the cooperative forms have the shorter
+// dependency chains, spreading a walk's candidates over the idle lanes.
+#ifndef WOS_SEQ_LANES
+#define WOS_SEQ_LANES 0
+#endif
+
+// One iteration of the walk loop for every lane of the wave (convergent): the lanes
+// with active == false take part in the cooperative queries only.  Returns the
+// termination code (>= 0) or -1 while the walk continues.
+template <int DIM, bool GG, bool BSTART, bool RB>
+__device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParams& prm, const LGeom& G, bool active,
+                                              WalkState<DIM>& st, Gfn<DIM, RB>& g, Pcg32& ws, float& ddist,
+                                              uint32_t& wsteps, float& firstR, StarLDS<DIM>* starL,
+                                              RayLDS<DIM>* rayL, RejLDS* rejL, uint32_t* c_iters, int lane) {
+  DIAG_T0(t_step);
+  int code = -1;
+  bool flip = false, query = false;
+  if (active) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
+  const bool seq = WOS_SEQ_LANES > 0 && __popcll(__ballot(active)) <= WOS_SEQ_LANES;  // wave-uniform
+  DIAG_T0(t_star);
+  float starQ = 0.0f;
+  if (seq) {
+    if (active && code < 0 && query) starQ = star_radius_lane<DIM>(G, sc, prm, st.pt, ddist, flip);
+  } else {
+    starQ = star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, st.pt, ddist, flip, starL, lane);
+  }
+  DIAG_ADD(D_STAR, t_star);
+  const bool live = active && code < 0;
+  float dir[DIM], org[DIM], starR = 0.0f;
+  for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
+  DIAG_T0(t_mid);
+  if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org, BSTART ? firstR : 0.0f);
+  DIAG_ADD(D_MID, t_mid);
+  Hit ip;
+  DIAG_T0(t_ray);
+  bool hit;
+  if (WOS_RAY_WAVE && !seq)
+    hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
+  else
+    hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 && ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
+  DIAG_ADD(D_RAY, t_ray);
+  DIAG_T0(t_end);
+  if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
+  DIAG_ADD(D_END, t_end);
+  float sp[DIM], pdf_unused;
+  for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
+  DIAG_T0(t_smp);
+  if (!prm.ignore_source) {
+    if (seq) {
+      if (live) sample_volume<DIM>(prm, g, dir, ws, &pdf_unused, sp, c_iters, false);
+    } else {
+      sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, c_iters, false, rejL, lane);
+    }
+  }
+  DIAG_ADD(D_SAMPLE, t_smp);
+  DIAG_T0(t_tail);
+  if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
+  if (BSTART) firstR = 0.0f;  // firstStep = false (walk_on_stars.h:325)
+  DIAG_ADD(D_TAIL, t_tail);
+  DIAG_ADD(D_STEP, t_step);
+  return code;
+}
+
+// the record of a finished walk (walk_on_stars.h:583-585: escaped and over-length walks are dropped)
+template <int DIM>
+__device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t t,
+                                            int code, const WalkState<DIM>& st, uint32_t wsteps, unsigned int* s_ctr) {
+  const bool recorded = code == WC_DIRICHLET || code == WC_RR;
+  if (recorded) {
+    const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
+    tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
+  }
+  tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
+  DIAG_MAX(D_WMAXLEN, wsteps);
+  atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
+  atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);
+}
+
+__device__ __forceinline__ void flush_walk_counters(unsigned long long* counters, const unsigned int* s_ctr) {
+  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
+    unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
+    if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
+  }
+}
+
 #ifndef WOS_TASK_GRAB
 #define WOS_TASK_GRAB 128
 #endif
@@ -3069,7 +3257,9 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // BSTART: the tasks are boundary-start walks (estimateSolution, walk_on_stars.h:353-464:
 // start normal, first sphere radius, on-Neumann flag from DevTasks::n0/r0/sflags, no
 // first ball, walk stream tag 6) -- boundary value caching (wos_bvc.hip).
-template <int DIM, bool GG, bool BSTART = false, bool RB = false>
+// RESUME: the queue is the survivor list of wos_walk_first_kernel (tk.surv, length
+// tk.shist[2 kCostBuckets]) and each task continues from its saved state.
+template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool RESUME = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_kernel(
     const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
@@ -3094,7 +3284,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #endif
   __syncthreads();
 
-  const uint32_t T = (uint32_t)tk.T;
+  // queue length: every task, or (RESUME) the survivors of the first step
+  const uint32_t T = RESUME ? tk.shist[2 * kCostBuckets] : (uint32_t)tk.T;
   const uint32_t wpp = (uint32_t)tk.wpp;
   // x / wpp as a shift when walks-per-point is a power of two (every shipped config)
   const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
@@ -3110,7 +3301,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // point's state) are in flight during a whole step and a lane that finishes a
   // walk starts the next one from registers (cross-lane shuffles) instead of a
   // chain of dependent global loads.
-  const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;  // <= 64 points per window
+  // <= 64 points per window (RESUME: 64 survivors, lane i holds surv[window + i])
+  const uint32_t G_win = RESUME ? (uint32_t)kWave : (kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp);
   uint32_t wq = 0, we = 0, wp0 = 0, wperm = 0;
   bool exhausted = false;
   int head = 0, S = 0;
@@ -3126,19 +3318,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         if (c >= T) { exhausted = true; break; }
         wq = c;
         we = (T - c) < G_win ? T : c + G_win;
-        wp0 = divw(c);
-        const uint32_t np = divw(we - 1) - wp0 + 1;
-        wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
+        if (RESUME) {
+          wp0 = c;
+          wperm = (uint32_t)lane < we - c ? tk.surv[c + lane] : 0u;
+        } else {
+          wp0 = divw(c);
+          const uint32_t np = divw(we - 1) - wp0 + 1;
+          wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
+        }
       }
       const int avail = (int)(we - wq);
       const int take = (kWave - S) < avail ? (kWave - S) : avail;
       const int pos = ((lane - head) & (kWave - 1)) - S;
       const bool mine = pos >= 0 && pos < take;
-      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = divw(q);
+      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = RESUME ? q : divw(q);
       const uint32_t pidx = (uint32_t)__shfl((int)wperm, (int)(qp - wp0));  // queue position -> permuted point
       if (mine) {
-        s_t = pidx * wpp + (q - qp * wpp);
-        s_ok = tk.pstate[pidx] & kPtEstimate;
+        if (RESUME) {
+          s_t = pidx;  // the survivor's task index
+          s_ok = 1u;
+        } else {
+          s_t = pidx * wpp + (q - qp * wpp);
+          s_ok = tk.pstate[pidx] & kPtEstimate;
+        }
         if (WOS_TASK_RING) {
           for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
           s_thr = tk.thr[s_t];
@@ -3185,7 +3387,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
           v_thr = __shfl(s_thr, src);
           v_tsrc = __shfl(s_tsrc, src);
           v_dd = __shfl(s_dd, src);
-        } else if (t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
+        } else if (!RESUME && t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
           for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];
           v_thr = tk.thr[v_t];
           v_tsrc = tk.tsrc[v_t];
@@ -3197,31 +3399,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
             tk.code[t] = 0u;
             t = -1;
           } else {
-            const uint32_t pidx = divw(v_t);
-            const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
-            for (int kk = 0; kk < DIM; kk++) { st.pt[kk] = v_pt[kk]; st.n[kk] = 0.0f; st.prevDir[kk] = 0.0f; }
-            // prevDir/prevDist only matter once the walk stands on a Neumann boundary,
-            // and every step rewrites them before that can happen
-            st.prevDist = 0.0f;
-            st.throughput = v_thr;
-            st.onNeumann = false;
-            st.walkLength = 0;
-            st.totalNeumann = 0.0f;
-            st.totalSource = v_tsrc;
-            ddist = v_dd;
-            g.init(yuk0, sc.absorption);
-            if constexpr (BSTART) {
-              // WalkState(pt, currentNormal, prevDirection = normal, FLT_MAX, 1, onNeumann)
-              // (walk_on_stars.h:437-439); walk w of sample pidx on its own stream
-              for (int kk = 0; kk < DIM; kk++) { st.n[kk] = tk.n0[kk * tk.T + t]; st.prevDir[kk] = st.n[kk]; }
-              st.prevDist = kFltMax;
-              st.onNeumann = (tk.sflags[t] & 1u) != 0u;
-              firstR = tk.r0[t];
-              ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 6));
-              wsteps = 0;
+            if constexpr (RESUME) {
+              walk_resume<DIM, RB>(sc, prm, tk, t, st, g, ws, ddist, wsteps);
+              firstR = 0.0f;
             } else {
-              ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
-              wsteps = 1;  // the first ball
+              const uint32_t pidx = divw(v_t);
+              const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
+              walk_start<DIM, BSTART, RB>(sc, prm, tk, t, pidx, w, v_pt, v_thr, v_tsrc, v_dd, base, stride, yuk0, st,
+                                          g, ws, ddist, wsteps, firstR);
             }
           }
         }
@@ -3250,54 +3435,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 
     DIAG_COUNT(D_ITERS, 1);
     DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
-    DIAG_T0(t_step);
-    int code = -1;
-    bool flip = false, query = false;
-    if (t >= 0) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
-    DIAG_T0(t_star);
-    const float starQ = star_radius_wave<DIM, GG>(G, sc, prm, t >= 0 && code < 0 && query, st.pt, ddist, flip,
-                                              starL, lane);
-    DIAG_ADD(D_STAR, t_star);
-    const bool live = t >= 0 && code < 0;
-    float dir[DIM], org[DIM], starR = 0.0f;
-    for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
-    DIAG_T0(t_mid);
-    if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org, BSTART ? firstR : 0.0f);
-    DIAG_ADD(D_MID, t_mid);
-    Hit ip;
-    DIAG_T0(t_ray);
-#if WOS_RAY_WAVE
-    const bool hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
-#else
-    const bool hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 &&
-                     ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
-#endif
-    DIAG_ADD(D_RAY, t_ray);
-    DIAG_T0(t_end);
-    if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
-    DIAG_ADD(D_END, t_end);
-    float sp[DIM], pdf_unused;
-    for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
-    DIAG_T0(t_smp);
-    if (!prm.ignore_source)
-      sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, &c_iters, false, rejL, lane);
-    DIAG_ADD(D_SAMPLE, t_smp);
-    DIAG_T0(t_tail);
-    if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
-    if (BSTART) firstR = 0.0f;  // firstStep = false (walk_on_stars.h:325)
-    DIAG_ADD(D_TAIL, t_tail);
-    DIAG_ADD(D_STEP, t_step);
+    const int code = walk_iteration<DIM, GG, BSTART, RB>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
+                                                         rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
-      const bool recorded = code == WC_DIRICHLET || code == WC_RR;
-      if (recorded) {
-        const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
-        tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
-      }
-      tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
-      DIAG_MAX(D_WMAXLEN, wsteps);
-      atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
-      atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL],
-                1u);
+      walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;
     }
     refill(tk);
@@ -3320,10 +3461,132 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
   }
 #endif
-  if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
-    unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
-    if (v) atomicAdd(&counters[threadIdx.x], (unsigned long long)v);
+  flush_walk_counters(counters, s_ctr);
+}
+
+// ---- two-phase walks: the first walk-kernel step of every task --------------
+// Most walks end in their first walk-kernel step (karman: 86 %), so the persistent
+// kernel's machinery -- the queue window, the staged ring, the hand-out, a task per
+// lane per iteration -- is paid per walk.  wos_walk_first_kernel runs that first
+// step for 64 consecutive tasks per wave and iteration (tasks in point-major order:
+// coalesced loads of the start records, every lane busy, no queue), writes the
+// records of the walks that ended, and saves the state of the others (walk_save),
+// counting them per cost bucket of their point.  wos_surv_offsets_kernel /
+// wos_surv_scatter_kernel list the survivors longest-expected-first, and the walk
+// kernel in RESUME mode finishes them.  Same arithmetic, same draws, same records.
+template <int DIM, bool GG, bool RB = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_first_kernel(
+    const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
+    unsigned long long* __restrict__ counters, int geom_floats) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ unsigned int s_ctr[C_NUM];
+  __shared__ uint32_t s_shist[kCostBuckets];
+  const DevScene& sc = sc_arg;
+  const DevParams& prm = prm_arg;
+  const DevTasks& tk = tk_arg;
+  const int lane = threadIdx.x & (kWave - 1);
+  const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
+  stage_rej_jump(prm);
+  const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();
+  StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
+  RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
+  RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
+  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
+  if (threadIdx.x < kCostBuckets) s_shist[threadIdx.x] = 0u;
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
+#endif
+  __syncthreads();
+  const int64_t T = tk.T;
+  const uint32_t wpp = (uint32_t)tk.wpp;
+  const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
+  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
+  uint32_t c_iters = 0;
+  const int64_t nchunks = (T + kWave - 1) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
+  for (int64_t chunk = (int64_t)blockIdx.x * (kBlock / kWave) + wave_u; chunk < nchunks; chunk += nwaves) {
+    KernArgsPtr ka = kernargs_opaque();
+    const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
+    const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
+    const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
+    const LGeom G = WOS_KVIEW ? geometry_view<DIM, GG>(sc, smem, true, false) : G0;
+    const int64_t t = chunk * kWave + lane;
+    const bool valid = t < T;
+    const uint32_t pidx = valid ? (wsh >= 0 ? (uint32_t)t >> wsh : (uint32_t)t / wpp) : 0u;
+    const int ps = valid ? tk.pstate[pidx] : 0;
+    const bool ok = (ps & kPtEstimate) != 0;
+    if (valid && !ok) tk.code[t] = 0u;  // point outside the domain: no walks
+    WalkState<DIM> st;
+    Gfn<DIM, RB> g;
+    Pcg32 ws;
+    float ddist = 0.0f, firstR = 0.0f;
+    uint32_t wsteps = 0;
+    for (int k = 0; k < DIM; k++) st.pt[k] = 0.0f;
+    if (ok) {
+      float v_pt[DIM];
+      for (int k = 0; k < DIM; k++) v_pt[k] = tk.pt[k * T + t];
+      const uint32_t w = ((uint32_t)t - pidx * wpp) >> (prm.n_anti - 1);
+      walk_start<DIM, false, RB>(sc, prm, tk, t, pidx, w, v_pt, tk.thr[t], tk.tsrc[t], tk.dd[t], base, stride, yuk0,
+                                 st, g, ws, ddist, wsteps, firstR);
+    }
+    if (__ballot(ok) == 0) continue;
+    DIAG_COUNT(D_ITERS, 1);
+    DIAG_COUNT(D_LANES, __popcll(__ballot(ok)));
+    const int code = walk_iteration<DIM, GG, false, RB>(sc, prm, G, ok, st, g, ws, ddist, wsteps, firstR, starL, rayL,
+                                                        rejL, &c_iters, lane);
+    if (ok) {
+      if (code >= 0) {
+        walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
+      } else {
+        walk_save<DIM>(tk, t, st, ws, ddist, wsteps);
+        atomicAdd(&s_shist[(ps >> 8) & (kCostBuckets - 1)], 1u);
+      }
+    }
   }
+  flush_counter(counters, C_ITERS, c_iters, lane);
+  __syncthreads();
+#if WOS_DIAG
+  if (threadIdx.x < D_NUM) {
+    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
+  }
+#endif
+  if (threadIdx.x < kCostBuckets && s_shist[threadIdx.x]) atomicAdd(&tk.shist[threadIdx.x], s_shist[threadIdx.x]);
+  flush_walk_counters(counters, s_ctr);
+}
+
+// survivor bucket offsets, highest bucket (longest expected walks) first, and the total
+// (templates only for the linkage: instantiated by wos_kernel.hip and wos_robust.hip)
+template <int N = 0>
+__global__ void wos_surv_offsets_kernel(uint32_t* __restrict__ shist) {
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int b = kCostBuckets - 1; b >= 0; b--) { shist[kCostBuckets + b] = acc; acc += shist[b]; }
+    shist[2 * kCostBuckets] = acc;
+  }
+}
+
+// the survivors (code == kInFlight) into tk.surv in bucket order; block-aggregated like
+// wos_lpt_scatter_kernel (order inside a bucket is immaterial: results do not depend on it)
+template <int N = 0>
+__global__ __launch_bounds__(256) void wos_surv_scatter_kernel(const DevTasks tk) {
+  __shared__ uint32_t cnt[kCostBuckets], base[kCostBuckets];
+  if (threadIdx.x < kCostBuckets) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int b = 0;
+  uint32_t local = 0;
+  const bool in = t < tk.T && tk.code[t] == kInFlight;
+  if (in) {
+    b = (tk.pstate[t / tk.wpp] >> 8) & (kCostBuckets - 1);
+    local = atomicAdd(&cnt[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kCostBuckets && cnt[threadIdx.x])
+    base[threadIdx.x] = atomicAdd(&tk.shist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (in) tk.surv[base[b] + local] = (uint32_t)t;
 }
 
 // ---- kernel 3: statistics + outputs ----------------------------------------

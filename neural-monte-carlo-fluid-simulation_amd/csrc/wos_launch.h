@@ -22,6 +22,11 @@ hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s);
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                         int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
                         int geom_floats, hipStream_t s);
+// two-phase walks (wos_walk_first_kernel + survivor order + the walk kernel in resume
+// mode), replacing launch_lpt_order + launch_walks
+hipError_t launch_walks_two_phase(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
+                                  int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
+                                  size_t shmem, int geom_floats, hipStream_t s);
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s);
 // per-wave LDS scratch of the first-ball kernel (after the staged geometry)
@@ -57,6 +62,9 @@ hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& p
 hipError_t launch_walks_rb(int dim, bool bstart, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                            int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                            size_t shmem, int geom_floats, hipStream_t s);
+hipError_t launch_walks_two_phase_rb(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
+                                     int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue,
+                                     int grid, size_t shmem, int geom_floats, hipStream_t s);
 // which: 0 first-ball, 1 walk, 2 boundary-start walk
 hipError_t occupancy_rb(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 }  // namespace wos

@@ -27,6 +27,18 @@ WOS_RB_WALK(3, false, false);
 WOS_RB_WALK(3, true, false);
 WOS_RB_WALK(2, false, true);  // boundary value caching (boundary-start walks)
 WOS_RB_WALK(2, true, true);
+// two-phase walks
+#define WOS_RB_TWO_PHASE(D, G)                                                                                    \
+  template __global__ void wos_walk_first_kernel<D, G, true>(const DevScene, const DevParams, const DevTasks,      \
+                                                             int64_t, int64_t, unsigned long long*, int);         \
+  template __global__ void wos_walk_kernel<D, G, false, true, true>(const DevScene, const DevParams, const DevTasks, \
+                                                                    int64_t, int64_t, unsigned long long*,        \
+                                                                    unsigned int*, int)
+WOS_RB_TWO_PHASE(2, false);
+WOS_RB_TWO_PHASE(2, true);
+WOS_RB_TWO_PHASE(3, false);
+WOS_RB_TWO_PHASE(3, true);
+#undef WOS_RB_TWO_PHASE
 #undef WOS_RB_FB
 #undef WOS_RB_WALK
 
@@ -61,6 +73,35 @@ hipError_t launch_walks_rb(int dim, bool bstart, const DevScene& sc, const DevPa
     if (sc.geom_global) WOS_LAUNCH_WALK(3, true, false); else WOS_LAUNCH_WALK(3, false, false);
   }
 #undef WOS_LAUNCH_WALK
+  return hipGetLastError();
+}
+
+hipError_t launch_walks_two_phase_rb(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
+                                     int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue,
+                                     int grid, size_t shmem, int geom_floats, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(tk.shist, 0, (2 * kCostBuckets + 1) * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+#define WOS_LAUNCH_FIRST(D, G)                                                                                 \
+  hipLaunchKernelGGL((wos_walk_first_kernel<D, G, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, \
+                     stride, counters, geom_floats)
+#define WOS_LAUNCH_RESUME(D, G)                                                                                \
+  hipLaunchKernelGGL((wos_walk_kernel<D, G, false, true, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, \
+                     base, stride, counters, tqueue, geom_floats)
+  if (dim == 2) {
+    if (sc.geom_global) WOS_LAUNCH_FIRST(2, true); else WOS_LAUNCH_FIRST(2, false);
+  } else {
+    if (sc.geom_global) WOS_LAUNCH_FIRST(3, true); else WOS_LAUNCH_FIRST(3, false);
+  }
+  hipLaunchKernelGGL(wos_surv_offsets_kernel<0>, dim3(1), dim3(64), 0, s, tk.shist);
+  const int sgrid = (int)((tk.T + 255) / 256);
+  if (sgrid > 0) hipLaunchKernelGGL(wos_surv_scatter_kernel<0>, dim3(sgrid), dim3(256), 0, s, tk);
+  if (dim == 2) {
+    if (sc.geom_global) WOS_LAUNCH_RESUME(2, true); else WOS_LAUNCH_RESUME(2, false);
+  } else {
+    if (sc.geom_global) WOS_LAUNCH_RESUME(3, true); else WOS_LAUNCH_RESUME(3, false);
+  }
+#undef WOS_LAUNCH_FIRST
+#undef WOS_LAUNCH_RESUME
   return hipGetLastError();
 }
 

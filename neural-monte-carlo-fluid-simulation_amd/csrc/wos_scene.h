@@ -148,9 +148,25 @@ struct DevTasks {
   float* n0;
   float* r0;
   uint32_t* sflags;
+  // Two-phase walks (wos_walk_first_kernel, then the walk kernel in resume mode): the
+  // walks still running after their first walk-kernel step keep pt / thr / tsrc / dd
+  // in the arrays above and the rest of their state here; code[t] = kInFlight marks
+  // them until they finish.  surv lists them in walk-queue order (cost buckets
+  // descending, shist = [bucket counts | bucket offsets | total]).
+  uint64_t* rrng;    // [T] walk stream state
+  float* rn;         // [DIM][T] current normal
+  float* rpd;        // [DIM][T] previous direction
+  float* rpdist;     // [T] previous distance
+  float* rtn;        // [T] Neumann total
+  uint32_t* rwl;     // [T] walkLength | onNeumann << 31
+  uint32_t* rsteps;  // [T] ball steps so far
+  uint32_t* surv;    // [T] survivor task indices
+  uint32_t* shist;   // [2 * kCostBuckets + 1]
 };
 
-constexpr int task_floats(int dim) { return 3 * dim + 6; }
+constexpr uint32_t kInFlight = 0xFFFFFFFFu;
+// floats per task: the record / start fields, then the two-phase state (rrng first, 8-B aligned)
+constexpr int task_floats(int dim) { return (3 * dim + 6) + (2 * dim + 7); }
 constexpr int kCostBuckets = 32;
 
 }  // namespace wos

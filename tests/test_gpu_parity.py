@@ -296,10 +296,10 @@ def test_mesh_beyond_lds_bit_exact(gpu, oracle):
 
 
 def test_mesh3d_beyond_lds_tree_bit_exact(gpu, oracle):
-    """a 3072-triangle cube (subdivided faces; records far beyond the LDS budget): the
+    """a 6912-triangle cube (subdivided faces; records far beyond the LDS budget): the
     global-memory geometry path with the group hierarchy (ray, star radius, closest
     point by group bounds) matches the oracle's brute-force scans"""
-    v, ix = workloads.subdivided_cube(16)
+    v, ix = workloads.subdivided_cube(24)
     cfg = workloads.cube_config(res=6, n_walks=16)
     osc = oracle.OracleScene(v, ix, cfg["source"], 350.0, watertight=True)
     sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)

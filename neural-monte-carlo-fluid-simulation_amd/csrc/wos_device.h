@@ -3231,9 +3231,8 @@ __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters
 #endif
 constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
 
-// experiments (0 = off): WOS_PRIO=n raises the wave priority with the age of its
-// oldest walk (steps / n); WOS_DRAIN=n stops handing tasks to a wave whose oldest
-// walk is n steps old, so the long walks run in light waves
+// experiment (0 = off): WOS_PRIO=n raises the wave priority with the age of its
+// oldest walk (steps / n) -- within noise on karman, slower on C and the cube
 #ifndef WOS_PRIO
 #define WOS_PRIO 0
 #endif
@@ -3243,9 +3242,6 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // index and its point's state are staged, the record is loaded at hand-out
 #ifndef WOS_TASK_RING
 #define WOS_TASK_RING 0
-#endif
-#ifndef WOS_DRAIN
-#define WOS_DRAIN 0
 #endif
 // 4 waves per SIMD (<= 128 VGPRs): latency hiding for the walk's long dependent chains
 #ifndef WOS_WALK_WAVES_PER_EU
@@ -3373,7 +3369,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     // ---- hand staged tasks to idle lanes (uniform control flow)
     {
       const uint64_t need = __ballot(t < 0);
-      if (need != 0 && S > 0 && (WOS_DRAIN == 0 || wmax < WOS_DRAIN)) {
+      if (need != 0 && S > 0) {
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         const int k = __popcll(need);
@@ -3419,7 +3415,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       refill(tk);
       continue;
     }
-#if WOS_PRIO || WOS_DRAIN
+#if WOS_PRIO
     {
       int wl = t >= 0 ? st.walkLength : 0;
       for (int off = kWave / 2; off > 0; off >>= 1) wl = smax(wl, __shfl_xor(wl, off));

@@ -2672,6 +2672,11 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 // 2D keeps the per-lane loop: measured faster for first balls, r1d);
 // lanes with active == false run pair 0's arithmetic for nothing (helping the
 // cooperative sampler) and write and count nothing.
+// 1: the 2D first-ball source sample uses the wave-cooperative rejection sampler too
+// (the 3D one always does); 0: each lane runs its own loop
+#ifndef WOS_FB_COOP2
+#define WOS_FB_COOP2 0
+#endif
 template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
@@ -2707,7 +2712,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       if (a == 0) {
         float dir[DIM];
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-        if constexpr (DIM == 3)
+        if constexpr (DIM == 3 || WOS_FB_COOP2)
           sample_volume_wave<DIM, RB, true>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
         else
           sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, true);
@@ -2894,10 +2899,15 @@ constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the
 #ifndef WOS_FB_WAVES_PER_EU
 #define WOS_FB_WAVES_PER_EU 1
 #endif
+// 2D: 4 waves/SIMD (128 VGPRs, 28 B/lane of spills) beats the unconstrained 155 VGPRs at
+// 3 waves/SIMD: first balls -2 % on karman, -10 % on config C (A/B, profiles/r2t_ab_fb_occupancy.log)
+#ifndef WOS_FB_WAVES_PER_EU2
+#define WOS_FB_WAVES_PER_EU2 4
+#endif
 // RB: robust float semantics (DevParams::robust; Gfn::scaled) -- separate instantiations
 // (wos_robust.hip), so the reference-semantics kernels carry none of its code
 template <int DIM, bool GG, bool RB = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_FB_WAVES_PER_EU2 : WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
     int lhs_floats) {

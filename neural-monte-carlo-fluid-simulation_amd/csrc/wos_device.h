@@ -2896,8 +2896,10 @@ enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
 #define WOS_PT_GRAB 2
 #endif
 constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the first-ball kernel
+// 3D: 3 waves/SIMD (168 VGPRs, 16-28 B/lane of spills) instead of the unconstrained 2:
+// first balls -20 % on the cube configs (profiles/r2u_ab_fb3d_occupancy.log)
 #ifndef WOS_FB_WAVES_PER_EU
-#define WOS_FB_WAVES_PER_EU 1
+#define WOS_FB_WAVES_PER_EU 3
 #endif
 // 2D: 4 waves/SIMD (128 VGPRs, 28 B/lane of spills) beats the unconstrained 155 VGPRs at
 // 3 waves/SIMD: first balls -2 % on karman, -10 % on config C (A/B, profiles/r2t_ab_fb_occupancy.log)

@@ -193,6 +193,8 @@ struct Geom {
   float *d_prim = nullptr, *d_paux = nullptr, *d_sil = nullptr, *d_dprim = nullptr, *d_dpaux = nullptr;
   float *d_pgroup = nullptr, *d_sgroup = nullptr, *d_dgroup = nullptr;
   float *d_ptree = nullptr, *d_stree = nullptr, *d_dtree = nullptr;
+  float* d_nbox = nullptr;  // fcpw's Neumann BVH (stochastic boundary sample)
+  int32_t *d_nchild = nullptr, *d_nref = nullptr;
   std::mutex mu;  // star grids
   struct Grid {
     float prec, min_r;
@@ -206,6 +208,7 @@ struct Geom {
     hipFree(d_prim); hipFree(d_paux); hipFree(d_sil); hipFree(d_dprim); hipFree(d_dpaux);
     hipFree(d_pgroup); hipFree(d_sgroup); hipFree(d_dgroup);
     hipFree(d_ptree); hipFree(d_stree); hipFree(d_dtree);
+    hipFree(d_nbox); hipFree(d_nchild); hipFree(d_nref);
     for (Grid& g : grids) hipFree(g.d);
   }
 };
@@ -265,6 +268,9 @@ int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
   HIP_TRY(upload(&g->d_ptree, g->host.ptree.node));
   HIP_TRY(upload(&g->d_stree, g->host.stree.node));
   HIP_TRY(upload(&g->d_dtree, g->host.dtree.node));
+  HIP_TRY(upload(&g->d_nbox, g->host.nbvh.box));
+  HIP_TRY(upload(&g->d_nchild, g->host.nbvh.child));
+  HIP_TRY(upload(&g->d_nref, g->host.nbvh.ref));
   {
     std::lock_guard<std::mutex> lk(g_geom_mu);
     g_geom_lru.insert(g_geom_lru.begin(), g);
@@ -437,6 +443,10 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   ds.ptree = tree(h.ptree, geom->d_ptree);
   ds.stree = tree(h.stree, geom->d_stree);
   ds.dtree = tree(h.dtree, geom->d_dtree);
+  ds.nbvh_box = geom->d_nbox;
+  ds.nbvh_child = geom->d_nchild;
+  ds.nbvh_ref = geom->d_nref;
+  ds.nbvh_branch = h.nbvh.branch;
   const int nsd = d->dim == 2 ? 2 : 3;
   for (int k = 0; k < 3; k++) {
     ds.sdims[k] = d->source ? (k < nsd ? d->source_dims[k] : 1) : 0;
@@ -564,7 +574,7 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
     HIP_TRY(hipMalloc((void**)&c.d_pstate,
-                      ((size_t)2 * points + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes) * sizeof(int32_t)));
+                      ((size_t)3 * points + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
@@ -597,8 +607,9 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, in
   tk.surv = (uint32_t*)f;
   tk.pstate = c.d_pstate + pipe * point_slice;
   tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap + pipe * point_slice);
-  tk.hist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
-  tk.shist = (uint32_t*)(c.d_pstate + 2 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
+  tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap + pipe * point_slice);
+  tk.hist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
+  tk.shist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
                          pipe * (2 * wos::kCostBuckets + 1));
   tk.T = T;
   tk.wpp = wpp;
@@ -853,6 +864,27 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   // 2: two-phase walks (first step of every task, then the survivors); 1: one persistent pass
   int phases = 1;
   if (const char* e = std::getenv("WOS_PHASES")) phases = std::atoi(e) == 2 ? 2 : 1;
+  // presorted first balls (point-setup kernel + queue order first, then the first balls
+  // in descending radius order); WOS_FB_SORT=0: setup inside the first-ball kernel (A/B)
+  bool fb_sort = true;
+  if (const char* e = std::getenv("WOS_FB_SORT")) fb_sort = e[0] != '0';
+  dp.fb_order = 0;
+  // The Neumann term (h == 0) is +0 at every step unless a ball's float members overflow
+  // (mu R > 85 is the kernels' gate).  In a watertight single-sided scene every estimated
+  // point and walk lies inside the boundary's bounding box, so R < its diagonal: below
+  // the gate the walk kernel runs without the term's code (bit-identical results).
+  {
+    double diag2 = 0.0;
+    for (int k = 0; k < 3; k++) diag2 += (double)host.ext[k] * host.ext[k];
+    const double mu_r = std::sqrt(std::max(0.0, (double)s->dev.absorption)) * std::sqrt(diag2) * 1.01;
+    dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0) ? 1 : 0;
+    if (const char* e = std::getenv("WOS_NEUMANN_INERT")) dp.neumann_inert = dp.neumann_inert && e[0] != '0';
+  }
+  if (const char* e = std::getenv("WOS_FB_ORDER")) dp.fb_order = std::max(0, std::min(2, std::atoi(e)));
+  if (fb_sort) {
+    geom_floats_fb = 0;
+    shmem_fb_launch = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
+  }
   const int64_t slice_tasks = kMaxBatchTasks / pipes;
   int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, slice_tasks / wpp));
   if (pipes > 1 && n > 0) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, (n + pipes - 1) / pipes));
@@ -862,7 +894,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (n > 0) {
     int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb, dp.robust != 0));
+    HIP_TRY(wos::occupancy_blocks_per_cu(fb_sort ? 2 : 0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb,
+                                         dp.robust != 0));
     grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
     HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk, dp.robust != 0));
@@ -901,9 +934,13 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     if (k >= pipes) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), ps));
     HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), ps));
     HIP_TRY(hipEventRecord(ev[0], ps));
+    if (fb_sort) {
+      HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, ps));
+      HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
+    }
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
-                                    q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, ps));
-    if (phases == 1) HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
+                                    q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, fb_sort, ps));
+    if (phases == 1 && !fb_sort) HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
     HIP_TRY(hipEventRecord(ev[1], ps));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
     if (phases == 2)

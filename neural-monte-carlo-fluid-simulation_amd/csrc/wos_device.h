@@ -321,6 +321,52 @@ __device__ Closest closest_wave_grouped(const float* prims, const float* groups,
   return c;
 }
 
+// The same query by ONE lane (the point-setup kernel: one point per lane).  The
+// group of the smallest box bound is evaluated first for a running minimum when
+// there are many groups, then every group whose bound does not exceed it; the
+// update rule (smaller fl(d*d), or equal and a larger index) makes the result the
+// brute-force one whatever the visiting order, as in closest_wave.
+template <int DIM>
+__device__ Closest closest_lane(const float* prims, const float* groups, int np, int ng, const float* x) {
+  constexpr int PS = Layout<DIM>::prim;
+  float bk = kFltMax;
+  int bi = -1;
+  const auto scan = [&](int g) {
+    const int p1 = (g + 1) * kGroup < np ? (g + 1) * kGroup : np;
+    for (int p = g * kGroup; p < p1; p++) {
+      float pt[DIM], t0, t1;
+      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+      const float d2 = d * d;
+      if (d2 < bk || (d2 == bk && p > bi)) { bk = d2; bi = p; }
+    }
+  };
+  if (ng <= 16) {  // small meshes: every primitive, uniform addresses (scalar loads)
+    for (int p = 0; p < np; p++) {
+      float pt[DIM], t0, t1;
+      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
+      const float d2 = d * d;
+      if (d2 <= bk) { bk = d2; bi = p; }
+    }
+    ng = 0;
+  } else {
+    float lbm = kFltMax;
+    int gm = 0;
+    for (int g = 0; g < ng; g++) {
+      const float lb = box_dist2<DIM>(groups + g * kGroupStride, x);
+      if (lb < lbm) { lbm = lb; gm = g; }
+    }
+    scan(gm);
+  }
+  for (int g = 0; g < ng; g++) {
+    if (box_dist2<DIM>(groups + g * kGroupStride, x) > bk) continue;
+    scan(g);
+  }
+  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
+  c.p[0] = c.p[1] = c.p[2] = 0.0f;
+  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
+  return c;
+}
+
 // Interaction::computeNormal via normal(uv) (line_segments.inl:57-73, triangles.inl:61-89)
 template <int DIM>
 __device__ __forceinline__ void closest_normal(const float* aux, const Closest& c, float* n) {
@@ -1913,37 +1959,96 @@ __device__ __forceinline__ float prim_area(const float* P) {
   }
 }
 
+// sampleNeumann's primitive choice (fcpw_scene_loader.h:599-620): fcpw's stochastic
+// traversal, Mbvh::intersectStochasticFromNode (mbvh.inl:1099-1283), over its wide
+// BVH (wos_fcpw_bvh.cpp, read from global memory): ONE root-to-leaf path, at each node
+// a child among those whose box overlaps the ball, chosen with probability ~ the
+// traversal weight |HarmonicGreensFnFreeSpace<3>::evaluate(max(|c - box centre|, 1e-2))|
+// (scene.h:157-160) by rescaling one uniform (u -> u/p or (u-p)/(1-p)); in the leaf a
+// primitive overlapping the ball ~ its area (intersectSpherePrimitives, :835-982; all
+// of them when the leaf box lies inside the ball).  2D runs in fcpw's 3D frame (z = 0).
+// Returns the primitive (-1: no sample) and its selection pdf (weight * traversalPdf) / total.
+template <int DIM>
+__device__ __forceinline__ int fcpw_stochastic_pick(const DevScene& sc, const float* prims, const float* x, float R,
+                                                 float u, float* sel_pdf) {
+  constexpr int PS = Layout<DIM>::prim;
+  const int B = sc.nbvh_branch;
+  const float r2 = R * R;
+  const float c[3] = {x[0], x[1], DIM == 3 ? x[2] : 0.0f};
+  float tpdf = 1.0f, d2NodeMax = kFltMax;
+  int node = 0;
+  for (;;) {
+    const int32_t* C = sc.nbvh_child + node * B;
+    if (C[0] < 0) {
+      const bool inside = d2NodeMax <= r2;
+      int sel = -1;
+      float total = 0.0f, selw = 0.0f, uu = u;
+#pragma clang loop unroll(disable)
+      for (int p = 0; p < C[3]; p++) {
+        const int q = sc.nbvh_ref[C[2] + p];
+        const float* P = prims + q * PS;
+        float d2 = 0.0f;
+        if (!inside) {
+          float pt[DIM], t0, t1;
+          const float d = cp_prim<DIM>(P, x, pt, &t0, &t1);
+          d2 = d * d;
+        }
+        if (d2 <= r2) {
+          const float w = prim_area<DIM>(P);
+          total += w;
+          const float prob = w / total;
+          if (uu < prob) { uu = uu / prob; sel = q; selw = w; }
+          else uu = (uu - prob) / (1.0f - prob);
+        }
+      }
+      if (sel < 0) return -1;
+      float d = selw * tpdf;
+      if (total > 0.0f) d /= total;
+      *sel_pdf = d;
+      return sel;
+    }
+    int sel = -1;
+    float tot = 0.0f, selw = 0.0f, selmax = 0.0f;
+#pragma clang loop unroll(disable)
+    for (int w = 0; w < B; w++) {
+      if (C[w] == 0x7FFFFFFF) continue;
+      const float* bx = sc.nbvh_box + (node * B + w) * 6;
+      // overlapWideBox (wide_query_operations.h:96-106)
+      float mn[3], mx[3], ct[3];
+      for (int k = 0; k < 3; k++) {
+        const float a = bx[k] - c[k], b = c[k] - bx[3 + k];
+        mn[k] = smax(smax(a, b), 0.0f);
+        mx[k] = smin(a, b);
+      }
+      const float d2min = (mn[0] * mn[0] + mn[1] * mn[1]) + mn[2] * mn[2];
+      const float d2max = (mx[0] * mx[0] + mx[1] * mx[1]) + mx[2] * mx[2];
+      if (!(d2min <= r2)) continue;
+      for (int k = 0; k < 3; k++) ct[k] = c[k] - (bx[k] + bx[3 + k]) * 0.5f;
+      const float rr = smax(__builtin_sqrtf((ct[0] * ct[0] + ct[1] * ct[1]) + ct[2] * ct[2]), 1e-2f);
+      const float weight = __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
+      tot += weight;
+      const float prob = weight / tot;
+      if (u < prob) { sel = w; selw = weight; selmax = d2max; u = u / prob; }
+      else u = (u - prob) / (1.0f - prob);
+    }
+    if (sel < 0) return -1;
+    node = C[sel];
+    tpdf *= selw / tot;
+    d2NodeMax = selmax;
+  }
+}
+
 // Neumann boundary sample (walk_on_stars.h:212-260).  With the reference's h == 0
 // (scene.h:176-181) the term is exactly +0 unless G or the throughput is
-// non-finite; only then the brute-force stochastic sample is evaluated.
+// non-finite; only then the stochastic sample is evaluated.
 template <int DIM, bool RB>
 __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM, RB>& g,
                                           WalkState<DIM>& st, float R, const float* rn) {
   constexpr int PS = Layout<DIM>::prim;
   const int np = sc.n_prims;
   const float* x = st.pt;
-  float total = 0.0f;
-  for (int p = 0; p < np; p++) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    if (d * d <= R * R) {
-      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
-      total += prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
-    }
-  }
-  if (!(total > 0.0f)) return;
-  float target = rn[0] * total, acc = 0.0f, selw = 0.0f;
-  int sel = -1;
-  for (int p = 0; p < np; p++) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    if (d * d <= R * R) {
-      float rr = smax(__builtin_sqrtf(d * d), 1e-2f);
-      float w = prim_area<DIM>(prims + p * PS) * __builtin_fabsf((float)(1.0 / (kFourPi * (double)rr)));
-      acc += w; sel = p; selw = w;
-      if (target < acc) break;
-    }
-  }
+  float sel_pdf = 0.0f;
+  const int sel = fcpw_stochastic_pick<DIM>(sc, prims, x, R, rn[0], &sel_pdf);
   if (sel < 0) return;
   const float* P = prims + sel * PS;
   float sp[DIM], sn[DIM], pdf;
@@ -1963,7 +2068,8 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
     for (int k = 0; k < 3; k++) { sp[k] = P[k] * u + P[3 + k] * v + P[6 + k] * w; sn[k] /= area; }
     pdf = 2.0f / area;
   }
-  pdf *= selw / total;
+  // Interaction::d = (weight * traversalPdf) / total, then *= samplePoint's pdf (mbvh.inl:1265-1276)
+  pdf = sel_pdf * pdf;
   float dts[DIM];
   for (int k = 0; k < DIM; k++) dts[k] = sp[k] - x[k];
   float distToSample = normv<DIM>(dts);
@@ -2043,7 +2149,9 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
 
 // after the ray query: the miss point and the Neumann term (walk_on_stars.h:200-260);
 // the source sample (convergent, sample_volume_wave) and walk_step_tail follow
-template <int DIM, bool RB>
+// NEU = false: the instantiation for scenes whose Neumann term is provably +0 at every
+// step (DevParams::neumann_inert) -- the term's code is compiled out, the draws stay
+template <int DIM, bool RB, bool NEU = true>
 __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
                                               Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, float starRadius,
                                               const float* dir, const float* org, bool hit, Hit& ip) {
@@ -2056,8 +2164,12 @@ __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParam
   if (!prm.ignore_neumann) {
     float rn[3] = {0.0f, 0.0f, 0.0f};
     for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
-    bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa == 1 && g.muR > 85.0f);
-    if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
+    if constexpr (NEU) {
+      bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa == 1 && g.muR > 85.0f);
+      if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
+    } else {
+      (void)np; (void)prims;
+    }
   }
 }
 
@@ -2906,9 +3018,81 @@ constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the
 #ifndef WOS_FB_WAVES_PER_EU2
 #define WOS_FB_WAVES_PER_EU2 4
 #endif
+
+// Sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
+// (fcpw_scene_loader.h:642-648) from the two closest-point queries, the masks of the
+// outputs (grid.h:155-179, 207-237) and the cost bucket of the point.  Cost buckets
+// order both queues: walks from points close to the boundary (small first ball) run
+// longest, so the walk queue takes high buckets first; first balls cost ~ their
+// radius (11.2 R rejection iterations per Yukawa sample at lambda = 350, the max over
+// the 64 lanes of a wave), so the presorted first-ball queue runs the buckets in the
+// opposite order.  Returns the pstate word; firstR = 0.99 min(dDist, nDist).
+template <int DIM>
+__device__ __forceinline__ int32_t point_state(const DevScene& sc, const DevParams& prm, float nDist, float nSigned,
+                                               float dDist, float dSigned, int* bucket_out, float* firstR) {
+  const bool inside = !sc.watertight ? true
+                      : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
+  const bool estimate = inside || sc.double_sided;
+  const float mask = prm.boundary_distance_mask;
+  const bool maskP = __builtin_fabsf(nDist) < mask;
+  const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
+  const float bd = smin(dDist, nDist);
+  int bucket = 0;
+  if (estimate) {
+    const float l2 = __builtin_amdgcn_logf(smax(bd, 1e-9f));  // log2
+    bucket = (int)sclamp((int)(-2.0f * l2) + 8, 1, kCostBuckets - 1);
+  }
+  *bucket_out = bucket;
+  *firstR = 0.99f * bd;
+  return (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
+}
+
+// Point setup for the presorted first balls: one point per lane (the exact scans of
+// closest_lane), pstate + first-ball radius per point and the bucket histogram.  The
+// first-ball kernel then takes the points in descending radius order, so the points
+// whose 64 lanes run the longest rejection loops start first instead of anywhere in
+// the queue (a late one had set the kernel's tail).
+template <int DIM>
+__global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc, const DevParams prm,
+                                                             const float* __restrict__ pts, int64_t n,
+                                                             const DevTasks tk) {
+  __shared__ uint32_t s_hist[kCostBuckets];
+  if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    float x[DIM];
+    for (int k = 0; k < DIM; k++) x[k] = pts[i * DIM + k];
+    float nDist = kFltMax, nSigned = kFltMax;
+    if (sc.n_prims > 0) {
+      const Closest c = closest_lane<DIM>(sc.prim, sc.pgroup, sc.n_prims, sc.n_pgroups, x);
+      nDist = c.d;
+      nSigned = signed_dist<DIM>(sc.paux, c, x);
+    }
+    float dDist, dSigned;
+    if (sc.n_dprims > 0) {
+      const Closest c = closest_lane<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x);
+      dDist = c.d;
+      dSigned = signed_dist<DIM>(sc.dpaux, c, x);
+    } else {
+      dDist = dSigned = bbox_far_dist<DIM>(sc, x);
+    }
+    int bucket;
+    float firstR;
+    tk.pstate[i] = point_state<DIM>(sc, prm, nDist, nSigned, dDist, dSigned, &bucket, &firstR);
+    tk.prad[i] = firstR;
+    atomicAdd(&s_hist[bucket], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
+}
+
 // RB: robust float semantics (DevParams::robust; Gfn::scaled) -- separate instantiations
-// (wos_robust.hip), so the reference-semantics kernels carry none of its code
-template <int DIM, bool GG, bool RB = false>
+// (wos_robust.hip), so the reference-semantics kernels carry none of its code.
+// PRE: presorted -- wos_point_setup_kernel + the walk-queue order ran first; queue
+// position q takes point perm[n_est - 1 - q] (largest first ball first) and reads its
+// radius instead of repeating the setup (no geometry staged: geom_floats = 0).
+template <int DIM, bool GG, bool RB = false, bool PRE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_FB_WAVES_PER_EU2 : WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
     const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
@@ -2917,9 +3101,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   __shared__ uint32_t s_hist[kCostBuckets];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const LGeom Gfb = stage_geometry<DIM, GG>(sc, smem, false);
+  LGeom Gfb{};
+  if constexpr (!PRE) Gfb = stage_geometry<DIM, GG>(sc, smem, false);
   stage_rej_jump(prm);
-  if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
+  if (!PRE && threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -2932,6 +3117,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   uint32_t c_iters = 0, c_pts = 0;
   const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
+  // PRE with a queue order (fb_order 1: walk-queue order, 2: reversed): the queue runs
+  // over the estimated points only (bucket 0 = not estimated, last in the walk order);
+  // fb_order 0: point order, the estimate bit read from pstate
+  const int order = PRE ? prm.fb_order : 0;
+  const int64_t nq = order != 0 ? n - (int64_t)tk.hist[0] : n;
 
   // point queue, one point ahead: the next index is taken (and its coordinates
   // loaded) while the current point is processed, so neither the queue atomic nor
@@ -2949,58 +3139,60 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     idx = __shfl(idx, 0);
     cend = idx + kPtGrab;
   }
-  float xn[DIM];
-  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
+  // queue position -> point index (identity unless PRE with a queue order)
+  const auto point_of = [&](unsigned int q) -> unsigned int {
+    if (order == 0 || (int64_t)q >= nq) return q;
+    return tk.perm[order == 1 ? (int64_t)q : nq - 1 - (int64_t)q];
+  };
+  unsigned int pn = point_of(idx);
+  float xn[DIM], rn = 0.0f;
+  bool en = true;
+  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < nq ? pts[(int64_t)pn * DIM + k] : 0.0f;
+  if (PRE && (int64_t)idx < nq) {
+    rn = tk.prad[pn];
+    if (order == 0) en = (tk.pstate[pn] & kPtEstimate) != 0;
+  }
   for (;;) {
-    if ((int64_t)idx >= n) break;
-    const int64_t gidx = base + (int64_t)idx * stride;
+    if ((int64_t)idx >= nq) break;
+    const unsigned int pidx = pn;
+    const int64_t gidx = base + (int64_t)pidx * stride;
     float x[DIM];
     for (int k = 0; k < DIM; k++) x[k] = xn[k];
+    float firstR = rn;
+    bool estimate = en;
     const bool grab = kPtGrab != 0 && idx + 1 >= cend;  // wave-uniform
     unsigned int nidx_l0 = 0;
     if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
 
-    // ---- sample point setup: createSolutionGrid (grid.h:85-101) + insideDomain
     DIAG_T0(t_fb0);
-    float nDist = kFltMax, nSigned = kFltMax;
-    if (sc.n_prims > 0) {
-      Closest c = (GG && sc.n_pgroups > kTreeMinGroups)
-                      ? closest_wave_grouped<DIM>(Lprim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, lane)
-                      : closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
-      nDist = c.d;
-      nSigned = signed_dist<DIM>(sc.paux, c, x);
-    }
-    float dDist, dSigned;
-    if (sc.n_dprims > 0) {
-      Closest c = sc.n_dgroups > kTreeMinGroups
-                      ? closest_wave_grouped<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, lane)
-                      : closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
-      dDist = c.d;
-      dSigned = signed_dist<DIM>(sc.dpaux, c, x);
-    } else {
-      dDist = dSigned = bbox_far_dist<DIM>(sc, x);
-    }
-    const bool inside = !sc.watertight ? true
-                        : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
-    const bool estimate = inside || sc.double_sided;
-    if (lane == 0) {
-      // masked outputs (grid.h:155-179, 207-237)
-      const float mask = prm.boundary_distance_mask;
-      const bool maskP = __builtin_fabsf(nDist) < mask;
-      const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
-      // cost bucket for the walk-queue order: walks from points close to the boundary
-      // (small first ball) run longest, so they are queued first (longest-first
-      // scheduling shortens the tail of the persistent walk kernel)
-      const float bd = smin(dDist, nDist);
-      int bucket = 0;
-      if (estimate) {
-        const float l2 = __builtin_amdgcn_logf(smax(bd, 1e-9f));  // log2
-        bucket = (int)sclamp((int)(-2.0f * l2) + 8, 1, kCostBuckets - 1);
+    if constexpr (!PRE) {
+      float nDist = kFltMax, nSigned = kFltMax;
+      if (sc.n_prims > 0) {
+        Closest c = (GG && sc.n_pgroups > kTreeMinGroups)
+                        ? closest_wave_grouped<DIM>(Lprim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, lane)
+                        : closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
+        nDist = c.d;
+        nSigned = signed_dist<DIM>(sc.paux, c, x);
       }
-      tk.pstate[idx] = (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
-      atomicAdd(&s_hist[bucket], 1u);
+      float dDist, dSigned;
+      if (sc.n_dprims > 0) {
+        Closest c = sc.n_dgroups > kTreeMinGroups
+                        ? closest_wave_grouped<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, lane)
+                        : closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
+        dDist = c.d;
+        dSigned = signed_dist<DIM>(sc.dpaux, c, x);
+      } else {
+        dDist = dSigned = bbox_far_dist<DIM>(sc, x);
+      }
+      int bucket;
+      const int32_t ps = point_state<DIM>(sc, prm, nDist, nSigned, dDist, dSigned, &bucket, &firstR);
+      estimate = (ps & kPtEstimate) != 0;
+      if (lane == 0) {
+        tk.pstate[pidx] = ps;
+        atomicAdd(&s_hist[bucket], 1u);
+      }
     }
-    // the next point: its index (the atomic has returned by now) and coordinates
+    // the next point: its index (the atomic has returned by now), coordinates (and radius)
     unsigned int nidx, ncend = cend;
     if (kPtGrab == 0) {
       nidx = idx + nwaves;
@@ -3010,7 +3202,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     } else {
       nidx = idx + 1;
     }
-    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
+    pn = point_of(nidx);
+    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < nq ? pts[(int64_t)pn * DIM + k] : 0.0f;
+    if (PRE && (int64_t)nidx < nq) {
+      rn = tk.prad[pn];
+      if (order == 0) en = (tk.pstate[pn] & kPtEstimate) != 0;
+    }
     if (!estimate) { idx = nidx; cend = ncend; continue; }
     c_pts += lane == 0;
     DIAG_ADD(D_FB_SETUP, t_fb0);
@@ -3024,11 +3221,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #endif
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
-    const float firstR = 0.99f * smin(dDist, nDist);
     for (int w0 = 0; w0 < npairs; w0 += kWave) {
       const int w = w0 + lane;
       first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
-                       (int64_t)idx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
+                           (int64_t)pidx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
     }
     DIAG_ADD(D_FB_BALLS, t_fb2);
     DIAG_ADD(D_FB_TOTAL, t_fb0);
@@ -3039,9 +3235,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
-  __syncthreads();
-  if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
+  if constexpr (!PRE) {
+    __syncthreads();
+    if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
+  }
 #if WOS_DIAG
+  __syncthreads();
   if (threadIdx.x < D_NUM) {
     if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
     else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
@@ -3162,7 +3361,7 @@ __device__ __forceinline__ float star_radius_lane(const LGeom& G, const DevScene
 // One iteration of the walk loop for every lane of the wave (convergent): the lanes
 // with active == false take part in the cooperative queries only.  Returns the
 // termination code (>= 0) or -1 while the walk continues.
-template <int DIM, bool GG, bool BSTART, bool RB>
+template <int DIM, bool GG, bool BSTART, bool RB, bool NEU = true>
 __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParams& prm, const LGeom& G, bool active,
                                               WalkState<DIM>& st, Gfn<DIM, RB>& g, Pcg32& ws, float& ddist,
                                               uint32_t& wsteps, float& firstR, StarLDS<DIM>* starL,
@@ -3195,7 +3394,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
     hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 && ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
   DIAG_ADD(D_RAY, t_ray);
   DIAG_T0(t_end);
-  if (live) walk_step_end<DIM>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
+  if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
   DIAG_ADD(D_END, t_end);
   float sp[DIM], pdf_unused;
   for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
@@ -3267,7 +3466,7 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // first ball, walk stream tag 6) -- boundary value caching (wos_bvc.hip).
 // RESUME: the queue is the survivor list of wos_walk_first_kernel (tk.surv, length
 // tk.shist[2 kCostBuckets]) and each task continues from its saved state.
-template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool RESUME = false>
+template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool RESUME = false, bool NEU = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_kernel(
     const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
@@ -3443,7 +3642,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 
     DIAG_COUNT(D_ITERS, 1);
     DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
-    const int code = walk_iteration<DIM, GG, BSTART, RB>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
+    const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);

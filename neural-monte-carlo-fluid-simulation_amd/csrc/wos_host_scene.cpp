@@ -226,6 +226,7 @@ bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err) {
   out.n_prims = (int)neu.ix.size();
   out.n_dprims = (int)dir.ix.size();
   build_silhouettes(neu, in.is_double_sided != 0, out.sil, out.n_sil);
+  if (in.n_prims > 0) build_fcpw_bvh(in.dim, in.vertices, in.prims, in.n_prims, kFcpwBranch, kFcpwLeaf, out.nbvh);
   // bounding box over all boundary vertices, padded by FLT_EPSILON per vertex
   for (int k = 0; k < 3; k++) { out.pmin[k] = kFltMax; out.pmax[k] = -kFltMax; }
   const Geom* gs[2] = {&neu, &dir};

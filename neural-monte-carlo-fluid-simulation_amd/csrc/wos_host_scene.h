@@ -31,6 +31,24 @@ struct HostTree {
 // the tree over `ngroups` group records of `stride` floats (box in the first 8)
 void build_group_tree(const std::vector<float>& groups, int stride, int ngroups, HostTree& out);
 
+// The Neumann boundary's wide BVH as fcpw builds it for the stochastic boundary sample
+// (wos_fcpw_bvh.cpp): node i has `branch` children; child box w at
+// box[(i * branch + w) * 6] = [min.xyz | max.xyz] (2D: z = 0 padded by FLT_EPSILON),
+// child[i * branch + w] = child node index, INT_MAX when unused (box min = FLT_MAX,
+// max = -FLT_MAX).  A leaf has child[0] < 0, child[2] = first reference,
+// child[3] = reference count; ref[r] = primitive of reference r.
+constexpr int kFcpwBranch = 4;  // FCPW_MBVH_BRANCHING_FACTOR (FCPW_USE_EIGHT_WIDE_BRANCHING off)
+constexpr int kFcpwLeaf = 8;    // FCPW_SIMD_WIDTH of an AVX/AVX2 build (fcpw CMakeLists.txt:83-95)
+struct HostFcpwBvh {
+  int branch = kFcpwBranch, leaf = kFcpwLeaf;
+  int n_nodes = 0, n_leaves = 0;
+  std::vector<float> box;
+  std::vector<int32_t> child;
+  std::vector<int32_t> ref;
+};
+void build_fcpw_bvh(int dim, const float* verts, const int32_t* prims, int n_prims, int branch, int leaf,
+                    HostFcpwBvh& out);
+
 struct HostScene {
   int dim = 2;
   int n_prims = 0, n_sil = 0, n_dprims = 0;
@@ -38,6 +56,7 @@ struct HostScene {
   std::vector<float> pgroup, sgroup, dgroup;  // culling boxes (kGroupStride floats each)
   int n_pgroups = 0, n_sgroups = 0, n_dgroups = 0;
   HostTree ptree, stree, dtree;
+  HostFcpwBvh nbvh;  // Neumann boundary, for the stochastic boundary sample
   float pmin[3] = {0, 0, 0}, pmax[3] = {0, 0, 0}, ext[3] = {0, 0, 0};
 };
 

@@ -9,20 +9,21 @@
 
 namespace wos {
 
-// ---- walk-queue order: bucket offsets (descending cost) and the permutation ---
-__global__ void wos_lpt_offsets_kernel(uint32_t* __restrict__ hist) {
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int b = kCostBuckets - 1; b >= 0; b--) { hist[kCostBuckets + b] = acc; acc += hist[b]; }
-  }
-}
-
-// block-aggregated: LDS bucket counts, one global range reservation per bucket per
-// block, then LDS-local placement (the global offsets see kCostBuckets atomics per
-// block instead of one per point)
+// ---- walk-queue order: the permutation, buckets in descending cost order ----
+// One launch: every block derives the bucket offsets from the final counts
+// hist[0, kCostBuckets) itself (exclusive sums in descending bucket order), counts its
+// points per bucket in LDS, reserves one range per bucket with an atomic on the fill
+// cursors hist[kCostBuckets + b] (zeroed with the counts), then places its points.
+// Order inside a bucket is immaterial: results do not depend on it.
 __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk, int64_t n) {
-  __shared__ uint32_t cnt[kCostBuckets], base[kCostBuckets];
-  if (threadIdx.x < kCostBuckets) cnt[threadIdx.x] = 0u;
+  __shared__ uint32_t cnt[kCostBuckets], base[kCostBuckets], off[kCostBuckets];
+  if (threadIdx.x < kCostBuckets) {
+    cnt[threadIdx.x] = 0u;
+    // offset of bucket b = points in buckets above b
+    uint32_t acc = 0;
+    for (int b = kCostBuckets - 1; b > (int)threadIdx.x; b--) acc += tk.hist[b];
+    off[threadIdx.x] = acc;
+  }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int b = 0;
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk,
   }
   __syncthreads();
   if (threadIdx.x < kCostBuckets && cnt[threadIdx.x])
-    base[threadIdx.x] = atomicAdd(&tk.hist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
+    base[threadIdx.x] = off[threadIdx.x] + atomicAdd(&tk.hist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
   __syncthreads();
   if (i < n) tk.perm[base[b] + local] = (uint32_t)i;
 }
@@ -43,6 +44,15 @@ template __global__ void wos_first_ball_kernel<2, false>(const DevScene, const D
                                                            unsigned int*, int, int);
 template __global__ void wos_walk_kernel<2, false>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
                                                      unsigned long long*, unsigned int*, int);
+#define WOS_INERT_WALK(D, G)                                                                                      \
+  template __global__ void wos_walk_kernel<D, G, false, false, false, false>(const DevScene, const DevParams,     \
+                                                                             const DevTasks, int64_t, int64_t,     \
+                                                                             unsigned long long*, unsigned int*, int)
+WOS_INERT_WALK(2, false);
+WOS_INERT_WALK(2, true);
+WOS_INERT_WALK(3, false);
+WOS_INERT_WALK(3, true);
+#undef WOS_INERT_WALK
 template __global__ void wos_first_ball_kernel<2, true>(const DevScene, const DevParams, const float*, int64_t,
                                                            int64_t, int64_t, const DevTasks, unsigned long long*,
                                                            unsigned int*, int, int);
@@ -69,6 +79,15 @@ WOS_TWO_PHASE(2, true);
 WOS_TWO_PHASE(3, false);
 WOS_TWO_PHASE(3, true);
 #undef WOS_TWO_PHASE
+#define WOS_PRE_FB(D)                                                                                          \
+  template __global__ void wos_first_ball_kernel<D, false, false, true>(const DevScene, const DevParams, const float*, \
+                                                                        int64_t, int64_t, int64_t, const DevTasks,    \
+                                                                        unsigned long long*, unsigned int*, int, int); \
+  template __global__ void wos_point_setup_kernel<D>(const DevScene, const DevParams, const float*, int64_t,         \
+                                                     const DevTasks)
+WOS_PRE_FB(2);
+WOS_PRE_FB(3);
+#undef WOS_PRE_FB
 template __global__ void wos_fold_kernel<2>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
                                             int32_t*);
 template __global__ void wos_fold_kernel<3>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
@@ -120,24 +139,38 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                               unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                              hipStream_t s) {
+                              bool pre, hipStream_t s) {
   if (prm.robust)
     return launch_first_balls_rb(dim, sc, prm, pts, n, base, stride, tk, counters, work, grid, shmem, geom_floats,
-                                 lhs_floats, s);
+                                 lhs_floats, pre, s);
 #define WOS_LAUNCH_FB(D, G)                                                                                  \
   hipLaunchKernelGGL((wos_first_ball_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, \
                      tk, counters, work, geom_floats, lhs_floats)
-  if (dim == 2) {
+#define WOS_LAUNCH_PRE(D)                                                                                          \
+  hipLaunchKernelGGL((wos_first_ball_kernel<D, false, false, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, \
+                     n, base, stride, tk, counters, work, 0, lhs_floats)
+  if (pre) {
+    if (dim == 2) WOS_LAUNCH_PRE(2); else WOS_LAUNCH_PRE(3);
+  } else if (dim == 2) {
     if (sc.geom_global) WOS_LAUNCH_FB(2, true); else WOS_LAUNCH_FB(2, false);
   } else {
     if (sc.geom_global) WOS_LAUNCH_FB(3, true); else WOS_LAUNCH_FB(3, false);
   }
 #undef WOS_LAUNCH_FB
+#undef WOS_LAUNCH_PRE
+  return hipGetLastError();
+}
+
+hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                              const DevTasks& tk, hipStream_t s) {
+  const int grid = (int)((n + 255) / 256);
+  if (grid < 1) return hipSuccess;
+  if (dim == 2) hipLaunchKernelGGL(wos_point_setup_kernel<2>, dim3(grid), dim3(256), 0, s, sc, prm, pts, n, tk);
+  else hipLaunchKernelGGL(wos_point_setup_kernel<3>, dim3(grid), dim3(256), 0, s, sc, prm, pts, n, tk);
   return hipGetLastError();
 }
 
 hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(wos_lpt_offsets_kernel, dim3(1), dim3(64), 0, s, tk.hist);
   const int grid = (int)((n + 255) / 256);
   if (grid > 0) hipLaunchKernelGGL(wos_lpt_scatter_kernel, dim3(grid), dim3(256), 0, s, tk, n);
   return hipGetLastError();
@@ -148,9 +181,15 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
                         int geom_floats, hipStream_t s) {
   if (prm.robust)
     return launch_walks_rb(dim, false, sc, prm, tk, base, stride, counters, tqueue, grid, shmem, geom_floats, s);
-#define WOS_LAUNCH_WALK(D, G)                                                                                   \
-  hipLaunchKernelGGL((wos_walk_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride, counters, \
-                     tqueue, geom_floats)
+#define WOS_LAUNCH_WALK(D, G)                                                                                    \
+  do {                                                                                                           \
+    if (prm.neumann_inert)                                                                                       \
+      hipLaunchKernelGGL((wos_walk_kernel<D, G, false, false, false, false>), dim3(grid), dim3(kBlock), shmem, s, sc, \
+                         prm, tk, base, stride, counters, tqueue, geom_floats);                                  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((wos_walk_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride,  \
+                         counters, tqueue, geom_floats);                                                         \
+  } while (0)
   if (dim == 2) {
     if (sc.geom_global) WOS_LAUNCH_WALK(2, true); else WOS_LAUNCH_WALK(2, false);
   } else {
@@ -210,7 +249,10 @@ size_t first_ball_wave_lds_bytes(int lhs_floats) {
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks, bool robust) {
-  if (robust) return occupancy_rb(which, dim, geom_global, shmem, blocks);
+  if (robust) return occupancy_rb(which == 2 ? 3 : which, dim, geom_global, shmem, blocks);
+  if (which == 2)
+    return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, false, false, true>, kBlock, shmem)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, false, false, true>, kBlock, shmem);
   if (which == 0) {
     if (dim == 2)
       return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, true>, kBlock, shmem)

@@ -16,7 +16,11 @@ constexpr int kNumCounterSlots = kNumCounters + 2 * kMaxPipes;
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                               unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                              hipStream_t s);
+                              bool pre, hipStream_t s);
+// presorted first balls (pre = true above): per-point setup, pstate + first-ball radius
+// + bucket histogram, before launch_lpt_order
+hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
+                              const DevTasks& tk, hipStream_t s);
 // bucket offsets + point permutation for the walk queue (after the first-ball kernel)
 hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s);
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
@@ -33,7 +37,7 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
 size_t first_ball_wave_lds_bytes(int lhs_floats);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
-// which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry);
+// which: 0 first-ball kernel, 1 walk kernel, 2 presorted first-ball kernel (the instantiation for LDS-staged or global geometry);
 // robust: the robust-float instantiations (wos_robust.hip)
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks,
                                    bool robust = false);
@@ -58,13 +62,13 @@ hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const
 hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                                  int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                                  unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                                 hipStream_t s);
+                                 bool pre, hipStream_t s);
 hipError_t launch_walks_rb(int dim, bool bstart, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                            int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                            size_t shmem, int geom_floats, hipStream_t s);
 hipError_t launch_walks_two_phase_rb(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                      int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue,
                                      int grid, size_t shmem, int geom_floats, hipStream_t s);
-// which: 0 first-ball, 1 walk, 2 boundary-start walk
+// which: 0 first-ball, 1 walk, 2 boundary-start walk, 3 presorted first-ball
 hipError_t occupancy_rb(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 }  // namespace wos

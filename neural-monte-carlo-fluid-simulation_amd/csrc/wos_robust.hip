@@ -21,6 +21,12 @@ WOS_RB_FB(2, false);
 WOS_RB_FB(2, true);
 WOS_RB_FB(3, false);
 WOS_RB_FB(3, true);
+template __global__ void wos_first_ball_kernel<2, false, true, true>(const DevScene, const DevParams, const float*,
+                                                                     int64_t, int64_t, int64_t, const DevTasks,
+                                                                     unsigned long long*, unsigned int*, int, int);
+template __global__ void wos_first_ball_kernel<3, false, true, true>(const DevScene, const DevParams, const float*,
+                                                                     int64_t, int64_t, int64_t, const DevTasks,
+                                                                     unsigned long long*, unsigned int*, int, int);
 WOS_RB_WALK(2, false, false);
 WOS_RB_WALK(2, true, false);
 WOS_RB_WALK(3, false, false);
@@ -45,7 +51,16 @@ WOS_RB_TWO_PHASE(3, true);
 hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                                  int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
                                  unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                                 hipStream_t s) {
+                                 bool pre, hipStream_t s) {
+  if (pre) {
+    if (dim == 2)
+      hipLaunchKernelGGL((wos_first_ball_kernel<2, false, true, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm,
+                         pts, n, base, stride, tk, counters, work, 0, lhs_floats);
+    else
+      hipLaunchKernelGGL((wos_first_ball_kernel<3, false, true, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm,
+                         pts, n, base, stride, tk, counters, work, 0, lhs_floats);
+    return hipGetLastError();
+  }
 #define WOS_LAUNCH_FB(D, G)                                                                                       \
   hipLaunchKernelGGL((wos_first_ball_kernel<D, G, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, \
                      stride, tk, counters, work, geom_floats, lhs_floats)
@@ -114,6 +129,8 @@ hipError_t occupancy_rb(int which, int dim, bool geom_global, size_t shmem, int*
     case 1:
       if (dim == 2) return geom_global ? WOS_OCC((wos_walk_kernel<2, true, false, true>)) : WOS_OCC((wos_walk_kernel<2, false, false, true>));
       return geom_global ? WOS_OCC((wos_walk_kernel<3, true, false, true>)) : WOS_OCC((wos_walk_kernel<3, false, false, true>));
+    case 3:
+      return dim == 2 ? WOS_OCC((wos_first_ball_kernel<2, false, true, true>)) : WOS_OCC((wos_first_ball_kernel<3, false, true, true>));
     default:
       return geom_global ? WOS_OCC((wos_walk_kernel<2, true, true, true>)) : WOS_OCC((wos_walk_kernel<2, false, true, true>));
   }

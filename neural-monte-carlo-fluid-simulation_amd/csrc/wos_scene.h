@@ -68,6 +68,12 @@ struct DevScene {
   const float* dgroup;   // n_dgroups boxes over consecutive Dirichlet primitives
   int32_t n_pgroups, n_sgroups, n_dgroups;
   DevTree ptree, stree, dtree;  // hierarchies over pgroup / sgroup / dgroup
+  // fcpw's wide BVH over the Neumann primitives (wos_host_scene.h HostFcpwBvh), read
+  // from global memory by the stochastic boundary sample; nullptr without Neumann prims
+  const float* nbvh_box;
+  const int32_t* nbvh_child;
+  const int32_t* nbvh_ref;
+  int32_t nbvh_branch;
   // 1: the kernels read the geometry records from global memory (L2) instead of
   // staging them in LDS -- scenes too large for the LDS budget (set per solve)
   int32_t geom_global;
@@ -103,6 +109,8 @@ struct DevParams {
   int32_t ignore_neumann;
   int32_t ignore_source;
   int32_t robust;           // wos_solver_params.robust_float (Gfn::scaled)
+  int32_t fb_order;         // presorted first balls: 0 point order, 1 walk-queue order, 2 reversed
+  int32_t neumann_inert;    // 1: no ball can reach the float-overflow regime (walk kernel without the Neumann term)
   uint64_t seed;
   // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
   // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the
@@ -139,6 +147,7 @@ struct DevTasks {
   int32_t* pstate;  // [n] bit0 estimated, bit1 mask p, bit2 mask grad p, bits 8..12 cost bucket
   uint32_t* perm;   // [n] walk-queue order of the points (longest expected walks first)
   uint32_t* hist;   // [2 * kCostBuckets] bucket counts, then running bucket offsets
+  float* prad;      // [n] first-ball radius 0.99 min(dDist, nDist) (point-setup kernel -> presorted first balls)
   int64_t T;
   int32_t wpp;      // walks per point = n_pairs * n_anti
   // Boundary-start walks (estimateSolution, walk_on_stars.h:353-464; boundary value

@@ -51,6 +51,10 @@
 #define TWO_PI_D 6.283185307179586     /* 2.0f*M_PI evaluated in double */
 #define FOUR_PI_D 12.566370614359172   /* 4.0f*M_PI evaluated in double */
 #define FEPS FLT_EPSILON
+/* FCPW_MBVH_BRANCHING_FACTOR (FCPW_USE_EIGHT_WIDE_BRANCHING off) and FCPW_SIMD_WIDTH of an
+ * AVX/AVX2 build (fcpw CMakeLists.txt:83-99): the shape of the tree sampleNeumann walks */
+#define ORACLE_FCPW_BRANCH 4
+#define ORACLE_FCPW_LEAF 8
 
 /* ------------------------------------------------------------------------- */
 /* math mode                                                                 */
@@ -299,12 +303,18 @@ typedef struct {
     int ns;
     float (*sa)[3], (*sb)[3], (*sn0)[3], (*sn1)[3];
     int32_t *smiss;
+    /* fcpw's wide BVH (Neumann boundary; geom_build_fcpw_bvh) */
+    int nb_branch, nb_nodes, nb_leaves;
+    float *nb_box;        /* [node][branch][min.xyz max.xyz] */
+    int32_t *nb_child;    /* [node][branch]; leaf: [-(leaf+1), leaf count, first ref, ref count] */
+    int32_t *nb_ref;      /* reference -> primitive */
 } geom_t;
 
 static void geom_free(geom_t *g)
 {
     free(g->v); free(g->ix); free(g->vn); free(g->pe); free(g->en);
     free(g->sa); free(g->sb); free(g->sn0); free(g->sn1); free(g->smiss);
+    free(g->nb_box); free(g->nb_child); free(g->nb_ref);
     memset(g, 0, sizeof(*g));
 }
 
@@ -697,6 +707,303 @@ static void offset_point(int dim, const float *p, const float *n, float *out)
 }
 
 /* ------------------------------------------------------------------------- */
+/* fcpw's wide BVH over the Neumann boundary, for the stochastic boundary    */
+/* sample (sampleNeumann, fcpw_scene_loader.h:599-620).  The scene loader     */
+/* builds Bvh_OverlapSurfaceArea with vectorize = true (:161-164), i.e. an    */
+/* Sbvh (OverlapSurfaceArea cost, 8 buckets, packed leaves of FCPW_SIMD_WIDTH */
+/* references; sbvh.inl:3-235) collapsed into an Mbvh with                    */
+/* FCPW_MBVH_BRANCHING_FACTOR children (mbvh.inl:46-133).  fcpw's Scene<3>    */
+/* holds 2D segments with z = 0; boxes carry the FLT_EPSILON padding of       */
+/* BoundingBox::expandToInclude(point) in every axis.                          */
+/* ------------------------------------------------------------------------- */
+#define OR_BVH_BUCKETS 8
+#define OR_SBVH_MAX_DEPTH 64
+
+typedef struct { float mn[3], mx[3]; } obox_t;
+
+static void obox_empty(obox_t *b) { for (int k = 0; k < 3; k++) { b->mn[k] = FLT_MAX; b->mx[k] = -FLT_MAX; } }
+static void obox_point(obox_t *b, const float *p)
+{
+    for (int k = 0; k < 3; k++) { b->mn[k] = sminf(b->mn[k], p[k] - FEPS); b->mx[k] = smaxf(b->mx[k], p[k] + FEPS); }
+}
+static void obox_box(obox_t *b, const obox_t *o)
+{
+    for (int k = 0; k < 3; k++) { b->mn[k] = sminf(b->mn[k], o->mn[k]); b->mx[k] = smaxf(b->mx[k], o->mx[k]); }
+}
+/* BoundingBox::surfaceArea (bounding_volumes.h:131-135); Eigen's fixed-size-3 reductions
+ * pair as x0 op (x1 op x2) (Redux.h redux_novec_unroller) */
+static float obox_area(const obox_t *b)
+{
+    float e[3];
+    for (int k = 0; k < 3; k++) e[k] = smaxf(b->mx[k] - b->mn[k], 1e-5f);
+    float pr = e[0] * (e[1] * e[2]);
+    return 2.0f * (pr / e[0] + (pr / e[1] + pr / e[2]));
+}
+
+typedef struct { obox_t box; int off, n, second; } osnode_t;
+
+typedef struct {
+    int leaf, depth_guess, nn;
+    int *prim; obox_t *rb; float (*rc)[3];
+    osnode_t *nodes;
+} osbvh_t;
+
+/* computeSplitCost (sbvh.inl:3-37), OverlapSurfaceArea, packLeaves */
+static float osbvh_cost(const osbvh_t *s, const obox_t *l, const obox_t *r, int nl, int nr, int depth)
+{
+    if (depth > 0 && ((float)s->depth_guess / depth) < 1.5f && nl % s->leaf != 0 && nr % s->leaf != 0) return FLT_MAX;
+    obox_t bi;
+    for (int k = 0; k < 3; k++) { bi.mn[k] = smaxf(l->mn[k], r->mn[k]); bi.mx[k] = sminf(l->mx[k], r->mx[k]); }
+    float cost = ((float)nl / obox_area(r) + (float)nr / obox_area(l)) * fabsf(obox_area(&bi));
+    int valid = bi.mx[0] >= bi.mn[0] && bi.mx[1] >= bi.mn[1] && bi.mx[2] >= bi.mn[2];
+    if (!valid) cost *= -1.0f;
+    return cost;
+}
+
+static void osbvh_build(osbvh_t *s, int parent, int st, int en, int depth)
+{
+    int me = s->nn++;
+    obox_t bb, bc; obox_empty(&bb); obox_empty(&bc);
+    for (int p = st; p < en; p++) { obox_box(&bb, &s->rb[p]); obox_point(&bc, s->rc[p]); }
+    osnode_t *nd = &s->nodes[me];
+    nd->box = bb; nd->off = 0; nd->n = 0; nd->second = 0;
+    int nr = en - st;
+    int leaf = nr <= s->leaf || depth == OR_SBVH_MAX_DEPTH - 2;
+    if (leaf) { nd->off = st; nd->n = nr; }
+    /* the second child to touch its parent records its offset (sbvh.inl:182-192) */
+    if (parent >= 0 && me != parent + 1) s->nodes[parent].second = me - parent;
+    if (leaf) return;
+    /* computeObjectSplit (sbvh.inl:39-111) */
+    float best = FLT_MAX, coord = 0.0f;
+    int dim = -1;
+    for (int d = 0; d < 3; d++) {
+        float ext = bb.mx[d] - bb.mn[d];
+        if (ext < 1e-6f) continue;
+        float width = ext / OR_BVH_BUCKETS;
+        obox_t bk[OR_BVH_BUCKETS], rk[OR_BVH_BUCKETS], acc, lb;
+        int cnt[OR_BVH_BUCKETS], rcnt[OR_BVH_BUCKETS];
+        for (int b = 0; b < OR_BVH_BUCKETS; b++) { obox_empty(&bk[b]); cnt[b] = 0; rcnt[b] = 0; }
+        for (int p = st; p < en; p++) {
+            int b = (int)((s->rc[p][d] - bb.mn[d]) / width);
+            if (b < 0) b = 0;
+            if (b > OR_BVH_BUCKETS - 1) b = OR_BVH_BUCKETS - 1;
+            obox_box(&bk[b], &s->rb[p]); cnt[b]++;
+        }
+        obox_empty(&acc);
+        for (int b = OR_BVH_BUCKETS - 1; b > 0; b--) {
+            obox_box(&acc, &bk[b]); rk[b] = acc;
+            rcnt[b] = cnt[b] + (b != OR_BVH_BUCKETS - 1 ? rcnt[b + 1] : 0);
+        }
+        obox_empty(&lb);
+        int nl = 0;
+        for (int b = 1; b < OR_BVH_BUCKETS; b++) {
+            obox_box(&lb, &bk[b - 1]); nl += cnt[b - 1];
+            if (nl > 0 && rcnt[b] > 0) {
+                float c = osbvh_cost(s, &lb, &rk[b], nl, rcnt[b], depth);
+                if (c < best) { best = c; dim = d; coord = bb.mn[d] + (float)b * width; }
+            }
+        }
+    }
+    if (dim == -1) {  /* LongestAxisCenter fallback: the first longest centroid-box axis */
+        dim = 0;
+        float m = bc.mx[0] - bc.mn[0];
+        for (int k = 1; k < 3; k++) if (bc.mx[k] - bc.mn[k] > m) { m = bc.mx[k] - bc.mn[k]; dim = k; }
+        coord = (bc.mn[dim] + bc.mx[dim]) * 0.5f;
+    }
+    /* performObjectSplit (sbvh.inl:113-140) */
+    int mid = st;
+    for (int i = st; i < en; i++) {
+        if (s->rc[i][dim] < coord) {
+            int tp = s->prim[i]; s->prim[i] = s->prim[mid]; s->prim[mid] = tp;
+            obox_t tb = s->rb[i]; s->rb[i] = s->rb[mid]; s->rb[mid] = tb;
+            float tc[3]; memcpy(tc, s->rc[i], 12); memcpy(s->rc[i], s->rc[mid], 12); memcpy(s->rc[mid], tc, 12);
+            mid++;
+        }
+    }
+    if (mid == st || mid == en) {
+        mid = st + (en - st) / 2;
+        while ((mid - st) % s->leaf != 0 && mid < en) mid++;
+        if (mid == en) mid = st + (en - st) / 2;
+    }
+    osbvh_build(s, me, st, mid, depth + 1);
+    osbvh_build(s, me, mid, en, depth + 1);
+}
+
+/* collapseSbvh (mbvh.inl:46-133) */
+static int ombvh_collapse(geom_t *g, const osbvh_t *s, int si)
+{
+    const int B = g->nb_branch;
+    const osnode_t *sn = &s->nodes[si];
+    int mi = g->nb_nodes++;
+    for (int w = 0; w < B; w++) {
+        float *bx = g->nb_box + ((size_t)mi * B + w) * 6;
+        for (int k = 0; k < 3; k++) { bx[k] = FLT_MAX; bx[3 + k] = -FLT_MAX; }
+        g->nb_child[(size_t)mi * B + w] = INT32_MAX;
+    }
+    if (sn->n > 0) {
+        int32_t *c = g->nb_child + (size_t)mi * B;
+        c[0] = -(g->nb_leaves + 1);
+        c[1] = sn->n / s->leaf + (sn->n % s->leaf != 0);
+        c[2] = sn->off; c[3] = sn->n;
+        g->nb_leaves += c[1];
+        return mi;
+    }
+    int list[8], cnt = 2;
+    list[0] = si + sn->second; list[1] = si + 1;
+    while (cnt < B) {
+        float best = -FLT_MAX; int bi = -1;
+        for (int i = 0; i < cnt; i++) {
+            const osnode_t *c = &s->nodes[list[i]];
+            if (c->n == 0) { float a = obox_area(&c->box); if (best < a) { best = a; bi = i; } }
+        }
+        if (bi < 0) break;
+        int x = list[bi];
+        list[bi] = x + s->nodes[x].second;
+        list[cnt++] = x + 1;
+    }
+    for (int i = 1; i < cnt; i++)  /* std::sort, ascending */
+        for (int j = i; j > 0 && list[j - 1] > list[j]; j--) { int t = list[j]; list[j] = list[j - 1]; list[j - 1] = t; }
+    for (int i = 0; i < cnt; i++) {
+        const osnode_t *c = &s->nodes[list[i]];
+        float *bx = g->nb_box + ((size_t)mi * B + i) * 6;
+        for (int k = 0; k < 3; k++) { bx[k] = c->box.mn[k]; bx[3 + k] = c->box.mx[k]; }
+        g->nb_child[(size_t)mi * B + i] = ombvh_collapse(g, s, list[i]);
+    }
+    return mi;
+}
+
+static int geom_build_fcpw_bvh(geom_t *g, int branch, int leaf)
+{
+    int np = g->np, nvp = g->dim;
+    if (np <= 0) return 0;
+    osbvh_t s;
+    memset(&s, 0, sizeof(s));
+    s.leaf = leaf;
+    s.depth_guess = (int)log2((double)np);
+    s.prim = (int *)malloc(sizeof(int) * np);
+    s.rb = (obox_t *)malloc(sizeof(obox_t) * np);
+    s.rc = (float (*)[3])malloc(sizeof(float) * 3 * np);
+    s.nodes = (osnode_t *)malloc(sizeof(osnode_t) * 2 * (size_t)np);
+    g->nb_branch = branch;
+    g->nb_box = (float *)malloc(sizeof(float) * 6 * branch * 2 * (size_t)np);
+    g->nb_child = (int32_t *)malloc(sizeof(int32_t) * branch * 2 * (size_t)np);
+    if (!s.prim || !s.rb || !s.rc || !s.nodes || !g->nb_box || !g->nb_child) return -1;
+    for (int i = 0; i < np; i++) {
+        s.prim[i] = i;
+        obox_empty(&s.rb[i]);
+        for (int v = 0; v < nvp; v++) obox_point(&s.rb[i], g->v[g->ix[i][v]]);
+        const float *pa = g->v[g->ix[i][0]], *pb = g->v[g->ix[i][1]];
+        for (int k = 0; k < 3; k++)
+            s.rc[i][k] = nvp == 2 ? (pa[k] + pb[k]) * 0.5f : (pa[k] + pb[k] + g->v[g->ix[i][2]][k]) / 3.0f;
+    }
+    osbvh_build(&s, -1, 0, np, 0);
+    g->nb_nodes = 0; g->nb_leaves = 0;
+    ombvh_collapse(g, &s, 0);
+    g->nb_ref = (int32_t *)malloc(sizeof(int32_t) * np);
+    for (int i = 0; i < np; i++) g->nb_ref[i] = s.prim[i];
+    free(s.prim); free(s.rb); free(s.rc); free(s.nodes);
+    return 0;
+}
+
+/* Mbvh::intersectStochasticFromNode (mbvh.inl:1099-1283) with LineSegment /
+ * Triangle leaves (intersectSpherePrimitives, :835-982), the traversal weight of the
+ * demo scene (|HarmonicGreensFnFreeSpace<3>::evaluate(max(r, 1e-2))|, scene.h:157-160)
+ * and no primitive weight.  One root-to-leaf path; returns the chosen primitive (or
+ * -1: no sample) and its selection pdf ((weight * traversalPdf) / leaf total). */
+static int fcpw_stochastic_pick(const geom_t *g, const float *x, float R, float u, float *sel_pdf)
+{
+    const int B = g->nb_branch;
+    const float r2 = R * R;
+    float c[3] = {x[0], x[1], g->dim == 3 ? x[2] : 0.0f};
+    float tpdf = 1.0f, d2NodeMax = FLT_MAX;
+    int node = 0;
+    for (;;) {
+        const int32_t *C = g->nb_child + (size_t)node * B;
+        if (C[0] < 0) {
+            int inside = d2NodeMax <= r2, sel = -1;
+            float total = 0.0f, selw = 0.0f, uu = u;
+            for (int p = 0; p < C[3]; p++) {
+                int q = g->nb_ref[C[2] + p];
+                float d2 = 0.0f;
+                if (!inside) {
+                    float pt[3], t0 = 0, t1 = 0, d;
+                    if (g->dim == 2) d = closest_point_segment(g->v[g->ix[q][0]], g->v[g->ix[q][1]], c, pt, &t0);
+                    else d = closest_point_triangle(g->v[g->ix[q][0]], g->v[g->ix[q][1]], g->v[g->ix[q][2]], c, pt, &t0, &t1);
+                    d2 = d * d;
+                }
+                if (d2 <= r2) {
+                    float w = prim_area(g, q);
+                    total += w;
+                    float prob = w / total;
+                    if (uu < prob) { uu = uu / prob; sel = q; selw = w; }
+                    else uu = (uu - prob) / (1.0f - prob);
+                }
+            }
+            if (sel < 0) return -1;
+            float d = selw * tpdf;
+            if (total > 0.0f) d /= total;
+            *sel_pdf = d;
+            return sel;
+        }
+        int sel = -1;
+        float tot = 0.0f, selw = 0.0f, selmax = 0.0f;
+        for (int w = 0; w < B; w++) {
+            if (C[w] == INT32_MAX) continue;
+            const float *bx = g->nb_box + ((size_t)node * B + w) * 6;
+            /* overlapWideBox (wide_query_operations.h:96-106) */
+            float mn[3], mx[3], ctr[3];
+            for (int k = 0; k < 3; k++) {
+                float a = bx[k] - c[k], b = c[k] - bx[3 + k];
+                mn[k] = smaxf(smaxf(a, b), 0.0f);
+                mx[k] = sminf(a, b);
+            }
+            float d2min = dot3(mn, mn), d2max = dot3(mx, mx);
+            if (!(d2min <= r2)) continue;
+            for (int k = 0; k < 3; k++) ctr[k] = c[k] - (bx[k] + bx[3 + k]) * 0.5f;
+            float rr = smaxf(sqrtf(dot3(ctr, ctr)), 1e-2f);
+            float weight = fabsf((float)(1.0 / (FOUR_PI_D * (double)rr)));
+            tot += weight;
+            float prob = weight / tot;
+            if (u < prob) { sel = w; selw = weight; selmax = d2max; u = u / prob; }
+            else u = (u - prob) / (1.0f - prob);
+        }
+        if (sel < 0) return -1;
+        node = C[sel];
+        tpdf *= selw / tot;
+        d2NodeMax = selmax;
+    }
+}
+
+/* the stochastic pick for a batch of uniforms at one ball (CPU property tests) */
+int oracle_fcpw_pick(const oracle_scene_desc *scene, const float *x, float R, int n, const float *us, int32_t *sel,
+                     float *pdf);
+
+/* the tree as built (CPU test against the product's host build) */
+int oracle_fcpw_bvh(int dim, const float *v, int nv, const int32_t *ix, int np, int branch, int leaf,
+                    float *box, int32_t *child, int32_t *ref, int cap_nodes, int *n_nodes)
+{
+    geom_t g;
+    memset(&g, 0, sizeof(g));
+    g.dim = dim; g.nv = nv; g.np = np;
+    g.v = (float (*)[3])calloc((size_t)nv, sizeof(float) * 3);
+    g.ix = (int32_t (*)[3])calloc((size_t)np, sizeof(int32_t) * 3);
+    for (int i = 0; i < nv; i++) for (int k = 0; k < dim; k++) g.v[i][k] = v[i * dim + k];
+    for (int p = 0; p < np; p++) for (int k = 0; k < dim; k++) g.ix[p][k] = ix[p * dim + k];
+    int rc = geom_build_fcpw_bvh(&g, branch, leaf);
+    if (rc == 0) {
+        *n_nodes = g.nb_nodes;
+        if (g.nb_nodes > cap_nodes) rc = -2;
+        else {
+            memcpy(box, g.nb_box, sizeof(float) * 6 * branch * (size_t)g.nb_nodes);
+            memcpy(child, g.nb_child, sizeof(int32_t) * branch * (size_t)g.nb_nodes);
+            memcpy(ref, g.nb_ref, sizeof(int32_t) * (size_t)np);
+        }
+    }
+    free(g.v); free(g.ix); free(g.nb_box); free(g.nb_child); free(g.nb_ref);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
 /* scene                                                                      */
 /* ------------------------------------------------------------------------- */
 typedef struct {
@@ -715,6 +1022,7 @@ static int scene_build(scene_t *sc, const oracle_scene_desc *d)
     sc->dim = d->dim;
     if (geom_build(&sc->neu, d->dim, d->n_vertices, d->n_prims, d->vertices, d->prims, 1, d->is_double_sided)) return -1;
     if (geom_build(&sc->dir, d->dim, d->n_dvertices, d->n_dprims, d->dvertices, d->dprims, 0, d->is_double_sided)) return -1;
+    if (geom_build_fcpw_bvh(&sc->neu, ORACLE_FCPW_BRANCH, ORACLE_FCPW_LEAF)) return -1;
     /* computeBoundingBox (fcpw_scene_loader.h:75-93), BoundingBox::expandToInclude pads by FLT_EPSILON */
     for (int k = 0; k < 3; k++) { sc->pmin[k] = FLT_MAX; sc->pmax[k] = -FLT_MAX; }
     const geom_t *gs[2] = {&sc->neu, &sc->dir};
@@ -734,6 +1042,17 @@ static int scene_build(scene_t *sc, const oracle_scene_desc *d)
 }
 
 static void scene_free(scene_t *sc) { geom_free(&sc->neu); geom_free(&sc->dir); }
+
+int oracle_fcpw_pick(const oracle_scene_desc *scene, const float *x, float R, int n, const float *us, int32_t *sel,
+                     float *pdf)
+{
+    scene_t sc;
+    if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
+    if (sc.neu.np <= 0) { scene_free(&sc); return -1; }
+    for (int i = 0; i < n; i++) { pdf[i] = 0.0f; sel[i] = fcpw_stochastic_pick(&sc.neu, x, R, us[i], &pdf[i]); }
+    scene_free(&sc);
+    return 0;
+}
 
 /* computeDistToDirichlet (fcpw_scene_loader.h:299-315) */
 static float dist_dirichlet(const scene_t *sc, const float *x, int signed_)
@@ -1120,39 +1439,16 @@ typedef struct {
 
 /* Neumann boundary sample + contribution (walk_on_stars.h:212-260).  With the
  * reference's h == 0 (scene.h:176-181) the term is exactly +0 unless G or the
- * throughput is non-finite; only then is the brute-force stochastic sample run. */
+ * throughput is non-finite; only then is the stochastic sample run. */
 static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float R, const float *rn)
 {
     const geom_t *ng = &sc->neu;
     int nonfinite = !isfinite(st->throughput) || (g->yukawa && !g->scaled && g->muR > 85.0f);
     if (!nonfinite || ng->np <= 0) return;
     const float *x = st->pt;
-    /* select a primitive overlapping the ball ~ area * |G_harmonic3D(max(d,1e-2))| */
-    float total = 0.0f;
-    for (int p = 0; p < ng->np; p++) {
-        cp_t c; float pt[3], t0 = 0, t1 = 0, d;
-        (void)c;
-        if (ng->dim == 2) d = closest_point_segment(ng->v[ng->ix[p][0]], ng->v[ng->ix[p][1]], x, pt, &t0);
-        else d = closest_point_triangle(ng->v[ng->ix[p][0]], ng->v[ng->ix[p][1]], ng->v[ng->ix[p][2]], x, pt, &t0, &t1);
-        if (d * d <= R * R) {
-            float r = smaxf(sqrtf(d * d), 1e-2f);
-            total += prim_area(ng, p) * fabsf((float)(1.0 / (FOUR_PI_D * (double)r)));
-        }
-    }
-    if (!(total > 0.0f)) return;
-    float target = rn[0] * total, acc = 0.0f;
-    int sel = -1; float selw = 0.0f;
-    for (int p = 0; p < ng->np; p++) {
-        float pt[3], t0 = 0, t1 = 0, d;
-        if (ng->dim == 2) d = closest_point_segment(ng->v[ng->ix[p][0]], ng->v[ng->ix[p][1]], x, pt, &t0);
-        else d = closest_point_triangle(ng->v[ng->ix[p][0]], ng->v[ng->ix[p][1]], ng->v[ng->ix[p][2]], x, pt, &t0, &t1);
-        if (d * d <= R * R) {
-            float r = smaxf(sqrtf(d * d), 1e-2f);
-            float w = prim_area(ng, p) * fabsf((float)(1.0 / (FOUR_PI_D * (double)r)));
-            acc += w; sel = p; selw = w;
-            if (target < acc) break;
-        }
-    }
+    /* sampleNeumann: fcpw's stochastic traversal picks the primitive (randNums[0]) */
+    float sel_pdf = 0.0f;
+    int sel = fcpw_stochastic_pick(ng, x, R, rn[0], &sel_pdf);
     if (sel < 0) return;
     float sp[3], sn[3], pdf;
     if (ng->dim == 2) {
@@ -1170,7 +1466,8 @@ static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float 
         for (int k = 0; k < 3; k++) { sp[k] = pa[k] * u + pb[k] * v + pc[k] * w; sn[k] /= area; }
         pdf = 2.0f / area;
     }
-    pdf *= selw / total;
+    /* Interaction::d: (weight * traversalPdf) / total, then *= samplePoint's pdf */
+    pdf = sel_pdf * pdf;
     float dts[3]; sub3(dts, sp, x);
     if (sc->dim == 2) dts[2] = 0.0f;
     float distToSample = norm3(dts);

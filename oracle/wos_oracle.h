@@ -107,6 +107,14 @@ double oracle_bessel(int which, double x, int math_mode); /* 0:i0 1:i1 2:k0 3:k1
 double oracle_math(int which, double x, int math_mode);   /* 0 exp 1 log 2 sin 3 cos 4 atan, f32: 10 expf 11 logf 12 sinf 13 cosf 14 cbrtf */
 uint32_t oracle_seed32(uint64_t key, uint64_t idx, uint64_t pair, uint32_t tag);
 int oracle_lhs(uint32_t seed, int n, int dims, float *out); /* stratified samples */
+/* fcpw's wide BVH over a boundary mesh as the oracle builds it (cap_nodes nodes of
+ * `branch` children: box [6 * branch], child [branch]; ref [np]) */
+/* fcpw's stochastic traversal (sampleNeumann's primitive choice) at ball (x, R) for
+ * n uniforms: chosen primitive (-1: none) and its selection pdf */
+int oracle_fcpw_pick(const oracle_scene_desc *scene, const float *x, float R, int n, const float *us, int32_t *sel,
+                     float *pdf);
+int oracle_fcpw_bvh(int dim, const float *v, int nv, const int32_t *ix, int np, int branch, int leaf,
+                    float *box, int32_t *child, int32_t *ref, int cap_nodes, int *n_nodes);
 
 #ifdef __cplusplus
 }

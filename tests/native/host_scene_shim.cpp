@@ -188,3 +188,17 @@ extern "C" int hs_group_tree(const float* groups, int stride, int ngroups, float
   }
   return (int)t.node.size();
 }
+
+// ---- fcpw's wide BVH over the Neumann boundary (csrc/wos_fcpw_bvh.cpp) ----
+extern "C" int hs_fcpw_bvh(int dim, const float* v, int nv, const int* ix, int np, int branch, int leaf, float* box,
+                           int* child, int* ref, int cap_nodes, int* n_nodes) {
+  (void)nv;
+  wos::HostFcpwBvh b;
+  wos::build_fcpw_bvh(dim, v, ix, np, branch, leaf, b);
+  *n_nodes = b.n_nodes;
+  if (b.n_nodes > cap_nodes) return -2;
+  std::copy(b.box.begin(), b.box.end(), box);
+  std::copy(b.child.begin(), b.child.end(), child);
+  std::copy(b.ref.begin(), b.ref.end(), ref);
+  return 0;
+}

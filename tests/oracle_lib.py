@@ -90,6 +90,12 @@ def lib():
                                  C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(Stats)]
         L.oracle_lhs.restype = C.c_int
         L.oracle_lhs.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_fcpw_pick.restype = C.c_int
+        L.oracle_fcpw_pick.argtypes = [C.POINTER(SceneDesc), C.c_void_p, C.c_float, C.c_int, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]
+        L.oracle_fcpw_bvh.restype = C.c_int
+        L.oracle_fcpw_bvh.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -193,6 +199,35 @@ def point_info(scene: OracleScene, pt):
         raise RuntimeError("oracle_point_info failed")
     keys = ["dirichlet_dist", "neumann_dist", "signed_neumann_dist", "inside", "star_radius", "n_silhouettes"]
     return {k: o.value for k, o in zip(keys, out)}
+
+
+def fcpw_pick(scene: OracleScene, x, R, us):
+    """fcpw's stochastic traversal at ball (x, R) for each uniform in us: (primitive or -1, selection pdf)."""
+    xr = np.asarray(x, np.float32).ravel()
+    x = np.zeros(3, np.float32)
+    x[:len(xr)] = xr
+    us = np.ascontiguousarray(us, np.float32)
+    sel = np.zeros(len(us), np.int32)
+    pdf = np.zeros(len(us), np.float32)
+    rc = lib().oracle_fcpw_pick(C.byref(scene.desc), x.ctypes.data, float(R), len(us), us.ctypes.data,
+                                sel.ctypes.data, pdf.ctypes.data)
+    assert rc == 0, rc
+    return sel, pdf
+
+
+def fcpw_bvh(v, ix, dim, branch=4, leaf=8):
+    """The oracle's restatement of fcpw's wide BVH: (box [n, branch, 6], child [n, branch], ref)."""
+    v = np.ascontiguousarray(v, np.float32)
+    ix = np.ascontiguousarray(ix, np.int32)
+    cap = 2 * ix.shape[0] + 8
+    box = np.zeros(cap * branch * 6, np.float32)
+    child = np.zeros(cap * branch, np.int32)
+    ref = np.zeros(ix.shape[0], np.int32)
+    n = C.c_int(0)
+    rc = lib().oracle_fcpw_bvh(dim, v.ctypes.data, v.shape[0], ix.ctypes.data, ix.shape[0], branch, leaf,
+                               box.ctypes.data, child.ctypes.data, ref.ctypes.data, cap, C.byref(n))
+    assert rc == 0, rc
+    return box[:n.value * branch * 6].reshape(n.value, branch, 6), child[:n.value * branch].reshape(n.value, branch), ref
 
 
 def lhs(seed, n, dims):

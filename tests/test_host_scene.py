@@ -28,6 +28,7 @@ def shim(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("hs") / "libhs.so")
     subprocess.run(["g++", "-std=c++17", "-O1", "-fPIC", "-shared", "-ffp-contract=off", "-I", CSRC,
                     os.path.join(HERE, "native", "host_scene_shim.cpp"), os.path.join(CSRC, "wos_host_scene.cpp"),
+                    os.path.join(CSRC, "wos_fcpw_bvh.cpp"),
                     "-o", out], check=True)
     return C.CDLL(out)
 

@@ -122,6 +122,7 @@ def rej_table(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("rt") / "libhs.so")
     subprocess.run(["g++", "-std=c++17", "-O1", "-fPIC", "-shared", "-ffp-contract=off", "-I", CSRC,
                     os.path.join(HERE, "native", "host_scene_shim.cpp"), os.path.join(CSRC, "wos_host_scene.cpp"),
+                    os.path.join(CSRC, "wos_fcpw_bvh.cpp"),
                     "-o", out], check=True)
     lib = C.CDLL(out)
     tabs = {}
@@ -166,6 +167,7 @@ def rej_env(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("re") / "libhs.so")
     subprocess.run(["g++", "-std=c++17", "-O1", "-fPIC", "-shared", "-ffp-contract=off", "-I", CSRC,
                     os.path.join(HERE, "native", "host_scene_shim.cpp"), os.path.join(CSRC, "wos_host_scene.cpp"),
+                    os.path.join(CSRC, "wos_fcpw_bvh.cpp"),
                     "-o", out], check=True)
     lib = C.CDLL(out)
     envs = {}

@@ -44,7 +44,7 @@ LIB = os.path.join(PKG, "lib", "libwos_hip.so")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="B", help="A, B, B_grid, C, D or E (SURVEY.md section 8(d))")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"])

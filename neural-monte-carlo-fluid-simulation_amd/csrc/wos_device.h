@@ -2917,7 +2917,9 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
     }
     tk.thr[t] = throughput;
     tk.tsrc[t] = totalSource;
-    tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
+    // without Dirichlet geometry the distance is the bbox far corner of the walk start,
+    // recomputed by the walk kernel from the same floats instead of stored and reloaded
+    if (sc.n_dprims > 0) tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
   }
 }
 
@@ -3552,7 +3554,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
           for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
           s_thr = tk.thr[s_t];
           s_tsrc = tk.tsrc[s_t];
-          s_dd = tk.dd[s_t];
+          s_dd = (BSTART || sc.n_dprims > 0) ? tk.dd[s_t] : bbox_far_dist<DIM>(sc, s_pt);
         }
       }
       S += take;
@@ -3598,7 +3600,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
           for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];
           v_thr = tk.thr[v_t];
           v_tsrc = tk.tsrc[v_t];
-          v_dd = tk.dd[v_t];
+          // boundary-start walks (BVC) always carry a stored distance
+          v_dd = (BSTART || sc.n_dprims > 0) ? tk.dd[v_t] : bbox_far_dist<DIM>(sc, v_pt);
         }
         if (t < 0 && rank < take) {
           t = (int64_t)v_t;
@@ -3734,7 +3737,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       float v_pt[DIM];
       for (int k = 0; k < DIM; k++) v_pt[k] = tk.pt[k * T + t];
       const uint32_t w = ((uint32_t)t - pidx * wpp) >> (prm.n_anti - 1);
-      walk_start<DIM, false, RB>(sc, prm, tk, t, pidx, w, v_pt, tk.thr[t], tk.tsrc[t], tk.dd[t], base, stride, yuk0,
+      walk_start<DIM, false, RB>(sc, prm, tk, t, pidx, w, v_pt, tk.thr[t], tk.tsrc[t],
+                                 sc.n_dprims > 0 ? tk.dd[t] : bbox_far_dist<DIM>(sc, v_pt), base, stride, yuk0,
                                  st, g, ws, ddist, wsteps, firstR);
     }
     if (__ballot(ok) == 0) continue;
@@ -3801,7 +3805,16 @@ __global__ __launch_bounds__(256) void wos_surv_scatter_kernel(const DevTasks tk
 // block's points are contiguous (point-major tasks), so they are staged through
 // LDS in chunks of kFoldChunk records per point with coalesced 64-B loads, then
 // every thread folds its own point's chunk in walk order.
-constexpr int kFoldPoints = 128, kFoldChunk = 16;
+#ifndef WOS_FOLD_POINTS
+#define WOS_FOLD_POINTS 128
+#endif
+#ifndef WOS_FOLD_CHUNK
+#define WOS_FOLD_CHUNK 16
+#endif
+#ifndef WOS_FOLD_UNROLL
+#define WOS_FOLD_UNROLL 4
+#endif
+constexpr int kFoldPoints = WOS_FOLD_POINTS, kFoldChunk = WOS_FOLD_CHUNK, kFoldUnroll = WOS_FOLD_UNROLL;
 
 template <int DIM>
 __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
@@ -3827,16 +3840,32 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   uint32_t steps = 0;
   for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
     const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
-    for (int e = tid; e < nb * kFoldChunk; e += kFoldPoints) {
-      const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
-      if (j >= cnt) continue;
-      const int64_t t = (p0 + pp) * wpp + c0 + j;
-      lds[0][pp][j] = __uint_as_float(tk.code[t]);
-      lds[1][pp][j] = tk.total[t];
-      lds[2][pp][j] = tk.first[t];
-      for (int k = 0; k < DIM; k++) {
-        lds[3 + k][pp][j] = tk.bdir[k * T + t];
-        lds[3 + DIM + k][pp][j] = tk.sdir[k * T + t];
+    // kFoldUnroll staging slots in flight per thread: all their loads are issued
+    // before the first LDS store (one HBM round trip per kFoldUnroll slots, not per slot)
+    for (int e0 = tid; e0 < nb * kFoldChunk; e0 += kFoldPoints * kFoldUnroll) {
+      float v[kFoldUnroll][NF];
+#pragma unroll
+      for (int u = 0; u < kFoldUnroll; u++) {
+        const int e = e0 + u * kFoldPoints;
+        const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
+        if (e >= nb * kFoldChunk || j >= cnt) continue;
+        const int64_t t = (p0 + pp) * wpp + c0 + j;
+        v[u][0] = __uint_as_float(tk.code[t]);
+        v[u][1] = tk.total[t];
+        v[u][2] = tk.first[t];
+#pragma unroll
+        for (int k = 0; k < DIM; k++) {
+          v[u][3 + k] = tk.bdir[k * T + t];
+          v[u][3 + DIM + k] = tk.sdir[k * T + t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kFoldUnroll; u++) {
+        const int e = e0 + u * kFoldPoints;
+        const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
+        if (e >= nb * kFoldChunk || j >= cnt) continue;
+#pragma unroll
+        for (int f = 0; f < NF; f++) lds[f][pp][j] = v[u][f];
       }
     }
     __syncthreads();

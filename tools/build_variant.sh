@@ -13,7 +13,8 @@ hipcc $FLAGS -c csrc/wos_robust.hip -o build/var/r_$NAME.o &
 hipcc $FLAGS -c csrc/wos_capi.hip -o build/var/c_$NAME.o &
 hipcc $FLAGS -x hip -c csrc/wos_host_scene.cpp -o build/var/s_$NAME.o &
 hipcc $FLAGS -x hip -c csrc/wos_bvc_host.cpp -o build/var/h_$NAME.o &
+hipcc $FLAGS -x hip -c csrc/wos_fcpw_bvh.cpp -o build/var/t_$NAME.o &
 wait
 hipcc --offload-arch=gfx950 -shared -fPIC -o lib/var/libwos_$NAME.so build/var/k_$NAME.o build/var/b_$NAME.o build/var/r_$NAME.o \
-  build/var/c_$NAME.o build/var/s_$NAME.o build/var/h_$NAME.o
+  build/var/c_$NAME.o build/var/s_$NAME.o build/var/h_$NAME.o build/var/t_$NAME.o
 echo lib/var/libwos_$NAME.so

@@ -2718,6 +2718,40 @@ __device__ __forceinline__ void lhs_permute(float* strat, const int* partner, in
   wave_sync();
 }
 
+// The same shuffle simulated step by step in registers, for nstrat <= 128: lane L
+// holds positions L and L + 64; step j reads a[j] and a[partner[j]] with v_readlane
+// (j and partner[j] are wave-uniform) and the two owning lanes take each other's
+// value -- the sequential swaps themselves, so the result is exact by construction.
+// No LDS traffic and no wave syncs inside the loop, but 128 dependent readlane steps:
+// measured slower (karman first balls 0.62 -> 0.80 ms, cube 1.67 -> 2.31 ms,
+// profiles/r2l_ab_lhs.log), so off by default.
+#ifndef WOS_LHS_LANES
+#define WOS_LHS_LANES 0
+#endif
+__device__ __forceinline__ void lhs_permute_lanes(float* strat, const int* partner, int nstrat, int sd, int dimi,
+                                                  int lane) {
+  const int* pd = partner + dimi * nstrat;
+  float a0 = lane < nstrat ? strat[sd * lane + dimi] : 0.0f;
+  float a1 = lane + kWave < nstrat ? strat[sd * (lane + kWave) + dimi] : 0.0f;
+  const int p0 = lane < nstrat ? pd[lane] : 0;
+  const int p1 = lane + kWave < nstrat ? pd[lane + kWave] : 0;
+  for (int j = 0; j < nstrat; j++) {
+    const int jl = j & (kWave - 1);
+    const bool jhi = j >= kWave;  // wave-uniform
+    const int q = __builtin_amdgcn_readlane(jhi ? p1 : p0, jl);
+    const int ql = q & (kWave - 1);
+    const bool qhi = q >= kWave;
+    const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(jhi ? a1 : a0), jl));
+    const float vq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qhi ? a1 : a0), ql));
+    if (lane == jl) { if (jhi) a1 = vq; else a0 = vq; }
+    if (lane == ql) { if (qhi) a1 = vj; else a0 = vj; }
+  }
+  wave_sync();
+  if (lane < nstrat) strat[sd * lane + dimi] = a0;
+  if (lane + kWave < nstrat) strat[sd * (lane + kWave) + dimi] = a1;
+  wave_sync();
+}
+
 // per-wave first-ball scratch after the stratified samples and partners: the
 // rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute
 __host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
@@ -2761,6 +2795,10 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
         for (int j = 0; j < nstrat; ++j) partner[i * nstrat + j] = j + (int)q.bounded((uint32_t)(nstrat - j));
     }
     wave_sync();
+  }
+  if (WOS_LHS_LANES && nstrat <= 2 * kWave) {
+    for (int i = 0; i < sd; ++i) lhs_permute_lanes(strat, partner, nstrat, sd, i, lane);
+    return;
   }
   if (nstrat <= 4 * kWave) {
     for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);

@@ -3491,6 +3491,12 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // Dirichlet distance), loaded one iteration ahead; 0 (default, measured faster on
 // every config: the staged records cost registers the step needs): only the task
 // index and its point's state are staged, the record is loaded at hand-out
+// 1: refill the ring right after the hand-out instead of at the end of the iteration
+// (the staged tasks' loads get a whole step to land): within noise on karman / C / D,
+// with the staged records as well (WOS_TASK_RING) slower (profiles/r2e_ab_refill.log)
+#ifndef WOS_EARLY_REFILL
+#define WOS_EARLY_REFILL 0
+#endif
 #ifndef WOS_TASK_RING
 #define WOS_TASK_RING 0
 #endif
@@ -3662,6 +3668,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         S -= take;
       }
     }
+    // early refill: the ring is topped up right after the hand-out, so the loads of the
+    // staged tasks (queue window, permutation, point state) have the whole step to land
+    // before the next hand-out reads them
+    if (WOS_EARLY_REFILL) refill(tk);
     if (__ballot(t >= 0) == 0) {
       if (S == 0 && exhausted) break;  // queue drained and every lane idle
       refill(tk);
@@ -3689,7 +3699,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;
     }
-    refill(tk);
+    if (!WOS_EARLY_REFILL) refill(tk);
     DIAG_ADD(D_LOOP, t_loop);
 #if WOS_DIAG
     if (exhausted) {

@@ -327,7 +327,8 @@ __device__ Closest closest_wave_grouped(const float* prims, const float* groups,
 // update rule (smaller fl(d*d), or equal and a larger index) makes the result the
 // brute-force one whatever the visiting order, as in closest_wave.
 template <int DIM>
-__device__ Closest closest_lane(const float* prims, const float* groups, int np, int ng, const float* x) {
+__device__ Closest closest_lane(const float* prims, const float* groups, int np, int ng, const float* x,
+                                int sub = 0, int nsub = 1) {
   constexpr int PS = Layout<DIM>::prim;
   float bk = kFltMax;
   int bi = -1;
@@ -340,12 +341,18 @@ __device__ Closest closest_lane(const float* prims, const float* groups, int np,
       if (d2 < bk || (d2 == bk && p > bi)) { bk = d2; bi = p; }
     }
   };
-  if (ng <= 16) {  // small meshes: every primitive, uniform addresses (scalar loads)
-    for (int p = 0; p < np; p++) {
+  if (ng <= 16) {  // small meshes: every primitive (lane `sub` of nsub: every nsub-th one)
+    for (int p = sub; p < np; p += nsub) {
       float pt[DIM], t0, t1;
       const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
       const float d2 = d * d;
       if (d2 <= bk) { bk = d2; bi = p; }
+    }
+    // the nsub lanes of a point are adjacent (nsub a power of two): min fl(d*d), larger index on ties
+    for (int off = 1; off < nsub; off <<= 1) {
+      const float ok = __shfl_xor(bk, off);
+      const int oi = __shfl_xor(bi, off);
+      if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
     }
     ng = 0;
   } else {
@@ -3087,7 +3094,14 @@ __device__ __forceinline__ int32_t point_state(const DevScene& sc, const DevPara
   return (estimate ? kPtEstimate : 0) | (maskP ? kPtMaskP : 0) | (maskG ? kPtMaskG : 0) | (bucket << 8);
 }
 
-// Point setup for the presorted first balls: one point per lane (the exact scans of
+// lanes per point of the setup kernel's small-mesh scans: 4 measured -9 us on karman,
+// +13 / +20 us on C / the cube (profiles/r2s_ab_setup_lanes.log): 1
+#ifndef WOS_SETUP_LANES
+#define WOS_SETUP_LANES 1
+#endif
+constexpr int kSetupLanes = WOS_SETUP_LANES;  // lanes per point of wos_point_setup_kernel (power of two)
+static_assert((kSetupLanes & (kSetupLanes - 1)) == 0 && kSetupLanes <= kWave, "kSetupLanes");
+// Point setup for the presorted first balls: one point per kSetupLanes lanes (the exact scans of
 // closest_lane), pstate + first-ball radius per point and the bucket histogram.  The
 // first-ball kernel then takes the points in descending radius order, so the points
 // whose 64 lanes run the longest rejection loops start first instead of anywhere in
@@ -3099,19 +3113,23 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
   __shared__ uint32_t s_hist[kCostBuckets];
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // kSetupLanes adjacent lanes per point share the small-mesh scans (closest_lane);
+  // the first of them writes the point's state
+  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = gi / kSetupLanes;
+  const int sub = (int)(gi % kSetupLanes);
   if (i < n) {
     float x[DIM];
     for (int k = 0; k < DIM; k++) x[k] = pts[i * DIM + k];
     float nDist = kFltMax, nSigned = kFltMax;
     if (sc.n_prims > 0) {
-      const Closest c = closest_lane<DIM>(sc.prim, sc.pgroup, sc.n_prims, sc.n_pgroups, x);
+      const Closest c = closest_lane<DIM>(sc.prim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, sub, kSetupLanes);
       nDist = c.d;
       nSigned = signed_dist<DIM>(sc.paux, c, x);
     }
     float dDist, dSigned;
     if (sc.n_dprims > 0) {
-      const Closest c = closest_lane<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x);
+      const Closest c = closest_lane<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, sub, kSetupLanes);
       dDist = c.d;
       dSigned = signed_dist<DIM>(sc.dpaux, c, x);
     } else {
@@ -3119,9 +3137,12 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
     }
     int bucket;
     float firstR;
-    tk.pstate[i] = point_state<DIM>(sc, prm, nDist, nSigned, dDist, dSigned, &bucket, &firstR);
-    tk.prad[i] = firstR;
-    atomicAdd(&s_hist[bucket], 1u);
+    const int32_t ps = point_state<DIM>(sc, prm, nDist, nSigned, dDist, dSigned, &bucket, &firstR);
+    if (sub == 0) {
+      tk.pstate[i] = ps;
+      tk.prad[i] = firstR;
+      atomicAdd(&s_hist[bucket], 1u);
+    }
   }
   __syncthreads();
   if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);

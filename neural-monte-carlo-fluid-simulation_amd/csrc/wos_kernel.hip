@@ -163,7 +163,7 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
 
 hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               const DevTasks& tk, hipStream_t s) {
-  const int grid = (int)((n + 255) / 256);
+  const int grid = (int)((n * kSetupLanes + 255) / 256);
   if (grid < 1) return hipSuccess;
   if (dim == 2) hipLaunchKernelGGL(wos_point_setup_kernel<2>, dim3(grid), dim3(256), 0, s, sc, prm, pts, n, tk);
   else hipLaunchKernelGGL(wos_point_setup_kernel<3>, dim3(grid), dim3(256), 0, s, sc, prm, pts, n, tk);

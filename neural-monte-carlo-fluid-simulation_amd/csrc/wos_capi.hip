@@ -574,7 +574,7 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
     HIP_TRY(hipMalloc((void**)&c.d_pstate,
-                      ((size_t)3 * points + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes) * sizeof(int32_t)));
+                      ((size_t)4 * points + (4 * wos::kCostBuckets + 3) * wos::kMaxPipes) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
@@ -608,9 +608,12 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, in
   tk.pstate = c.d_pstate + pipe * point_slice;
   tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap + pipe * point_slice);
   tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap + pipe * point_slice);
-  tk.hist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
-  tk.shist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
+  tk.pdone = (uint32_t*)tk.prad;  // the walk kernel's; prad is the first-ball kernel's
+  tk.rq = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + pipe * point_slice);
+  tk.hist = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
+  tk.shist = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
                          pipe * (2 * wos::kCostBuckets + 1));
+  tk.rqc = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes + pipe * 2);
   tk.T = T;
   tk.wpp = wpp;
   return tk;
@@ -880,6 +883,10 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0) ? 1 : 0;
     if (const char* e = std::getenv("WOS_NEUMANN_INERT")) dp.neumann_inert = dp.neumann_inert && e[0] != '0';
   }
+  // in-kernel fold (WOS_TAIL_FOLD=1 with kernels built -DWOS_TAIL_FOLD=1; measured slower)
+  dp.tail_fold = 0;
+  if (const char* e = std::getenv("WOS_TAIL_FOLD")) dp.tail_fold = e[0] == '1';
+  if (phases != 1) dp.tail_fold = 0;
   if (const char* e = std::getenv("WOS_FB_ORDER")) dp.fb_order = std::max(0, std::min(2, std::atoi(e)));
   if (fb_sort) {
     geom_floats_fb = 0;
@@ -941,6 +948,16 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
                                     q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, fb_sort, ps));
     if (phases == 1 && !fb_sort) HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
+    if (dp.tail_fold) {
+      // pdone aliases prad: cleared once the first-ball kernel is done with it
+      HIP_TRY(hipMemsetAsync(tk.pdone, 0, (size_t)nb * sizeof(uint32_t), ps));
+      HIP_TRY(hipMemsetAsync(tk.rq, 0xFF, (size_t)nb * sizeof(uint32_t), ps));
+      HIP_TRY(hipMemsetAsync(tk.rqc, 0, 2 * sizeof(uint32_t), ps));
+      tk.p_out = d_p + b0;
+      tk.g_out = d_g + b0 * dim;
+      tk.nest_out = d_nest ? d_nest + b0 : nullptr;
+      tk.steps_out = d_steps ? d_steps + b0 : nullptr;
+    }
     HIP_TRY(hipEventRecord(ev[1], ps));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
     if (phases == 2)
@@ -950,6 +967,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
       HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
                                 shmem_walk, geom_floats_walk, ps));
     HIP_TRY(hipEventRecord(ev[2], ps));
+    // with the in-kernel fold: only the points it left (their walks outlasted its wait)
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
                              d_steps ? d_steps + b0 : nullptr, ps));
     HIP_TRY(hipEventRecord(ev[3], ps));

@@ -3491,6 +3491,89 @@ __device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams&
   atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);
 }
 
+// A task of point pidx has finished (its record is stored): count it; the walk that
+// completes the point queues it for the in-kernel fold.  Release on the count orders
+// this walk's record stores before it; the completing walk's acquire-release sees every
+// other walk's, and its release store of the queue entry passes them to the folder.
+// (The count itself is relaxed behind a release fence -- this wave's stores complete --
+// and only the completing walk takes the acquire: an acquire per walk would invalidate
+// the CU's L1 under every walker.)
+__device__ __forceinline__ void task_done(const DevTasks& tk, uint32_t pidx) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const uint32_t old = __hip_atomic_fetch_add(&tk.pdone[pidx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1u == (uint32_t)tk.wpp) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t slot = atomicAdd(&tk.rqc[0], 1u);
+    __hip_atomic_store(&tk.rq[slot], pidx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// wos_fold_kernel's statistics for one point by one lane, records read straight from
+// memory kFoldBatch at a time (the same operations in the same order: bit-identical)
+constexpr int kFoldBatch = 8;
+template <int DIM>
+__device__ void fold_point(const DevParams& prm, const DevTasks& tk, uint32_t i) {
+  const int64_t T = tk.T;
+  const int wpp = tk.wpp;
+  const int ps = tk.pstate[i];
+  const bool estimate = ps & kPtEstimate;
+  float mean[DIM + 1];
+  for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
+  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
+  int sN = 0;
+  uint32_t steps = 0;
+  if (estimate) {
+    for (int c0 = 0; c0 < wpp; c0 += kFoldBatch) {
+      uint32_t vc[kFoldBatch];
+      float vt[kFoldBatch], vf[kFoldBatch], vb[kFoldBatch][DIM], vs[kFoldBatch][DIM];
+#pragma unroll
+      for (int j = 0; j < kFoldBatch; j++) {
+        const int64_t t = (int64_t)i * wpp + c0 + j;
+        if (c0 + j < wpp) {
+          vc[j] = tk.code[t];
+          vt[j] = tk.total[t];
+          vf[j] = tk.first[t];
+          for (int k = 0; k < DIM; k++) { vb[j][k] = tk.bdir[k * T + t]; vs[j][k] = tk.sdir[k * T + t]; }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kFoldBatch; j++) {
+        const int r = c0 + j;
+        if (r >= wpp) break;
+        if (r % prm.n_anti == 0) {
+          cvb = mean[0];
+          cvs = sFirst / (float)(sN > 1 ? sN : 1);
+          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
+        }
+        const uint32_t code = vc[j];
+        steps += code >> 1;
+        if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
+        const float total = vt[j];
+        const float first = vf[j];
+        sN += 1;
+        const float fN = (float)sN;
+        {
+          const float delta = total - mean[0];
+          mean[0] += delta / fN;
+        }
+        for (int k = 0; k < DIM; k++) {
+          const float be = (total - first - cvb) * vb[j][k];
+          const float se = (first - cvs) * vs[j][k];
+          const float delta = (be + se) - mean[k + 1];
+          mean[k + 1] += delta / fN;
+        }
+        sFirst += first;
+      }
+    }
+  }
+  const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
+  tk.p_out[i] = maskP ? 0.0f : mean[0];
+  for (int k = 0; k < DIM; k++) tk.g_out[(int64_t)i * DIM + k] = maskG ? 0.0f : mean[k + 1];
+  if (tk.nest_out) tk.nest_out[i] = sN;
+  if (tk.steps_out) tk.steps_out[i] = (int32_t)steps;
+  tk.pdone[i] = (uint32_t)wpp + 1u;  // folded: the fold kernel that follows skips the point
+}
+
 __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters, const unsigned int* s_ctr) {
   if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
     unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
@@ -3515,6 +3598,21 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 // 1: refill the ring right after the hand-out instead of at the end of the iteration
 // (the staged tasks' loads get a whole step to land): within noise on karman / C / D,
 // with the staged records as well (WOS_TASK_RING) slower (profiles/r2e_ab_refill.log)
+// 1: compile the in-kernel fold into the walk kernel (used when DevParams::tail_fold).
+// It is best effort: a folding wave waits at most kTailFoldSpins sleeps for a claimed
+// point's last walk, and wos_fold_kernel (always launched after the walk kernel) folds
+// every point not marked folded -- so a slow tail costs time, never results.
+// Off: bit-identical (tests/test_gpu_switches.py) but the per-walk completion count
+// needs a device-scope release, i.e. an L2 write-back on MI355X's per-XCD L2s, for
+// every walk: karman walk kernel 2.4 -> 6.0 ms, cube 3.2 -> 16 ms
+// (profiles/r2t_ab_tail_fold*.log), whatever the folders' wait.
+#ifndef WOS_TAIL_FOLD
+#define WOS_TAIL_FOLD 0
+#endif
+#ifndef WOS_TAIL_SPINS
+#define WOS_TAIL_SPINS (1u << 16)
+#endif
+constexpr uint32_t kTailFoldSpins = WOS_TAIL_SPINS;
 #ifndef WOS_EARLY_REFILL
 #define WOS_EARLY_REFILL 0
 #endif
@@ -3543,6 +3641,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const DevParams& prm = prm_arg;
   const DevTasks& tk = tk_arg;
   const int lane = threadIdx.x & (kWave - 1);
+  // the in-kernel fold (DevParams::tail_fold) belongs to the first-ball walks
+  constexpr bool TAILF = WOS_TAIL_FOLD && !BSTART && !RESUME;
   const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
   // per-wave scratch shared by the star and ray queries (used one after the other)
@@ -3672,6 +3772,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
           t = (int64_t)v_t;
           if (!v_ok) {  // point outside the domain: no walks
             tk.code[t] = 0u;
+            if (TAILF && prm.tail_fold) task_done(tk, divw(v_t));
             t = -1;
           } else {
             if constexpr (RESUME) {
@@ -3718,6 +3819,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
                                                          rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
+      if (TAILF && prm.tail_fold) task_done(tk, divw((uint32_t)t));
       t = -1;
     }
     if (!WOS_EARLY_REFILL) refill(tk);
@@ -3731,6 +3833,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #endif
   }
 
+  // ---- in-kernel fold: this wave has nothing left to walk; it folds finished points
+  // (64 queue slots per claim, a lane per point) while the last walks run elsewhere.
+  // Every slot below the point count is eventually written (each point's last walk
+  // queues it), so the waits end; they sleep instead of spinning hot.
+  if (TAILF && prm_arg.tail_fold) {
+    const uint32_t npts = (uint32_t)(tk_arg.T / tk_arg.wpp);
+    for (;;) {
+      uint32_t h = 0;
+      if (lane == 0) h = atomicAdd(&tk_arg.rqc[1], (uint32_t)kWave);
+      h = (uint32_t)__shfl((int)h, 0);
+      if (h >= npts) break;
+      const uint32_t slot = h + (uint32_t)lane;
+      if (slot < npts) {
+        uint32_t p;
+        uint32_t spins = 0;  // bounded: a point whose walks outlast the wait is left to the fold kernel
+        // relaxed polling (an acquire per poll would invalidate the CU's L1 under the
+        // walkers' feet), then one acquire fence before the records are read
+        while ((p = __hip_atomic_load(&tk_arg.rq[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0xFFFFFFFFu &&
+               ++spins < kTailFoldSpins)
+          __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (p != 0xFFFFFFFFu) fold_point<DIM>(prm_arg, tk_arg, p);
+      }
+    }
+  }
   DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
   flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();
@@ -3900,8 +4027,11 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   const int64_t i = p0 + tid;
   const int64_t T = tk.T;
   const int wpp = tk.wpp;
+  // points already folded by the walk kernel's idle waves (DevParams::tail_fold)
+  const bool folded = prm.tail_fold && tid < nb && tk.pdone[i] == (uint32_t)wpp + 1u;
+  if (__syncthreads_and(folded || tid >= nb)) return;
   const int ps = tid < nb ? tk.pstate[i] : 0;
-  const bool estimate = ps & kPtEstimate;
+  const bool estimate = (ps & kPtEstimate) && !folded;
   float mean[DIM + 1];
   for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
   float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
@@ -3968,7 +4098,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
     }
     __syncthreads();
   }
-  if (tid >= nb) return;
+  if (tid >= nb || folded) return;
   const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
   p_out[i] = maskP ? 0.0f : mean[0];
   for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];

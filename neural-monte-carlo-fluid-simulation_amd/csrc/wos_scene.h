@@ -111,6 +111,7 @@ struct DevParams {
   int32_t robust;           // wos_solver_params.robust_float (Gfn::scaled)
   int32_t fb_order;         // presorted first balls: 0 point order, 1 walk-queue order, 2 reversed
   int32_t neumann_inert;    // 1: no ball can reach the float-overflow regime (walk kernel without the Neumann term)
+  int32_t tail_fold;        // 1: walk-kernel waves with nothing left to walk fold finished points (no fold kernel)
   uint64_t seed;
   // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
   // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the
@@ -170,6 +171,17 @@ struct DevTasks {
   uint32_t* rwl;     // [T] walkLength | onNeumann << 31
   uint32_t* rsteps;  // [T] ball steps so far
   uint32_t* surv;    // [T] survivor task indices
+  // In-kernel fold (DevParams::tail_fold): walks finished per point (pdone, [n], aliases
+  // prad, which only the first-ball kernel reads), the queue of points whose walks have
+  // all finished (rq, [n], 0xFFFFFFFF until written), its cursors rqc = [tail, head],
+  // and the fold's outputs (wos_fold_kernel's arguments).
+  uint32_t* pdone;
+  uint32_t* rq;
+  uint32_t* rqc;
+  float* p_out;
+  float* g_out;
+  int32_t* nest_out;
+  int32_t* steps_out;
   uint32_t* shist;   // [2 * kCostBuckets + 1]
 };
 

@@ -7,7 +7,9 @@ per-point walk counts and step counts bit for bit:
                    the setup inside the first-ball kernel;
 * WOS_FB_ORDER     the presorted first-ball queue order (point / walk-queue / reversed);
 * WOS_NEUMANN_INERT the walk kernel without the Neumann term's code for scenes that
-                   cannot reach the float-overflow regime vs the full kernel.
+                   cannot reach the float-overflow regime vs the full kernel;
+* WOS_TAIL_FOLD    the statistics folded inside the walk kernel by its idle waves vs
+                   the separate fold kernel.
 Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance),
 the Dirichlet obstacle (stored distance) and the cube (3D)."""
 import os
@@ -27,6 +29,7 @@ SETTINGS = [
     {"WOS_FB_ORDER": "2"},
     {"WOS_NEUMANN_INERT": "0"},
     {"WOS_FB_SORT": "0", "WOS_NEUMANN_INERT": "0"},
+    {"WOS_TAIL_FOLD": "0"},
 ]
 
 

@@ -3100,6 +3100,10 @@ __device__ __forceinline__ int32_t point_state(const DevScene& sc, const DevPara
 #define WOS_SETUP_LANES 1
 #endif
 constexpr int kSetupLanes = WOS_SETUP_LANES;  // lanes per point of wos_point_setup_kernel (power of two)
+#ifndef WOS_SETUP_LDS_FLOATS
+#define WOS_SETUP_LDS_FLOATS 4096
+#endif
+constexpr int kSetupLdsFloats = WOS_SETUP_LDS_FLOATS;  // 16 KB: 1024 segments / 455 triangles
 static_assert((kSetupLanes & (kSetupLanes - 1)) == 0 && kSetupLanes <= kWave, "kSetupLanes");
 // Point setup for the presorted first balls: one point per kSetupLanes lanes (the exact scans of
 // closest_lane), pstate + first-ball radius per point and the bucket histogram.  The
@@ -3111,8 +3115,20 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
                                                              const float* __restrict__ pts, int64_t n,
                                                              const DevTasks tk) {
   __shared__ uint32_t s_hist[kCostBuckets];
+  // small boundaries staged in LDS: every lane scans every record (broadcast reads)
+  // instead of one global round trip per primitive
+  __shared__ __attribute__((aligned(16))) float s_prim[kSetupLdsFloats];
+  constexpr int PS = Layout<DIM>::prim;
+  const int nfl = sc.n_prims * PS, dfl = sc.n_dprims * PS;
+  const bool lds_n = nfl <= kSetupLdsFloats, lds_d = nfl + dfl <= kSetupLdsFloats;
+  if (lds_n)
+    for (int k = threadIdx.x; k < nfl; k += blockDim.x) s_prim[k] = sc.prim[k];
+  if (lds_d)
+    for (int k = threadIdx.x; k < dfl; k += blockDim.x) s_prim[nfl + k] = sc.dprim[k];
   if (threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
   __syncthreads();
+  const float* nprim = lds_n ? s_prim : sc.prim;
+  const float* dprim = lds_d ? s_prim + nfl : sc.dprim;
   // kSetupLanes adjacent lanes per point share the small-mesh scans (closest_lane);
   // the first of them writes the point's state
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3123,13 +3139,13 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
     for (int k = 0; k < DIM; k++) x[k] = pts[i * DIM + k];
     float nDist = kFltMax, nSigned = kFltMax;
     if (sc.n_prims > 0) {
-      const Closest c = closest_lane<DIM>(sc.prim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, sub, kSetupLanes);
+      const Closest c = closest_lane<DIM>(nprim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, sub, kSetupLanes);
       nDist = c.d;
       nSigned = signed_dist<DIM>(sc.paux, c, x);
     }
     float dDist, dSigned;
     if (sc.n_dprims > 0) {
-      const Closest c = closest_lane<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, sub, kSetupLanes);
+      const Closest c = closest_lane<DIM>(dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, sub, kSetupLanes);
       dDist = c.d;
       dSigned = signed_dist<DIM>(sc.dpaux, c, x);
     } else {

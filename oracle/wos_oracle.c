@@ -21,9 +21,13 @@
  *   scene / PDE   bindings/zombie/demo/scene.h:54-200, image.h:42-58,
  *                 bindings/zombie3d/demo/scene_3d.h:22-128
  *
- * fcpw's wide BVH is replaced by fcpw's own brute-force "Baseline" semantics
- * (aggregates/baseline.inl); queries are order-independent except for exact
- * ties (resolved "last wins", as the reference's `<=` scans do).
+ * For the deterministic queries fcpw's wide BVH is replaced by fcpw's own
+ * brute-force "Baseline" semantics (aggregates/baseline.inl); they are
+ * order-independent except for exact ties (resolved "last wins", as the
+ * reference's `<=` scans do).  The stochastic Neumann sample, whose result
+ * depends on the tree, walks fcpw's tree itself, restated here
+ * (geom_build_fcpw_bvh: sbvh.inl:3-235 + mbvh.inl:46-133; fcpw_stochastic_pick:
+ * mbvh.inl:835-982,1099-1283).
  *
  * Deliberate, documented deviations from the reference:
  *  - RNG seeds: the reference seeds every point and every antithetic pair from

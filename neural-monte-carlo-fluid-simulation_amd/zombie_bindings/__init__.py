@@ -26,6 +26,8 @@ import numpy as np
 
 from wos_amd import engine as _engine
 
+from . import _image
+
 __all__ = ["Scene", "wost", "bvc"]
 
 
@@ -36,20 +38,8 @@ def _required(d, key):
 
 
 def _read_pfm(path):
-    with open(path, "rb") as f:
-        header = f.readline().decode().strip()
-        if header not in ("Pf", "PF"):
-            raise ValueError(f"{path}: not a PFM file")
-        w, h = map(int, f.readline().decode().split())
-        scale = float(f.readline().decode().strip())
-        ch = 1 if header == "Pf" else 3
-        data = np.frombuffer(f.read(), dtype="<f4" if scale < 0 else ">f4").astype(np.float32)
-    img = data.reshape(h, w, ch)[::-1]  # PFM rows are bottom-to-top
-    if ch == 3:  # Image<1>::setFromRGB grayscale (image.h:72-76)
-        img = 0.299 * img[..., 0] + 0.587 * img[..., 1] + 0.114 * img[..., 2]
-    else:
-        img = img[..., 0]
-    return np.ascontiguousarray(img, dtype=np.float32)
+    """readPFM (image.h:105-149): file row order, double-precision grayscale."""
+    return _image.read_pfm(path)
 
 
 class Scene:
@@ -59,8 +49,9 @@ class Scene:
         config = dict(config)
         boundary = _required(config, "boundary")
         if source is None:
-            # Scene(const json&) reads the source image named by "sourceValue" (scene.h:22-52)
-            src = _read_pfm(_required(config, "sourceValue"))
+            # Scene(const json&) reads the source image named by "sourceValue" (scene.h:22-52):
+            # Image<1>(file) -- PFM or PNG, rows in the file's order (image.h:84-171)
+            src = _image.read_image(_required(config, "sourceValue"))
             watertight_default, flip_default = True, True
         else:
             src = source

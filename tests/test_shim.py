@@ -59,13 +59,63 @@ def test_solution_image_writers(tmp_path):
     np.testing.assert_array_equal(px[..., 0], np.clip((img * 255).astype(int), 0, 255))
 
 
-def test_pfm_reader_roundtrip(tmp_path):
+def test_pfm_reader_file_row_order(tmp_path):
+    """readPFM keeps the file's row order (image.h:136-147): row 0 of the grid the
+    engine gets is the first row stored in the file -- no bottom-to-top flip."""
     img = np.arange(12, dtype=np.float32).reshape(3, 4)
     path = tmp_path / "x.pfm"
     with open(path, "wb") as f:
         f.write(b"Pf\n4 3\n-1.0\n")
-        f.write(img[::-1].astype("<f4").tobytes())
+        f.write(img.astype("<f4").tobytes())
     np.testing.assert_array_equal(zombie_bindings._read_pfm(str(path)), img)
+
+
+def _scene_dict_pair(tmp_path, fmt):
+    """Scene(dict) on a source image file and Scene(dict, mat) on the grid the reference
+    decodes from it, with the same explicit scene flags (the two ctors' defaults differ,
+    scene.h:23,33 vs :55,62)."""
+    from test_image_reader import quadrant_image
+    img = quadrant_image(80, 200)
+    if fmt == "pfm":
+        path = tmp_path / "src.pfm"
+        with open(path, "wb") as f:
+            f.write(b"Pf\n200 80\n-1\n" + img.astype("<f4").tobytes())
+    else:
+        PIL = pytest.importorskip("PIL.Image")
+        path = tmp_path / "src.png"
+        PIL.fromarray(((img + 2.0) * 50.0).astype(np.uint8), "L").save(path)
+    from zombie_bindings import _image
+    grid = _image.read_image(str(path))
+    scene_cfg = dict(workloads.SCENE_BASE, boundary=workloads.KARMAN_OBJ, sourceValue=str(path))
+    return zombie_bindings.Scene(scene_cfg), zombie_bindings.Scene(scene_cfg, grid.tolist()), grid
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["pfm", "png"])
+def test_scene_dict_image_equals_matrix_scene(gpu, tmp_path, fmt):
+    """A Scene(dict) solve (source read from a PFM / PNG file) equals the Scene(dict, mat)
+    solve on the same decoded grid bit for bit, and the pressure follows the FILE's
+    quadrants: with lambda = 350 the screened solution is ~ f / lambda away from the
+    quadrant edges, so p * 350 has the sign of the file's quadrant value."""
+    s_img, s_mat, grid = _scene_dict_pair(tmp_path, fmt)
+    _, solver, output = _configs()
+    bb = s_img.bbox
+    lo, hi = np.array(bb["bbox_min"], np.float32), np.array(bb["bbox_max"], np.float32)
+    ext = hi - lo
+    # one point per quadrant, away from the midlines, the walls and the cylinder (x ~ 0)
+    fr = np.array([[0.62, 0.2], [0.92, 0.2], [0.62, 0.8], [0.92, 0.8]], np.float32)
+    pts = (lo + fr * ext).astype(np.float32)
+    _, p1, g1 = zombie_bindings.wost(s_img, solver, output, pts, return_numpy=True)
+    _, p2, g2 = zombie_bindings.wost(s_mat, solver, output, pts, return_numpy=True)
+    np.testing.assert_array_equal(p1, p2)
+    np.testing.assert_array_equal(g1, g2)
+    h, w = grid.shape
+    for k in range(4):
+        i = min(int(np.float32(fr[k, 1]) * h), h - 1)
+        j = min(int(np.float32(fr[k, 0]) * w), w - 1)
+        f = grid[i, j]
+        assert f != 0
+        assert abs(p1[k] * 350.0 - f) < 0.25 * abs(f), (k, p1[k] * 350.0, f)
 
 
 @pytest.mark.gpu

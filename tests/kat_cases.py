@@ -158,3 +158,85 @@ def z_with_bias_floor(runs_p, runs_g, case, rel_floor=5e-4):
     the reference and robust modes are bit-identical, tests/test_oracle.py)."""
     c = dict(case, bias=max(case["bias"], rel_floor * float(np.sqrt(np.mean(case["p"] ** 2)))))
     return per_point_z(runs_p, runs_g, c)
+
+
+def _l_points(rng, npts, margin, near_corner):
+    """Uniform points of the L-shape [0,2]x[0,1] U [0,1]x[1,2] at least `margin` from its
+    walls, plus `near_corner` points within 0.3 of the reflex vertex (1, 1)."""
+    pts = []
+    while len(pts) < npts:
+        q = rng.uniform(margin, 2 - margin, 2)
+        if q[0] <= 1 - margin or q[1] <= 1 - margin:
+            pts.append(q)
+    k = 0
+    while k < near_corner:
+        q = 1.0 + rng.uniform(-0.3, 0.3, 2)
+        if (q[0] <= 1 - margin or q[1] <= 1 - margin) and np.all(q >= margin) and np.hypot(*(q - 1)) > margin:
+            pts.append(q)
+            k += 1
+    return np.asarray(pts)
+
+
+def lshape2d(lam=50.0, m=1, n=1, n_walks=128, npts=1200, near_corner=300, res=800, seed=7):
+    """Non-convex Neumann KAT: the L-shape [0,2]x[0,1] U [0,1]x[1,2]
+    (three unit squares, counter-clockwise so normals (s.y,-s.x) point out), zero-flux
+    walls, f = cos(m pi x) cos(n pi y).  Every wall lies on an integer line, where f's
+    normal derivative vanishes, so p = f / (lambda + pi^2 (m^2 + n^2)) exactly on the
+    L.  The reflex vertex (1, 1) is the scene's one silhouette candidate (its dihedral
+    angle is not below 1e-3, scene.h:84-90), so the star radius of every point that
+    sees both of its segments from opposite sides is set by it
+    (computeStarRadius, fcpw_scene_loader.h:621-641) -- the path no convex KAT reaches."""
+    v = np.array([[0, 0], [2, 0], [2, 1], [1, 1], [1, 2], [0, 2]], np.float32)
+    ix = np.array([[0, 1], [1, 2], [2, 3], [3, 4], [4, 5], [5, 0]], np.int32)
+    pmin, pmax = v.min(0) - EPS32, v.max(0) + EPS32
+    ys = (np.arange(res) + 0.5) / res * (pmax[1] - pmin[1]) + pmin[1]
+    xs = (np.arange(res) + 0.5) / res * (pmax[0] - pmin[0]) + pmin[0]
+    X, Y = np.meshgrid(xs, ys)   # rows ~ y
+    km, kn = m * np.pi, n * np.pi
+    f = (np.cos(km * X) * np.cos(kn * Y)).astype(np.float32)
+    pts = _l_points(np.random.default_rng(seed), npts, 0.03, near_corner).astype(np.float32)
+    k2 = km ** 2 + kn ** 2
+    x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+    pe = np.cos(km * x) * np.cos(kn * y) / (lam + k2)
+    gx = -km * np.sin(km * x) * np.cos(kn * y) / (lam + k2)
+    gy = -kn * np.cos(km * x) * np.sin(kn * y) / (lam + k2)
+    h = (pmax - pmin).max() / res
+    return {"name": f"lshape2d_l{lam:g}_m{m}n{n}", "dim": 2, "vertices": v, "prims": ix, "source": f,
+            "absorption": lam, "solver": _solver(n_walks), "output": {"boundaryDistanceMask": 1e-3},
+            "points": pts, "p": pe, "grad": np.stack([gx, gy], -1), "bias": h * h / 8 * k2 / lam, "kw": {}}
+
+
+def lprism3d(lam=50.0, m=1, n=1, l=1, n_walks=128, npts=600, near_corner=150, res=96, seed=9):
+    """3D analogue: the L-shape extruded over z in [0, 1] (12 vertices, 20 triangles wound
+    like scenes/cube.obj: (b-a)x(c-a) points out), f = cos(m pi x) cos(n pi y) cos(l pi z),
+    p = f / (lambda + pi^2 (m^2 + n^2 + l^2)).  The reflex edge x = y = 1 is the one
+    silhouette edge candidate (edge_silhouettes.inl:83-111, sbvh.inl:405-421); the
+    triangulation's flat diagonals are ignored (dihedral angle 0)."""
+    poly = np.array([[0, 0], [2, 0], [2, 1], [1, 1], [1, 2], [0, 2]], np.float64)
+    v = np.concatenate([np.c_[poly, np.zeros(6)], np.c_[poly, np.ones(6)]]).astype(np.float32)
+    tris = []
+    for a in range(6):  # side walls: quad (a, b, b+6, a+6), outward for a CCW polygon
+        b = (a + 1) % 6
+        tris += [(a, b, b + 6), (a, b + 6, a + 6)]
+    fan = [(0, 1, 2), (0, 2, 3), (0, 3, 4), (0, 4, 5)]   # star-shaped from vertex 0
+    tris += [(a, c, b) for a, b, c in fan]                # bottom (z = 0): facing -z
+    tris += [(a + 6, b + 6, c + 6) for a, b, c in fan]    # top (z = 1): facing +z
+    ix = np.array(tris, np.int32)
+    pmin, pmax = v.min(0) - EPS32, v.max(0) + EPS32
+    axes = [(np.arange(res) + 0.5) / res * (pmax[k] - pmin[k]) + pmin[k] for k in range(3)]
+    X, Y, Z = np.meshgrid(*axes, indexing="ij")
+    kx, ky, kz = m * np.pi, n * np.pi, l * np.pi
+    f = (np.cos(kx * X) * np.cos(ky * Y) * np.cos(kz * Z)).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    xy = _l_points(rng, npts, 0.04, near_corner)
+    pts = np.c_[xy, rng.uniform(0.04, 0.96, len(xy))].astype(np.float32)
+    x, y, z = (pts[:, k].astype(np.float64) for k in range(3))
+    k2 = kx ** 2 + ky ** 2 + kz ** 2
+    cx, cy, cz = np.cos(kx * x), np.cos(ky * y), np.cos(kz * z)
+    sx, sy, sz = np.sin(kx * x), np.sin(ky * y), np.sin(kz * z)
+    pe = cx * cy * cz / (lam + k2)
+    ge = np.stack([-kx * sx * cy * cz, -ky * cx * sy * cz, -kz * cx * cy * sz], -1) / (lam + k2)
+    h = (pmax - pmin).max() / res
+    return {"name": f"lprism3d_l{lam:g}_m{m}{n}{l}", "dim": 3, "vertices": v, "prims": ix, "source": f,
+            "absorption": lam, "solver": _solver(n_walks), "output": {"boundaryDistanceMask": 1e-3},
+            "points": pts, "p": pe, "grad": ge, "bias": h * h / 8 * k2 / lam, "kw": {}}

@@ -27,6 +27,12 @@ CASES = {
     "cube3d_l350_m111": lambda: kat_cases.cube3d(350.0, 1, 1, 1),
     "cube3d_l50_m111": lambda: kat_cases.cube3d(50.0, 1, 1, 1),
     "cube3d_l350_m210": lambda: kat_cases.cube3d(350.0, 2, 1, 0),
+    # non-convex: the reflex vertex / edge is a silhouette candidate (star-radius path)
+    "lshape2d_l50_m1n1": lambda: kat_cases.lshape2d(50.0, 1, 1),
+    "lshape2d_l10_m2n1": lambda: kat_cases.lshape2d(10.0, 2, 1),
+    "lshape2d_l350_m1n2": lambda: kat_cases.lshape2d(350.0, 1, 2),
+    "lprism3d_l50_m111": lambda: kat_cases.lprism3d(50.0, 1, 1, 1),
+    "lprism3d_l350_m210": lambda: kat_cases.lprism3d(350.0, 2, 1, 0),
 }
 
 
@@ -37,10 +43,12 @@ def test_gpu_kat(gpu, name):
     P, G = [], []
     for k in range(16):
         p, g, st = sc.solve(c["points"], solver_params(c["solver"], c["output"], seed=0x4B410000 + k))
-        assert st["points_estimated"] == c["points"].shape[0] and st["walks_escaped"] == 0
+        assert st["points_estimated"] == c["points"].shape[0]
+        # convex cases: no escapes; the L's reflex vertex leaks a rare walk (test_oracle.py)
+        assert st["walks_escaped"] <= (1e-4 * st["walks_recorded"] if "shape" in name or "prism" in name else 0)
         P.append(p)
         G.append(g)
     sc.close()
-    kat_cases.check_unbiased(P[0], G[0], c, 0.1 if c["absorption"] > 100 else 0.3)
+    kat_cases.check_unbiased(P[0], G[0], c, 0.1 if c["absorption"] > 100 else (0.3 if c["absorption"] >= 50 else 0.6))
     zp, zg = kat_cases.per_point_z(P, G, c)
     kat_cases.check_z(zp, zg)

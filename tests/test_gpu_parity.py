@@ -224,6 +224,21 @@ def test_double_sided_bit_exact(gpu, oracle, dim):
     _compare(oracle, osc, sc, cfg, pts)
 
 
+@pytest.mark.parametrize("which", ["lshape2d", "lprism3d"])
+def test_nonconvex_l_bit_exact(gpu, oracle, which):
+    """The non-convex KAT scenes (kat_cases.lshape2d / lprism3d): the reflex vertex /
+    edge is the star radius's only silhouette candidate, including the walks that leak
+    through it and escape (dropped, walk_on_stars.h:280-286)."""
+    import kat_cases
+    c = kat_cases.lshape2d(10.0, 2, 1) if which == "lshape2d" else kat_cases.lprism3d(50.0, 1, 1, 1)
+    cfg = {"solver": c["solver"], "output": c["output"]}
+    osc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], watertight=True)
+    sc = WosScene(c["vertices"], c["prims"], c["source"], c["absorption"], watertight=True)
+    for seed in (0x5EED0001, 0x4C000003):
+        _compare(oracle, osc, sc, cfg, c["points"], seed=seed)
+    sc.close()
+
+
 def test_cube3d_bit_exact(gpu, oracle):
     cfg = workloads.cube_config(res=10, n_walks=64)
     osc, sc = _pair(cfg, oracle, dim=3)

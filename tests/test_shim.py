@@ -83,7 +83,7 @@ def _scene_dict_pair(tmp_path, fmt):
     else:
         PIL = pytest.importorskip("PIL.Image")
         path = tmp_path / "src.png"
-        PIL.fromarray(((img + 2.0) * 50.0).astype(np.uint8), "L").save(path)
+        PIL.fromarray(((img + 2.5) * 50.0).astype(np.uint8), "L").save(path)  # 175 225 75 25
     from zombie_bindings import _image
     grid = _image.read_image(str(path))
     scene_cfg = dict(workloads.SCENE_BASE, boundary=workloads.KARMAN_OBJ, sourceValue=str(path))

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 6
+#define WOS_ABI_VERSION 7
 
 enum {
     WOS_OK = 0,
@@ -125,7 +125,14 @@ typedef struct wos_solver_params {
                                                (distributions.h:585-587,695); 1: balls with mu R > 80 use
                                                exponentially scaled Bessels and ratios (finite, correct) --
                                                identical to mode 0 on every ball with mu R <= 80 */
+    uint32_t schedule;                      /* WOS_SCHED_* bits: how the solve is scheduled on the GPU,
+                                               never what it computes (results are bit-identical) */
 } wos_solver_params;
+
+/* wos_solver_params.schedule (no reference analogue; 0 = the engine's choice) */
+#define WOS_SCHED_GEOM_GLOBAL   0x1u  /* read the geometry records through L2 even when they fit LDS */
+#define WOS_SCHED_FULL_NEUMANN  0x2u  /* keep the walk kernel's Neumann term even when it is provably +0 */
+#define WOS_SCHED_NO_STAR_GRID  0x4u  /* no star-radius cell grid: the cooperative group scan alone */
 
 void wos_default_params(wos_solver_params *p);
 

@@ -91,9 +91,7 @@ struct DevCtx {
   hipEvent_t done = nullptr;   // end of the last enqueued solve
   hipStream_t last_stream = nullptr;
   bool inflight = false;       // a solve may still run on last_stream
-  hipStream_t aux[wos::kMaxPipes] = {};  // pipelines 1.. (pipeline 0 is the caller's stream)
   float* d_rejtab = nullptr;   // rejection bound table, 2D then 3D (DevParams::rej_tab)
-  hipEvent_t fork = nullptr, join[wos::kMaxPipes] = {};
   int stat_waiters = 0;        // wos_solve_stats calls waiting on a slot's event without the lock
   std::condition_variable no_waiters;
 };
@@ -114,14 +112,6 @@ void ctx_free(DevCtx& c) {
     q = StatSlot{};
   }
   if (c.done) hipEventDestroy(c.done);
-  for (int i = 0; i < wos::kMaxPipes; i++) {
-    if (c.aux[i]) hipStreamDestroy(c.aux[i]);
-    if (c.join[i]) hipEventDestroy(c.join[i]);
-    c.aux[i] = nullptr;
-    c.join[i] = nullptr;
-  }
-  if (c.fork) hipEventDestroy(c.fork);
-  c.fork = nullptr;
   c.d_pts = c.d_p = c.d_g = nullptr;
   c.d_nest = c.d_steps = nullptr;
   c.ws_points = 0;
@@ -138,14 +128,11 @@ void ctx_free(DevCtx& c) {
 // the rejection bound tables (host, computed once per process)
 const std::vector<float>& rejection_tables() {
   static std::once_flag once;
-  // [2D bound | 3D bound | 2D envelope | 3D envelope] (DevParams::rej_tab, rej_env)
-  constexpr size_t kEnv = (size_t)wos::kRejTabBins * wos::kRejEnvX * 2;
-  static std::vector<float> t(2 * wos::kRejTabBins + 2 * kEnv);
+  // [2D bound | 3D bound] (DevParams::rej_tab)
+  static std::vector<float> t(2 * wos::kRejTabBins);
   std::call_once(once, [] {
     wos::rejection_bound_table(2, t.data());
     wos::rejection_bound_table(3, t.data() + wos::kRejTabBins);
-    wos::rejection_envelope_table(2, t.data() + 2 * wos::kRejTabBins);
-    wos::rejection_envelope_table(3, t.data() + 2 * wos::kRejTabBins + kEnv);
   });
   return t;
 }
@@ -167,11 +154,6 @@ int ctx_ready(DevCtx& c, int device) {
     HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
   }
   HIP_TRY(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-  for (int i = 1; i < wos::kMaxPipes; i++) {
-    HIP_TRY(hipStreamCreateWithFlags(&c.aux[i], hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&c.join[i], hipEventDisableTiming));
-  }
   c.ready = true;
   return WOS_OK;
 }
@@ -280,22 +262,12 @@ int geom_get(const wos_scene_desc* d, int device, std::shared_ptr<Geom>& out) {
   return WOS_OK;
 }
 
-// LDS budget of the star-radius grid (staged by every walk-kernel workgroup);
-// WOS_STAR_GRID_BUDGET (bytes) overrides it for A/B runs
-size_t star_grid_budget() {
-  const char* e = std::getenv("WOS_STAR_GRID_BUDGET");
-  if (e && *e) return (size_t)std::strtoul(e, nullptr, 10);
-  return 16 * 1024;
-}
+// LDS budget of the star-radius grid (staged by every walk-kernel workgroup)
+constexpr size_t kStarGridBudget = 16 * 1024;
 
 // dynamic LDS a workgroup may use: 160 KB per CU minus the kernels' static LDS
 // (rejection jump table 2 KB, counters, histogram)
 constexpr size_t kLdsDynamicMax = 160 * 1024 - 4096;
-
-bool star_grid_enabled() {
-  const char* e = std::getenv("WOS_STAR_GRID");  // "0": always the cooperative group scan (A/B runs, tests)
-  return !(e && e[0] == '0');
-}
 
 // the star grid of `g` for the solver's silhouette precision and minR (built once)
 int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
@@ -303,7 +275,7 @@ int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
   for (const Geom::Grid& x : g.grids)
     if (x.prec == prec && x.min_r == min_r) { *out = &x; return WOS_OK; }
   Geom::Grid x{prec, min_r, false, {}, nullptr};
-  x.ok = wos::build_star_grid(g.host, prec, min_r, star_grid_budget(), x.grid);
+  x.ok = wos::build_star_grid(g.host, prec, min_r, kStarGridBudget, x.grid);
   if (x.ok) {
     HIP_TRY(hipMalloc((void**)&x.d, x.grid.words.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(x.d, x.grid.words.data(), x.grid.words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -563,7 +535,7 @@ constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
 
 int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
   // sized for 3D records so either dimension fits
-  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3)) + 1;  // + rrng alignment
+  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
   if (tasks > c.task_cap) {
     hipFree(c.d_tasks);
     c.d_tasks = nullptr; c.task_cap = 0;
@@ -573,20 +545,16 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
   if (points > c.pstate_cap) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c.d_pstate,
-                      ((size_t)4 * points + (4 * wos::kCostBuckets + 3) * wos::kMaxPipes) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)3 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
 }
 
-// SoA views into the task workspace for a chunk of T tasks: pipeline `pipe` owns
-// tasks [pipe * task_slice, ...) and points [pipe * point_slice, ...) of the workspace
-wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, int64_t task_slice,
-                        int64_t point_slice) {
+// SoA views into the task workspace for a chunk of T tasks
+wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   wos::DevTasks tk{};
-  const int tf = std::max(wos::task_floats(dim), wos::task_floats(3)) + 1;
-  float* f = c.d_tasks + (size_t)pipe * task_slice * tf;
+  float* f = c.d_tasks;
   tk.pt = f; f += dim * T;
   tk.thr = f; f += T;
   tk.tsrc = f; f += T;
@@ -595,25 +563,11 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp, int pipe, in
   tk.bdir = f; f += dim * T;
   tk.sdir = f; f += dim * T;
   tk.total = f; f += T;
-  tk.code = (uint32_t*)f; f += T;
-  if (((uintptr_t)f & 7u) != 0) f += 1;  // (T even in practice; keep rrng 8-B aligned regardless)
-  tk.rrng = (uint64_t*)f; f += 2 * T;
-  tk.rn = f; f += dim * T;
-  tk.rpd = f; f += dim * T;
-  tk.rpdist = f; f += T;
-  tk.rtn = f; f += T;
-  tk.rwl = (uint32_t*)f; f += T;
-  tk.rsteps = (uint32_t*)f; f += T;
-  tk.surv = (uint32_t*)f;
-  tk.pstate = c.d_pstate + pipe * point_slice;
-  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap + pipe * point_slice);
-  tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap + pipe * point_slice);
-  tk.pdone = (uint32_t*)tk.prad;  // the walk kernel's; prad is the first-ball kernel's
-  tk.rq = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap + pipe * point_slice);
-  tk.hist = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + pipe * 2 * wos::kCostBuckets);
-  tk.shist = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + 2 * wos::kCostBuckets * wos::kMaxPipes +
-                         pipe * (2 * wos::kCostBuckets + 1));
-  tk.rqc = (uint32_t*)(c.d_pstate + 4 * c.pstate_cap + (4 * wos::kCostBuckets + 1) * wos::kMaxPipes + pipe * 2);
+  tk.code = (uint32_t*)f;
+  tk.pstate = c.d_pstate;
+  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap);
+  tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap);
+  tk.hist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap);
   tk.T = T;
   tk.wpp = wpp;
   return tk;
@@ -696,7 +650,7 @@ int walk_layout(wos_scene* s, const wos_solver_params* prm, WalkLayout& L) {
   dsc = s->dev;
   dsc.sgrid = nullptr;
   dsc.sgrid_words = dsc.sgrid_off_words = 0;
-  if (star_grid_enabled() && host.n_sil > 0) {
+  if (!(prm->schedule & WOS_SCHED_NO_STAR_GRID) && host.n_sil > 0) {
     const Geom::Grid* gr = nullptr;
     int rc = star_grid(geom, prm->silhouette_precision, prm->min_star_radius, &gr);
     if (rc != WOS_OK) return rc;
@@ -800,10 +754,7 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     if (rc != WOS_OK) return rc;
     dp.jump = c.d_jump;
     dp.n_jump = c.n_jump;
-    const char* rt = std::getenv("WOS_REJ_TABLE");  // "0": the scene-independent bound only (A/B)
-    dp.rej_tab = (rt && rt[0] == '0') ? nullptr : c.d_rejtab;
-    const char* re = std::getenv("WOS_REJ_ENV");  // "0": no two-sided envelope (A/B)
-    dp.rej_env = (re && re[0] == '0') ? nullptr : c.d_rejtab + 2 * wos::kRejTabBins;
+    dp.rej_tab = c.d_rejtab;
   }
 
   // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
@@ -818,25 +769,21 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   int geom_floats_walk = wl.geom_floats_walk;
   size_t shmem_walk = wl.shmem_walk;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
-  const size_t shmem_fb =
-      (size_t)geom_floats * sizeof(float) + wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
-  // scenes beyond the LDS budget (or WOS_GEOM_GLOBAL=1): geometry read from global
+  // the first-ball kernel stages no geometry (the point-setup kernel did the queries)
+  const size_t shmem_fb = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
+  // scenes beyond the LDS budget (or WOS_SCHED_GEOM_GLOBAL): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
-  int geom_floats_fb = geom_floats;
-  size_t shmem_fb_launch = shmem_fb;
-  const char* gg = std::getenv("WOS_GEOM_GLOBAL");
-  if ((gg && gg[0] == '1') || std::max(shmem_fb, shmem_walk) > kLdsDynamicMax) {
+  if ((prm->schedule & WOS_SCHED_GEOM_GLOBAL) ||
+      std::max((size_t)geom_floats * sizeof(float) + shmem_fb, shmem_walk) > kLdsDynamicMax) {
     dfb.geom_global = 1;
     dsc.geom_global = 1;
-    geom_floats_fb = 0;
     geom_floats_walk = 0;
-    shmem_fb_launch = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
     shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
-    if (std::max(shmem_fb_launch, shmem_walk) > kLdsDynamicMax)
-      return fail(WOS_E_CAPACITY, "wos_solve: nWalks exceed the LDS budget of the first-ball kernel (" +
-                                      std::to_string(shmem_fb_launch) + " bytes)");
   }
+  if (std::max(shmem_fb, shmem_walk) > kLdsDynamicMax)
+    return fail(WOS_E_CAPACITY, "wos_solve: nWalks exceed the LDS budget of the first-ball kernel (" +
+                                    std::to_string(shmem_fb) + " bytes)");
 
   // the shared workspace may still be in use by a solve enqueued on another stream
   HIP_TRY(ctx_order(c, st));
@@ -857,52 +804,27 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   }
   HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
 
-  // Points are solved in chunks whose walk tasks fit the task workspace.  With
-  // WOS_SPLIT = S > 1 the chunks are dealt round-robin to S pipelines (the caller's
-  // stream + S-1 internal streams, each with its own workspace slice and queues), so
-  // one chunk's first balls run in the long-walk tail of another chunk's walk kernel.
+  // Points are solved in chunks whose walk tasks fit the task workspace.
   const int64_t wpp = (int64_t)dp.n_pairs * dp.n_anti;
-  int pipes = 1;
-  if (const char* e = std::getenv("WOS_SPLIT")) pipes = std::max(1, std::min(wos::kMaxPipes, std::atoi(e)));
-  // 2: two-phase walks (first step of every task, then the survivors); 1: one persistent pass
-  int phases = 1;
-  if (const char* e = std::getenv("WOS_PHASES")) phases = std::atoi(e) == 2 ? 2 : 1;
-  // presorted first balls (point-setup kernel + queue order first, then the first balls
-  // in descending radius order); WOS_FB_SORT=0: setup inside the first-ball kernel (A/B)
-  bool fb_sort = true;
-  if (const char* e = std::getenv("WOS_FB_SORT")) fb_sort = e[0] != '0';
-  dp.fb_order = 0;
   // The Neumann term (h == 0) is +0 at every step unless a ball's float members overflow
   // (mu R > 85 is the kernels' gate).  In a watertight single-sided scene every estimated
   // point and walk lies inside the boundary's bounding box, so R < its diagonal: below
-  // the gate the walk kernel runs without the term's code (bit-identical results).
+  // the gate the walk kernel runs without the term's code (bit-identical results;
+  // WOS_SCHED_FULL_NEUMANN keeps the full kernel).
   {
     double diag2 = 0.0;
     for (int k = 0; k < 3; k++) diag2 += (double)host.ext[k] * host.ext[k];
     const double mu_r = std::sqrt(std::max(0.0, (double)s->dev.absorption)) * std::sqrt(diag2) * 1.01;
-    dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0) ? 1 : 0;
-    if (const char* e = std::getenv("WOS_NEUMANN_INERT")) dp.neumann_inert = dp.neumann_inert && e[0] != '0';
+    dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0 &&
+                        !(prm->schedule & WOS_SCHED_FULL_NEUMANN)) ? 1 : 0;
   }
-  // in-kernel fold (WOS_TAIL_FOLD=1 with kernels built -DWOS_TAIL_FOLD=1; measured slower)
-  dp.tail_fold = 0;
-  if (const char* e = std::getenv("WOS_TAIL_FOLD")) dp.tail_fold = e[0] == '1';
-  if (phases != 1) dp.tail_fold = 0;
-  if (const char* e = std::getenv("WOS_FB_ORDER")) dp.fb_order = std::max(0, std::min(2, std::atoi(e)));
-  if (fb_sort) {
-    geom_floats_fb = 0;
-    shmem_fb_launch = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
-  }
-  const int64_t slice_tasks = kMaxBatchTasks / pipes;
-  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, slice_tasks / wpp));
-  if (pipes > 1 && n > 0) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, (n + pipes - 1) / pipes));
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
   const int64_t n_chunks = n > 0 ? (n + chunk - 1) / chunk : 0;
-  if (n_chunks < pipes) pipes = (int)std::max<int64_t>(1, n_chunks);
   int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;
   if (n > 0) {
-    int rc = ensure_tasks(c, dim, (int64_t)pipes * chunk * wpp, (int64_t)pipes * chunk);
+    int rc = ensure_tasks(c, dim, chunk * wpp, chunk);
     if (rc != WOS_OK) return rc;
-    HIP_TRY(wos::occupancy_blocks_per_cu(fb_sort ? 2 : 0, dim, dfb.geom_global != 0, shmem_fb_launch, &bpc_fb,
-                                         dp.robust != 0));
+    HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, false, shmem_fb, &bpc_fb, dp.robust != 0));
     grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
     HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk, dp.robust != 0));
@@ -923,58 +845,30 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
   HIP_TRY(hipEventRecord(q.ev0, st));
-  if (pipes > 1) {
-    HIP_TRY(hipEventRecord(c.fork, st));
-    for (int i = 1; i < pipes; i++) HIP_TRY(hipStreamWaitEvent(c.aux[i], c.fork, 0));
-  }
   for (int64_t k = 0; k < n_chunks; k++) {
-    const int pipe = (int)(k % pipes);
-    hipStream_t ps = pipe == 0 ? st : c.aux[pipe];
     const int64_t b0 = k * chunk;
     hipEvent_t* ev = &q.bev[4 * k];
     const int64_t nb = std::min(chunk, n - b0);
-    wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp, pipe, chunk * wpp, chunk);
+    wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp);
     const int64_t bbase = index_base + b0 * index_stride;
-    unsigned long long* qslot = c.d_counters + wos::kNumCounters + 2 * pipe;
+    unsigned long long* qslot = c.d_counters + wos::kNumCounters;
     unsigned int* q_points = (unsigned int*)qslot;
     unsigned int* q_tasks = (unsigned int*)(qslot + 1);
-    if (k >= pipes) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), ps));
-    HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), ps));
-    HIP_TRY(hipEventRecord(ev[0], ps));
-    if (fb_sort) {
-      HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, ps));
-      HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
-    }
+    if (k > 0) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), st));
+    HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, st));
+    HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
-                                    q_points, grid_fb, shmem_fb_launch, geom_floats_fb, lhs_floats, fb_sort, ps));
-    if (phases == 1 && !fb_sort) HIP_TRY(wos::launch_lpt_order(tk, nb, ps));
-    if (dp.tail_fold) {
-      // pdone aliases prad: cleared once the first-ball kernel is done with it
-      HIP_TRY(hipMemsetAsync(tk.pdone, 0, (size_t)nb * sizeof(uint32_t), ps));
-      HIP_TRY(hipMemsetAsync(tk.rq, 0xFF, (size_t)nb * sizeof(uint32_t), ps));
-      HIP_TRY(hipMemsetAsync(tk.rqc, 0, 2 * sizeof(uint32_t), ps));
-      tk.p_out = d_p + b0;
-      tk.g_out = d_g + b0 * dim;
-      tk.nest_out = d_nest ? d_nest + b0 : nullptr;
-      tk.steps_out = d_steps ? d_steps + b0 : nullptr;
-    }
-    HIP_TRY(hipEventRecord(ev[1], ps));
+                                    q_points, grid_fb, shmem_fb, lhs_floats, st));
+    HIP_TRY(hipEventRecord(ev[1], st));
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
-    if (phases == 2)
-      HIP_TRY(wos::launch_walks_two_phase(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
-                                          shmem_walk, geom_floats_walk, ps));
-    else
-      HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
-                                shmem_walk, geom_floats_walk, ps));
-    HIP_TRY(hipEventRecord(ev[2], ps));
-    // with the in-kernel fold: only the points it left (their walks outlasted its wait)
+    HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
+                              shmem_walk, geom_floats_walk, st));
+    HIP_TRY(hipEventRecord(ev[2], st));
     HIP_TRY(wos::launch_fold(dim, dp, tk, nb, d_p + b0, d_g + b0 * dim, d_nest ? d_nest + b0 : nullptr,
-                             d_steps ? d_steps + b0 : nullptr, ps));
-    HIP_TRY(hipEventRecord(ev[3], ps));
-  }
-  for (int i = 1; i < pipes; i++) {
-    HIP_TRY(hipEventRecord(c.join[i], c.aux[i]));
-    HIP_TRY(hipStreamWaitEvent(st, c.join[i], 0));
+                             d_steps ? d_steps + b0 : nullptr, st));
+    HIP_TRY(hipEventRecord(ev[3], st));
   }
   HIP_TRY(hipEventRecord(q.ev1, st));
   HIP_TRY(hipMemcpyAsync(q.h_cnt, c.d_counters, wos::kNumCounters * sizeof(unsigned long long),
@@ -1125,6 +1019,8 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   }
   q.ticket = ticket;
   q.n_batches = 1;
+  q.bpc_fb = 0;
+  q.bpc_walk = 0;
   HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(q.ev0, st));
   HIP_TRY(hipEventRecord(q.bev[0], st));
@@ -1132,6 +1028,29 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_bpt, nb, d_bdd, nullptr, nullptr, nullptr, st));
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_dc, nd, nullptr, nullptr, d_din, d_dsrc, st));
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_ept, ne, d_edd, d_end, d_ein, nullptr, st));
+  // the cache size is known once the domain candidates' inside test is: a samples buffer
+  // too small for it fails here, before the walks, with counts[] filled for a retry
+  int64_t nd_keep = nd;
+  if (!geom.double_sided && nd > 0) {
+    std::vector<int32_t> din0(nd);
+    HIP_TRY(hipMemcpyAsync(din0.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    nd_keep = 0;
+    for (int64_t i = 0; i < nd; i++) nd_keep += din0[i] != 0;
+  } else if (geom.double_sided) {
+    nd_keep = 0;
+    for (int64_t i = 0; i < nd; i++) {
+      const float x = smp.dcand[2 * i], y = smp.dcand[2 * i + 1];
+      nd_keep += (x >= pmin[0] && y >= pmin[1] && x <= pmax[0] && y <= pmax[1]);
+    }
+  }
+  if (samples && samples_capacity < nb + nd_keep) {
+    if (counts) { counts[0] = smp.nb_main; counts[1] = smp.nb_aligned; counts[2] = nd_keep; counts[3] = nb + nd_keep; }
+    HIP_TRY(hipStreamSynchronize(st));
+    c.inflight = false;
+    return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
+                                    std::to_string(nb + nd_keep) + " samples (counts[3])");
+  }
 
   // ---- estimates at the boundary samples: estimateSolution walks (walk_on_stars.h:353-464)
   wos_solver_params wp = *prm;
@@ -1144,7 +1063,6 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     dp.jump = c.d_jump;
     dp.n_jump = c.n_jump;
     dp.rej_tab = c.d_rejtab;
-    dp.rej_env = c.d_rejtab + 2 * wos::kRejTabBins;
   }
   WalkLayout wl;
   {
@@ -1152,8 +1070,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     if (rc != WOS_OK) return rc;
   }
   wos::DevScene dsc = wl.dsc;
-  const char* gg = std::getenv("WOS_GEOM_GLOBAL");
-  if ((gg && gg[0] == '1') || wl.shmem_walk > kLdsDynamicMax) {
+  if ((prm->schedule & WOS_SCHED_GEOM_GLOBAL) || wl.shmem_walk > kLdsDynamicMax) {
     dsc.geom_global = 1;
     wl.geom_floats_walk = 0;
     wl.shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(2);
@@ -1163,7 +1080,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (nb > 0) {
     int rc = ensure_tasks(c, 2, nb * wpp, nb);
     if (rc != WOS_OK) return rc;
-    wos::DevTasks tk = task_view(c, 2, nb * wpp, (int32_t)wpp, 0, nb * wpp, nb);
+    wos::DevTasks tk = task_view(c, 2, nb * wpp, (int32_t)wpp);
     tk.n0 = tk.bdir;
     tk.r0 = tk.first;
     tk.sflags = reinterpret_cast<uint32_t*>(tk.sdir);
@@ -1236,12 +1153,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     if (rc != WOS_OK) return rc;
     stats->points_estimated = (uint64_t)nb;
   }
-  if (samples) {
-    if (samples_capacity < nrec)
-      return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
-                                      std::to_string(nrec) + " samples");
-    if (nrec > 0) std::memcpy(samples, recs.data(), recs.size() * sizeof(float));
-  }
+  if (samples && nrec > 0) std::memcpy(samples, recs.data(), recs.size() * sizeof(float));
   return WOS_OK;
 }
 

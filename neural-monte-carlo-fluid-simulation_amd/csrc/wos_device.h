@@ -27,43 +27,8 @@
 
 namespace wos {
 
-// 1: the star-grid candidate lists of all lanes are evaluated wave-cooperatively;
-// 0: each lane scans its own cell list sequentially
-#ifndef WOS_CELL_COOP
-#define WOS_CELL_COOP 1
-#endif
-#ifndef WOS_ABL_NO_SIL
-#define WOS_ABL_NO_SIL 0
-#endif
-#ifndef WOS_ABL_NO_RAY
-#define WOS_ABL_NO_RAY 0
-#endif
-#ifndef WOS_ABL_ONE_REJ
-#define WOS_ABL_ONE_REJ 0
-#endif
-#ifndef WOS_NO_FASTREJ
-#define WOS_NO_FASTREJ 0
-#endif
-// timing-only ablations (wrong results): float Bessels in the ball update and the
-// direction-sampled Poisson kernel; a constant source texel
-#ifndef WOS_ABL_FAST_BESSEL
-#define WOS_ABL_FAST_BESSEL 0
-#endif
-#ifndef WOS_ABL_CONST_SRC
-#define WOS_ABL_CONST_SRC 0
-#endif
-#ifndef WOS_ABL_FB
-#define WOS_ABL_FB 0
-#endif
-#ifndef WOS_ABL_NO_STATS
-#define WOS_ABL_NO_STATS 0
-#endif
-
 #ifndef WOS_DIAG
 #define WOS_DIAG 0
-#endif
-#ifndef WOS_RAY_WAVE
-#define WOS_RAY_WAVE 1
 #endif
 
 constexpr int kWave = 64;
@@ -242,90 +207,12 @@ __device__ __forceinline__ float box_dist2(const float* B, const float* x) {
 
 struct Closest { float d; float p[3]; float t0, t1; int prim; };
 
-// Wave-cooperative closest point over `np` primitives (key fl(d*d), last index
-// wins ties, mbvh.inl:1297-1351); the result is uniform across the wave.
-template <int DIM>
-__device__ Closest closest_wave(const float* prims, int np, const float* x, int lane) {
-  constexpr int PS = Layout<DIM>::prim;
-  float bk = kFltMax; int bi = -1;
-  for (int p = lane; p < np; p += kWave) {
-    float pt[DIM], t0, t1;
-    float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-    float d2 = d * d;
-    if (d2 <= bk) { bk = d2; bi = p; }
-  }
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    float ok = __shfl_xor(bk, off);
-    int oi = __shfl_xor(bi, off);
-    if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
-  }
-  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
-  c.p[0] = c.p[1] = c.p[2] = 0.0f;
-  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
-  return c;
-}
-
-// The same query for scenes with many groups (global-memory geometry): the group of
-// the smallest box bound is evaluated first for a running minimum, then every group
-// whose bound does not exceed it (lanes take groups by stride) -- the brute-force
-// result (min fl(d*d), last index on ties).
-template <int DIM>
-__device__ Closest closest_wave_grouped(const float* prims, const float* groups, int np, int ng, const float* x,
-                                        int lane) {
-  constexpr int PS = Layout<DIM>::prim;
-  float lbm = kFltMax;
-  int gm = 0x7FFFFFFF;
-  for (int g = lane; g < ng; g += kWave) {
-    const float lb = box_dist2<DIM>(groups + g * kGroupStride, x);
-    if (lb < lbm) { lbm = lb; gm = g; }
-  }
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    const float ol = __shfl_xor(lbm, off);
-    const int og = __shfl_xor(gm, off);
-    if (ol < lbm || (ol == lbm && og < gm)) { lbm = ol; gm = og; }
-  }
-  float bk = kFltMax;
-  int bi = -1;
-  if (lane < kGroup && gm != 0x7FFFFFFF) {
-    const int p = gm * kGroup + lane;
-    if (p < np) {
-      float pt[DIM], t0, t1;
-      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-      bk = d * d;
-      bi = p;
-    }
-  }
-  float sr2 = bk;
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    const float o = __shfl_xor(sr2, off);
-    sr2 = o < sr2 ? o : sr2;
-  }
-  for (int g = lane; g < ng; g += kWave) {
-    if (box_dist2<DIM>(groups + g * kGroupStride, x) > sr2) continue;
-    const int p1 = (g + 1) * kGroup < np ? (g + 1) * kGroup : np;
-    for (int p = g * kGroup; p < p1; p++) {
-      float pt[DIM], t0, t1;
-      const float d = cp_prim<DIM>(prims + p * PS, x, pt, &t0, &t1);
-      const float d2 = d * d;
-      if (d2 < bk || (d2 == bk && p > bi)) { bk = d2; bi = p; }
-    }
-  }
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    float ok = __shfl_xor(bk, off);
-    int oi = __shfl_xor(bi, off);
-    if (ok < bk || (ok == bk && oi > bi)) { bk = ok; bi = oi; }
-  }
-  Closest c; c.prim = bi; c.d = kFltMax; c.t0 = c.t1 = 0.0f;
-  c.p[0] = c.p[1] = c.p[2] = 0.0f;
-  if (bi >= 0) c.d = cp_prim<DIM>(prims + bi * PS, x, c.p, &c.t0, &c.t1);
-  return c;
-}
-
-// The same query by ONE lane (the point-setup kernel: one point per lane).  The
+// Closest point by ONE lane (the point-setup kernel: one point per lane), key fl(d*d),
+// last index among equal keys (the reference's `<=` scan, baseline.inl:60-260).  The
 // group of the smallest box bound is evaluated first for a running minimum when
 // there are many groups, then every group whose bound does not exceed it; the
 // update rule (smaller fl(d*d), or equal and a larger index) makes the result the
-// brute-force one whatever the visiting order, as in closest_wave.
+// brute-force one whatever the visiting order.
 template <int DIM>
 __device__ Closest closest_lane(const float* prims, const float* groups, int np, int ng, const float* x,
                                 int sub = 0, int nsub = 1) {
@@ -897,7 +784,6 @@ __device__ __forceinline__ void offset_point(const float* p, const float* n, flo
 template <int DIM>
 __device__ __forceinline__ float source_value(const DevScene& sc, const float* x) {
   if (sc.source == nullptr) return 0.0f;
-  if (WOS_ABL_CONST_SRC) return 0.5f;
   if constexpr (DIM == 2) {
     float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
     float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
@@ -1044,16 +930,12 @@ struct Gfn {
       return;
     }
     if constexpr (DIM == 2) {
-#if WOS_ABL_FAST_BESSEL
-      A0 = k0_fast(muR); A1 = i0_fast(muR); B0 = k1_fast(muR); B1 = i1_fast(muR);
-#else
       double i0, k0, i1, k1;
       bessel_ik<true, true>((double)muR, &i0, &k0, &i1, &k1);
       A0 = (float)k0;
       A1 = (float)i0;
       B0 = (float)k1;
       B1 = (float)i1;
-#endif
     } else {
       float expmuR = fexp(-muR);
       float exp2muR = expmuR * expmuR;
@@ -1170,9 +1052,6 @@ struct Gfn {
     float mur = rr * sqrtLambda;
     if (scaled()) return scaled_dir_poisson_kernel<DIM>(mur, muR, A0, A1);
     if constexpr (DIM == 2) {
-#if WOS_ABL_FAST_BESSEL
-      float K1mur = k1_fast(mur), I1mur = i1_fast(mur);
-#else
       float K1mur, I1mur;
       if (WOS_PK_REUSE && rr == R) {
         // |y - c| rounds to R (about half the sphere points): mu r is mu R, whose K1 and I1
@@ -1185,7 +1064,6 @@ struct Gfn {
         K1mur = (float)k1;
         I1mur = (float)i1;
       }
-#endif
       float Q = K1mur + I1mur * A0 / A1;
       return mur * Q;
     } else {
@@ -1389,34 +1267,6 @@ __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, 
   return (q > 0.0f && q < 3.0e38f) ? q : 3.0e38f;
 }
 
-// Offset of a ball's row of the two-sided rejection envelope (DevParams::rej_env,
-// wos_host_scene.h rejection_envelope_table), or -1 when there is none: no table, the
-// s -> 0 bin, mu R beyond the table, or a non-positive / non-finite R / (norm bound).
-// (default off: the per-item table gather measured slower than the arithmetic it saves,
-// karman walk +4.5 %, cube +21 %: the load latency sits inside every generation)
-#ifndef WOS_REJ_ENV
-#define WOS_REJ_ENV 0
-#endif
-template <int DIM>
-__device__ __forceinline__ int rej_env_row(const DevParams& prm, float muR, float cR) {
-  if (!WOS_REJ_ENV || prm.rej_env == nullptr || !(muR >= 0.0f) || !(cR > 0.0f && cR < 3.0e38f)) return -1;
-  const int k = (int)(kRejTabScale * __builtin_sqrtf(muR));
-  if (k < 1 || k >= kRejTabBins) return -1;
-  return ((DIM == 3 ? kRejTabBins : 0) + k) * kRejEnvX * 2;
-}
-
-// Envelope decision of one iteration: 1 accept (u < lo R / (norm bound)), 0 reject
-// (u > hi R / (norm bound)), -1 the exact test (or its certified fast path) decides.
-__device__ __forceinline__ int rej_env_decide(const DevParams& prm, int row, float cR, float u, float x) {
-  if (row < 0) return -1;
-  const int j = (int)(x * (float)kRejEnvX);
-  const float* e = prm.rej_env + row + 2 * j;
-  const float hi = e[0], lo = e[1];
-  if (u > hi * cR) return 0;
-  if (u < lo * cR) return 1;
-  return -1;
-}
-
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM, bool RB>
@@ -1446,12 +1296,10 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
   // norm() depends only on the ball: hoisted out of the loop (same value every iteration)
   const float nrm = g.norm();
   // fast path: 2D Yukawa while I0 stays finite in float (float Bessels need mu*r < ~88)
-  const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f && !WOS_NO_FASTREJ;
+  const bool fast = DIM == 2 && g.yukawa && g.muR < 80.0f;
   const float rho = g.A0 / g.A1;
   const float invNB = 1.0f / (nrm * bound);
   const float quick = g.yukawa ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
-  const float cR = R * invNB;
-  const int env = (g.yukawa && (fast || DIM == 3)) ? rej_env_row<DIM>(prm, g.muR, cR) : -1;
   int iter = 0;
   do {
     float u = s.nextf();
@@ -1461,7 +1309,6 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
     int decided = -1;  // 1 accept, 0 reject, -1 undecided
     if (u > quick) {
       decided = 0;
-    } else if ((decided = rej_env_decide(prm, env, cR, u, xd)) >= 0) {
     } else if (fast) {
       const float mur = g.r * g.sqrtLambda;
       float k0, i0v;
@@ -1478,7 +1325,7 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
       float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
       decided = u < pdfRadius / bound ? 1 : 0;
     }
-    if (decided == 1 || WOS_ABL_ONE_REJ) break;
+    if (decided == 1) break;
   } while (iter < 1000);
   if (need_pdf) *pdf = g.evaluate() / nrm;  // pdf of the last sampled radius (before the clamps)
   *iters += (uint32_t)iter;
@@ -1518,26 +1365,6 @@ constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
 template <int DIM, bool FB>
 constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : (FB ? WOS_REJ_BMIN3_FB : WOS_REJ_BMIN3);
 static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 16, "RejLDS::surv holds 64 * 16 items");
-// 1: screen a generation's items with the certain-reject bound, then evaluate the
-// survivors compacted over the wave; 0 (default): every lane evaluates its own
-// items (the screen + compaction measured 15-20 % slower on karman / cube / C)
-#ifndef WOS_REJ_COMPACT
-#define WOS_REJ_COMPACT 0
-#endif
-// Self phase: while more than this many lanes of the wave are unfinished, a
-// generation would give each owner B = 1 item (2D) anyway, so every unfinished lane
-// evaluates its own next iteration from its own stream in registers -- no LDS
-// staging, no owner scan, no wave syncs; the cooperative generations start when at
-// most this many lanes remain.  64 disables the phase (the default: with the block
-// sizes above it measured no faster than the cooperative generations, within noise).
-#ifndef WOS_REJ_SELF2
-#define WOS_REJ_SELF2 64
-#endif
-#ifndef WOS_REJ_SELF3
-#define WOS_REJ_SELF3 64
-#endif
-template <int DIM>
-constexpr int kRejSelf = DIM == 2 ? WOS_REJ_SELF2 : WOS_REJ_SELF3;
 
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
@@ -1582,44 +1409,12 @@ __device__ __forceinline__ int rej_div(int item, int B, uint32_t mB) {
   return (int)(((uint32_t)item * mB) >> 16);
 }
 
-// x-dependent certain-reject bound of one iteration, after its radius draw x:
-//   2D  T(x) = x R Q(mu x R) invNB <= x R K0(mu x R) invNB < sqrt(pi x R / (2 mu)) e^{-mu x R} invNB
-//       (K_nu increasing in nu, K_{1/2}(z) = sqrt(pi / 2z) e^{-z}; the subtracted rho I0 >= 0)
-//   3D  T(x) = x R (e^{-mu r} - rho sinh(mu r)) invNB <= x R e^{-mu x R} invNB
-// with a 0.1 % + 1e-6 R invNB margin over the A&S / float rounding of the exact test,
-// evaluated while mu x R < 80 (no underflow).  u above it is the exact test's reject.
-// Default off: it resolves 80 % (2D) / 92 % (3D) of the items instead of 22 % / 26 %
-// (tools DIAG build), yet measured slower (karman walk +1.3 %, cube +5.6 %): a wave
-// pays for the fast path whenever any of its lanes needs it, and with compaction
-// (WOS_REJ_COMPACT) the extra LDS round trips cost more than the arithmetic saved.
-#ifndef WOS_REJ_XB
-#define WOS_REJ_XB 0
-#endif
-__device__ __forceinline__ bool rej_xbound_reject(int dim, float u, float x, float muR, float xb, float Rinv) {
-  if (!WOS_REJ_XB) return false;
-  const float z = x * muR;
-  if (!(z < 80.0f)) return false;
-  const float e = __builtin_amdgcn_exp2f(z * -1.44269502f);
-  const float shape = dim == 2 ? __builtin_amdgcn_sqrtf(x) : x;
-  return u > (xb * shape * e) * 1.001f + 1e-6f * Rinv;
-}
-
 struct RejLDS {
   unsigned long long s0[kWave];
   float R[kWave], sqrtL[kWave];
   float c0[kWave], c1[kWave];  // 2D: rho = A0/A1, 1/(norm*bound)   3D: A0, A1 (ball members)
   float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
   float qb[kWave];                 // certain-reject bound (rej_quick_bound)
-#if WOS_REJ_XB
-  float xb[kWave], xmu[kWave];     // x-dependent bound (rej_xbound_reject): its constant, mu R
-#endif
-#if WOS_REJ_ENV
-  float cR[kWave];                 // R / (norm bound): scale of the envelope (rej_env_decide)
-  int env[kWave];                  // the ball's envelope row (rej_env_row), -1: none
-#endif
-#if WOS_REJ_COMPACT
-  uint16_t surv[kWave * 16];       // items that passed the certain-reject screen (one generation)
-#endif
   float nrm[kWave], bound[kWave];
   uint32_t base[kWave], acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
@@ -1693,8 +1488,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
                                                    bool need_pdf, RejLDS* L, int lane) {
   bool coop = false;
   float bound = 0.0f, nrm = 1.0f;
-  if (active && g.yukawa && !WOS_ABL_ONE_REJ &&
-      (DIM == 3 ? !g.scaled() : (g.muR < 80.0f && !WOS_NO_FASTREJ))) {
+  if (active && g.yukawa && (DIM == 3 ? !g.scaled() : g.muR < 80.0f)) {
     const float R = g.R, lam = g.lambda, sl = g.sqrtLambda;
     const float a = DIM == 2 ? 2.2f : 2.0f, b = DIM == 2 ? 0.6f : 0.5f;
     bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
@@ -1708,52 +1502,12 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
     bool done = !coop;
     DIAG_COUNT(D_RCALLS, 1);
     DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
-    if (kRejSelf<DIM> < kWave) {
-      // self phase (see kRejSelf): iteration j0 of every unfinished lane, sequential draws
-      const float invNB = coop ? 1.0f / (nrm * bound) : 0.0f;
-      const float qb = coop ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 0.0f;
-      const float rho = coop ? g.A0 / g.A1 : 0.0f;
-      // s advances past the self draws; the end of the call resets it from s0
-      while (__popcll(__ballot(!done)) > kRejSelf<DIM>) {
-        DIAG_COUNT(D_RGENS, 1);
-        if (!done) {
-          const float u = s.nextf();
-          const float x = s.nextf();
-          int dcs = 0;
-          DIAG_LANE(D_RITEMS);
-          if (u > qb) {
-            DIAG_LANE(D_RQUICK);
-          } else {
-            const float rr = x * g.R;
-            if constexpr (DIM == 2) dcs = rej_fast_decide(u, rr, g.sqrtLambda, rho, invNB);
-            else dcs = rej_fast_decide3(u, rr, g.sqrtLambda, rho, invNB);
-            if (dcs < 0) {
-              DIAG_LANE(D_RUND);
-              g.r = rr;
-              const float p = g.evaluate() / nrm;
-              const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
-              dcs = u < pdfRadius / bound ? 1 : 0;
-            }
-          }
-          if (dcs == 1) { jacc = j0; done = true; }
-          else if (++j0 >= kRejMax) { jacc = kRejMax - 1; done = true; }  // limit: last radius kept
-        }
-      }
-    }
     if (!done) {
       L->s0[lane] = s0;
       L->R[lane] = g.R;
       L->sqrtL[lane] = g.sqrtLambda;
       const float invNB = 1.0f / (nrm * bound);
       L->qb[lane] = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB);
-#if WOS_REJ_XB
-      L->xb[lane] = DIM == 2 ? __builtin_sqrtf(1.57079637f * g.R / g.sqrtLambda) * invNB : g.R * invNB;
-      L->xmu[lane] = g.muR;
-#endif
-#if WOS_REJ_ENV
-      L->cR[lane] = g.R * invNB;
-      L->env[lane] = rej_env_row<DIM>(prm, g.muR, g.R * invNB);
-#endif
       if constexpr (DIM == 2) {
         L->c0[lane] = g.A0 / g.A1;
         L->c1[lane] = 1.0f / (nrm * bound);
@@ -1788,70 +1542,6 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         L->und[lane] = 0u;
       }
       wave_sync();
-#if WOS_REJ_COMPACT
-      // phase A: the certain-reject screens of every item (its draws and the x bound);
-      // phase B: the survivors, compacted, evaluated densely by the whole wave
-      uint32_t keep = 0;
-      for (int q = 0; q < per; q++) {
-        const int item = lane * per + q;
-        const int orank = rej_div(item, B, mB), b = item - orank * B;
-        if (orank < nact) {
-          const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
-          DIAG_LANE(D_RITEMS);
-          if (j < kRejMax) {
-            const uint64_t st = rej_state(prm, L->s0[owner], j);
-            const float u = draw_float(st);
-            bool rej = u > L->qb[owner];
-#if WOS_REJ_XB
-            if (!rej) {
-              const float x = draw_float(st * kPcgMult + kPcgInc);
-              rej = rej_xbound_reject(DIM, u, x, L->xmu[owner], L->xb[owner],
-                                      L->R[owner] * (DIM == 2 ? L->c1[owner] : L->inv3[owner]));
-            }
-#endif
-            if (!rej) keep |= 1u << q;
-            else DIAG_LANE(D_RQUICK);
-          }
-        }
-      }
-      {
-        // compaction by item slot: ballot + mbcnt ranks, no cross-lane scan
-        uint32_t total = 0;
-        for (int q = 0; q < per; q++) {
-          const bool k = (keep >> q) & 1u;
-          const uint64_t bal = __ballot(k);
-          if (k) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            L->surv[total + rank] = (uint16_t)(lane * per + q);
-          }
-          total += (uint32_t)__popcll(bal);
-        }
-        wave_sync();
-        for (uint32_t k = lane; k < total; k += kWave) {
-          const int item = (int)L->surv[k];
-          const int orank = rej_div(item, B, mB), b = item - orank * B;
-          const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
-          const uint64_t st = rej_state(prm, L->s0[owner], j);
-          const float u = draw_float(st);
-          const float x = draw_float(st * kPcgMult + kPcgInc);
-          int dcs;
-          if constexpr (DIM == 2) {
-            dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
-          } else {
-            const float rr = x * L->R[owner];
-            dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
-            if (dcs < 0)
-              dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner], L->nrm[owner],
-                                      L->bound[owner]);
-          }
-          if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
-          else if (dcs < 0) { atomicOr(&L->und[owner], 1u << b); DIAG_LANE(D_RUND); }
-        }
-      }
-#else
       for (int q = 0; q < per; q++) {
         const int item = lane * per + q;
         const int orank = rej_div(item, B, mB), b = item - orank * B;
@@ -1868,28 +1558,14 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
               DIAG_LANE(D_RQUICK);
             } else {
               const float x = draw_float(st * kPcgMult + kPcgInc);
-#if WOS_REJ_ENV
-              dcs = rej_env_decide(prm, L->env[owner], L->cR[owner], u, x);
-#else
-              dcs = -1;
-#endif
-#if WOS_REJ_XB
-              if (dcs < 0 && rej_xbound_reject(DIM, u, x, L->xmu[owner], L->xb[owner],
-                                               L->R[owner] * (DIM == 2 ? L->c1[owner] : L->inv3[owner]))) {
-                dcs = 0;
-                DIAG_LANE(D_RQUICK);
-              }
-#endif
-              if (dcs < 0) {
-                if constexpr (DIM == 2) {
-                  dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
-                } else {
-                  const float rr = x * L->R[owner];
-                  dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
-                  if (dcs < 0)
-                    dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner],
-                                            L->nrm[owner], L->bound[owner]);
-                }
+              if constexpr (DIM == 2) {
+                dcs = rej_fast_decide(u, x * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]);
+              } else {
+                const float rr = x * L->R[owner];
+                dcs = rej_fast_decide3(u, rr, L->sqrtL[owner], L->rho3[owner], L->inv3[owner]);
+                if (dcs < 0)
+                  dcs = rej_exact_decide3(u, rr, L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner],
+                                          L->nrm[owner], L->bound[owner]);
               }
             }
             if (dcs == 1) atomicOr(&L->acc[owner], 1u << b);
@@ -1897,7 +1573,6 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           }
         }
       }
-#endif
       wave_sync();
       if (!done) {
         const uint32_t acc = L->acc[lane], und = L->und[lane];
@@ -2120,7 +1795,7 @@ __device__ __forceinline__ int walk_step_begin(const DevScene& sc, const DevPara
       *flip = true;
     }
   }
-  *query = !(prm.steps_before_maximal_spheres <= st.walkLength || WOS_ABL_NO_SIL);
+  *query = !(prm.steps_before_maximal_spheres <= st.walkLength);
   return -1;
 }
 
@@ -2437,30 +2112,6 @@ __device__ __forceinline__ int star_cell(const DevScene& sc, const float* x) {
   return c;
 }
 
-// computeStarRadius for one lane from its cell's candidate list: the sequential
-// scan of star_radius (candidates in index order, r2 shrinking, minR break) over
-// the only candidates that can decide it (wos_host_scene.h StarGrid), hence the
-// full scan's result.
-template <int DIM>
-__device__ __forceinline__ float star_radius_cell(const LGeom& G, int cell, const float* x, float r2, float minR2,
-                                                  float minR, float dflt, bool flip, float prec) {
-  const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
-  const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
-  const int e1 = off[cell + 1];
-  bool found = false;
-  float best = 0.0f;
-  for (int e = off[cell]; e < e1; e++) {
-    float d2, d;
-    if (star_candidate<DIM>(G, (int)lst[e], x, r2, flip, prec, &d2, &d)) {
-      r2 = d2;
-      best = d;
-      found = true;
-      if (minR2 >= r2) break;
-    }
-  }
-  return found ? smax(best, minR) : dflt;
-}
-
 template <int DIM>
 __device__ __forceinline__ float star_candidate_dist(const LGeom& G, int s, const float* x) {
   constexpr int SS = Layout<DIM>::sil;
@@ -2502,15 +2153,10 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
   if (need && G.sgrid != nullptr) {
     const int cell = star_cell<DIM>(sc, x);
     if (cell >= 0) {
-      if (!WOS_CELL_COOP) {
-        result = star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
-        need = false;
-      } else {
-        const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
-        c_beg = off[cell];
-        c_end = off[cell + 1];
-        use_cell = true;
-      }
+      const uint16_t* off = reinterpret_cast<const uint16_t*>(G.sgrid);
+      c_beg = off[cell];
+      c_end = off[cell + 1];
+      use_cell = true;
     }
   }
   if (__ballot(need) == 0) return result;
@@ -2522,7 +2168,7 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     L->brk[lane] = 0xFFFFFFFFu;
     L->best[lane] = ~0ull;
   }
-  if (WOS_CELL_COOP && __ballot(use_cell) != 0) {
+  if (__ballot(use_cell) != 0) {
     // the (lane, candidate) pairs of all cell lists, spread over the wave in windows
     // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
     // the longest list; accepted candidates fold into the owner like the group scan
@@ -2725,40 +2371,6 @@ __device__ __forceinline__ void lhs_permute(float* strat, const int* partner, in
   wave_sync();
 }
 
-// The same shuffle simulated step by step in registers, for nstrat <= 128: lane L
-// holds positions L and L + 64; step j reads a[j] and a[partner[j]] with v_readlane
-// (j and partner[j] are wave-uniform) and the two owning lanes take each other's
-// value -- the sequential swaps themselves, so the result is exact by construction.
-// No LDS traffic and no wave syncs inside the loop, but 128 dependent readlane steps:
-// measured slower (karman first balls 0.62 -> 0.80 ms, cube 1.67 -> 2.31 ms,
-// profiles/r2l_ab_lhs.log), so off by default.
-#ifndef WOS_LHS_LANES
-#define WOS_LHS_LANES 0
-#endif
-__device__ __forceinline__ void lhs_permute_lanes(float* strat, const int* partner, int nstrat, int sd, int dimi,
-                                                  int lane) {
-  const int* pd = partner + dimi * nstrat;
-  float a0 = lane < nstrat ? strat[sd * lane + dimi] : 0.0f;
-  float a1 = lane + kWave < nstrat ? strat[sd * (lane + kWave) + dimi] : 0.0f;
-  const int p0 = lane < nstrat ? pd[lane] : 0;
-  const int p1 = lane + kWave < nstrat ? pd[lane + kWave] : 0;
-  for (int j = 0; j < nstrat; j++) {
-    const int jl = j & (kWave - 1);
-    const bool jhi = j >= kWave;  // wave-uniform
-    const int q = __builtin_amdgcn_readlane(jhi ? p1 : p0, jl);
-    const int ql = q & (kWave - 1);
-    const bool qhi = q >= kWave;
-    const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(jhi ? a1 : a0), jl));
-    const float vq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qhi ? a1 : a0), ql));
-    if (lane == jl) { if (jhi) a1 = vq; else a0 = vq; }
-    if (lane == ql) { if (qhi) a1 = vj; else a0 = vj; }
-  }
-  wave_sync();
-  if (lane < nstrat) strat[sd * lane + dimi] = a0;
-  if (lane + kWave < nstrat) strat[sd * (lane + kWave) + dimi] = a1;
-  wave_sync();
-}
-
 // per-wave first-ball scratch after the stratified samples and partners: the
 // rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute
 __host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
@@ -2803,10 +2415,6 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
     }
     wave_sync();
   }
-  if (WOS_LHS_LANES && nstrat <= 2 * kWave) {
-    for (int i = 0; i < sd; ++i) lhs_permute_lanes(strat, partner, nstrat, sd, i, lane);
-    return;
-  }
   if (nstrat <= 4 * kWave) {
     for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);
     return;
@@ -2829,11 +2437,6 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 // 2D keeps the per-lane loop: measured faster for first balls, r1d);
 // lanes with active == false run pair 0's arithmetic for nothing (helping the
 // cooperative sampler) and write and count nothing.
-// 1: the 2D first-ball source sample uses the wave-cooperative rejection sampler too
-// (the 3D one always does); 0: each lane runs its own loop
-#ifndef WOS_FB_COOP2
-#define WOS_FB_COOP2 0
-#endif
 template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
@@ -2853,12 +2456,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   // Bessel constants are evaluated once (identical values either way)
   Gfn<DIM, RB> g0;
   g0.init(yuk0, sc.absorption);
-#if WOS_ABL_FB == 1
-  { const int y = g0.yukawa; g0.yukawa = 0; g0.update_ball(x, firstR, false); g0.yukawa = y;
-    g0.muR = firstR * g0.sqrtLambda; g0.A0 = 0.5f; g0.A1 = 1.5f; g0.B0 = 0.3f; g0.B1 = 0.7f; }
-#else
   g0.update_ball(x, firstR, prm.robust != 0);
-#endif
   for (int a = 0; a < prm.n_anti; a++) {
     const int64_t t = t0 + a;
     Gfn<DIM, RB> g = g0;
@@ -2869,7 +2467,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       if (a == 0) {
         float dir[DIM];
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-        if constexpr (DIM == 3 || WOS_FB_COOP2)
+        if constexpr (DIM == 3)
           sample_volume_wave<DIM, RB, true>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
         else
           sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, true);
@@ -2884,11 +2482,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       totalSource += throughput * contrib;
       firstSource = contrib;
       float gr[DIM];
-#if WOS_ABL_FB == 2
-      for (int k = 0; k < DIM; k++) gr[k] = (g.yVol[k] - g.c[k]) * 0.5f;
-#else
       g.gradient(gr);
-#endif
       float den = sourcePdf * gnorm;
       for (int k = 0; k < DIM; k++) sdir[k] = gr[k] / den;
     }
@@ -2950,10 +2544,6 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
     }
     if (!active) continue;
-#if WOS_ABL_FB == 5
-    if (firstSource == 12345.0f) tk.first[t] = throughput + totalSource + bdir[0] + sdir[0];
-    continue;
-#endif
     tk.first[t] = firstSource;
     for (int k = 0; k < DIM; k++) {
       tk.bdir[k * T + t] = bdir[k];
@@ -3051,10 +2641,7 @@ __device__ __forceinline__ void flush_counter(unsigned long long* counters, int 
 enum { kPtEstimate = 1, kPtMaskP = 2, kPtMaskG = 4 };
 
 // ---- kernel 1: point setup + first balls ----------------------------------
-#ifndef WOS_PT_GRAB
-#define WOS_PT_GRAB 2
-#endif
-constexpr unsigned int kPtGrab = WOS_PT_GRAB;  // points per queue atomic of the first-ball kernel
+constexpr unsigned int kPtGrab = 2;  // points per queue atomic of the first-ball kernel
 // 3D: 3 waves/SIMD (168 VGPRs, 16-28 B/lane of spills) instead of the unconstrained 2:
 // first balls -20 % on the cube configs (profiles/r2u_ab_fb3d_occupancy.log)
 #ifndef WOS_FB_WAVES_PER_EU
@@ -3166,136 +2753,75 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
 
 // RB: robust float semantics (DevParams::robust; Gfn::scaled) -- separate instantiations
 // (wos_robust.hip), so the reference-semantics kernels carry none of its code.
-// PRE: presorted -- wos_point_setup_kernel + the walk-queue order ran first; queue
-// position q takes point perm[n_est - 1 - q] (largest first ball first) and reads its
-// radius instead of repeating the setup (no geometry staged: geom_floats = 0).
-template <int DIM, bool GG, bool RB = false, bool PRE = false>
+// wos_point_setup_kernel ran first: point i's state and first-ball radius are read
+// from pstate / prad (no geometry is staged: the first balls query none).
+template <int DIM, bool RB = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_FB_WAVES_PER_EU2 : WOS_FB_WAVES_PER_EU))) void wos_first_ball_kernel(
     const DevScene sc, const DevParams prm, const float* __restrict__ pts, int64_t n, int64_t base, int64_t stride,
-    const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int geom_floats,
-    int lhs_floats) {
+    const DevTasks tk, unsigned long long* __restrict__ counters, unsigned int* __restrict__ work, int lhs_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ uint32_t s_hist[kCostBuckets];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  LGeom Gfb{};
-  if constexpr (!PRE) Gfb = stage_geometry<DIM, GG>(sc, smem, false);
   stage_rej_jump(prm);
-  if (!PRE && threadIdx.x < kCostBuckets) s_hist[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
-  const float* Lprim = Gfb.prim;
-  float* strat = smem + geom_floats + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
+  float* strat = smem + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
   int* partner = (int*)(strat + lhs_floats);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);
 
   uint32_t c_iters = 0, c_pts = 0;
   const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
-  // PRE with a queue order (fb_order 1: walk-queue order, 2: reversed): the queue runs
-  // over the estimated points only (bucket 0 = not estimated, last in the walk order);
-  // fb_order 0: point order, the estimate bit read from pstate
-  const int order = PRE ? prm.fb_order : 0;
-  const int64_t nq = order != 0 ? n - (int64_t)tk.hist[0] : n;
 
-  // point queue, one point ahead: the next index is taken (and its coordinates
-  // loaded) while the current point is processed, so neither the queue atomic nor
-  // the point load sits on a point's critical path
-  // Points are taken kPtGrab at a time (one queue atomic per chunk: a single-address
-  // atomic per point serialises at ~13 ns, which had bounded the whole kernel);
-  // kPtGrab = 0: static round-robin over the waves of the grid.
-  const unsigned int nwaves = gridDim.x * (kBlock / kWave);
-  const unsigned int wave_id = blockIdx.x * (kBlock / kWave) + wave;
-  unsigned int idx = 0, cend = 0;
-  if (kPtGrab == 0) {
-    idx = wave_id;
-  } else {
-    if (lane == 0) idx = atomicAdd(work, kPtGrab);
-    idx = __shfl(idx, 0);
-    cend = idx + kPtGrab;
-  }
-  // queue position -> point index (identity unless PRE with a queue order)
-  const auto point_of = [&](unsigned int q) -> unsigned int {
-    if (order == 0 || (int64_t)q >= nq) return q;
-    return tk.perm[order == 1 ? (int64_t)q : nq - 1 - (int64_t)q];
-  };
-  unsigned int pn = point_of(idx);
+  // point queue, one point ahead: the next index is taken (and its coordinates,
+  // radius and state loaded) while the current point is processed, so neither the
+  // queue atomic nor the point loads sit on a point's critical path.  Points are
+  // taken kPtGrab at a time (one queue atomic per chunk: a single-address atomic per
+  // point serialises at ~13 ns, which had bounded the whole kernel).
+  unsigned int idx = 0;
+  if (lane == 0) idx = atomicAdd(work, kPtGrab);
+  idx = __shfl(idx, 0);
+  unsigned int cend = idx + kPtGrab;
   float xn[DIM], rn = 0.0f;
-  bool en = true;
-  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < nq ? pts[(int64_t)pn * DIM + k] : 0.0f;
-  if (PRE && (int64_t)idx < nq) {
-    rn = tk.prad[pn];
-    if (order == 0) en = (tk.pstate[pn] & kPtEstimate) != 0;
+  bool en = false;
+  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
+  if ((int64_t)idx < n) {
+    rn = tk.prad[idx];
+    en = (tk.pstate[idx] & kPtEstimate) != 0;
   }
   for (;;) {
-    if ((int64_t)idx >= nq) break;
-    const unsigned int pidx = pn;
+    if ((int64_t)idx >= n) break;
+    const unsigned int pidx = idx;
     const int64_t gidx = base + (int64_t)pidx * stride;
     float x[DIM];
     for (int k = 0; k < DIM; k++) x[k] = xn[k];
-    float firstR = rn;
-    bool estimate = en;
-    const bool grab = kPtGrab != 0 && idx + 1 >= cend;  // wave-uniform
+    const float firstR = rn;
+    const bool estimate = en;
+    const bool grab = idx + 1 >= cend;  // wave-uniform
     unsigned int nidx_l0 = 0;
     if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
-
     DIAG_T0(t_fb0);
-    if constexpr (!PRE) {
-      float nDist = kFltMax, nSigned = kFltMax;
-      if (sc.n_prims > 0) {
-        Closest c = (GG && sc.n_pgroups > kTreeMinGroups)
-                        ? closest_wave_grouped<DIM>(Lprim, sc.pgroup, sc.n_prims, sc.n_pgroups, x, lane)
-                        : closest_wave<DIM>(Lprim, sc.n_prims, x, lane);
-        nDist = c.d;
-        nSigned = signed_dist<DIM>(sc.paux, c, x);
-      }
-      float dDist, dSigned;
-      if (sc.n_dprims > 0) {
-        Closest c = sc.n_dgroups > kTreeMinGroups
-                        ? closest_wave_grouped<DIM>(sc.dprim, sc.dgroup, sc.n_dprims, sc.n_dgroups, x, lane)
-                        : closest_wave<DIM>(sc.dprim, sc.n_dprims, x, lane);
-        dDist = c.d;
-        dSigned = signed_dist<DIM>(sc.dpaux, c, x);
-      } else {
-        dDist = dSigned = bbox_far_dist<DIM>(sc, x);
-      }
-      int bucket;
-      const int32_t ps = point_state<DIM>(sc, prm, nDist, nSigned, dDist, dSigned, &bucket, &firstR);
-      estimate = (ps & kPtEstimate) != 0;
-      if (lane == 0) {
-        tk.pstate[pidx] = ps;
-        atomicAdd(&s_hist[bucket], 1u);
-      }
-    }
-    // the next point: its index (the atomic has returned by now), coordinates (and radius)
+    // the next point: its index (the atomic has returned by now), coordinates, radius, state
     unsigned int nidx, ncend = cend;
-    if (kPtGrab == 0) {
-      nidx = idx + nwaves;
-    } else if (grab) {
+    if (grab) {
       nidx = (unsigned int)__shfl((int)nidx_l0, 0);
       ncend = nidx + kPtGrab;
     } else {
       nidx = idx + 1;
     }
-    pn = point_of(nidx);
-    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < nq ? pts[(int64_t)pn * DIM + k] : 0.0f;
-    if (PRE && (int64_t)nidx < nq) {
-      rn = tk.prad[pn];
-      if (order == 0) en = (tk.pstate[pn] & kPtEstimate) != 0;
+    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
+    if ((int64_t)nidx < n) {
+      rn = tk.prad[nidx];
+      en = (tk.pstate[nidx] & kPtEstimate) != 0;
     }
     if (!estimate) { idx = nidx; cend = ncend; continue; }
     c_pts += lane == 0;
     DIAG_ADD(D_FB_SETUP, t_fb0);
     DIAG_COUNT(D_FB_PTS, 1);
     DIAG_T0(t_fb1);
-#if WOS_ABL_FB == 3
-    for (int i = lane; i < 2 * npairs * (DIM - 1); i += kWave) strat[i] = (i + 0.5f) / (2 * npairs * (DIM - 1));
-    wave_sync();
-#else
     build_lhs<DIM>(prm, gidx, strat, partner, reinterpret_cast<char*>(rejL), lane);
-#endif
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
     for (int w0 = 0; w0 < npairs; w0 += kWave) {
@@ -3312,10 +2838,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   }
   flush_counter(counters, C_ITERS, c_iters, lane);
   flush_counter(counters, C_PTS, c_pts, lane);
-  if constexpr (!PRE) {
-    __syncthreads();
-    if (threadIdx.x < kCostBuckets && s_hist[threadIdx.x]) atomicAdd(&tk.hist[threadIdx.x], s_hist[threadIdx.x]);
-  }
 #if WOS_DIAG
   __syncthreads();
   if (threadIdx.x < D_NUM) {
@@ -3359,82 +2881,6 @@ __device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& 
   }
 }
 
-// ... the complete state of a walk that continues after its first walk-kernel step
-// (two-phase walks: DevTasks r* arrays), and its restoration.  The Green's function
-// carries nothing across steps but its kind, which follows from the walk length
-// (walk_step_tail switches to Yukawa when walkLength reaches steps_before_tikhonov).
-template <int DIM>
-__device__ __forceinline__ void walk_save(const DevTasks& tk, int64_t t, const WalkState<DIM>& st, const Pcg32& ws,
-                                          float ddist, uint32_t wsteps) {
-  const int64_t T = tk.T;
-  for (int k = 0; k < DIM; k++) {
-    tk.pt[k * T + t] = st.pt[k];
-    tk.rn[k * T + t] = st.n[k];
-    tk.rpd[k * T + t] = st.prevDir[k];
-  }
-  tk.thr[t] = st.throughput;
-  tk.tsrc[t] = st.totalSource;
-  tk.dd[t] = ddist;
-  tk.rpdist[t] = st.prevDist;
-  tk.rtn[t] = st.totalNeumann;
-  tk.rwl[t] = (uint32_t)st.walkLength | (st.onNeumann ? 0x80000000u : 0u);
-  tk.rsteps[t] = wsteps;
-  tk.rrng[t] = ws.state;
-  tk.code[t] = kInFlight;
-}
-
-template <int DIM, bool RB>
-__device__ __forceinline__ void walk_resume(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t t,
-                                            WalkState<DIM>& st, Gfn<DIM, RB>& g, Pcg32& ws, float& ddist,
-                                            uint32_t& wsteps) {
-  const int64_t T = tk.T;
-  for (int k = 0; k < DIM; k++) {
-    st.pt[k] = tk.pt[k * T + t];
-    st.n[k] = tk.rn[k * T + t];
-    st.prevDir[k] = tk.rpd[k * T + t];
-  }
-  st.throughput = tk.thr[t];
-  st.totalSource = tk.tsrc[t];
-  ddist = tk.dd[t];
-  st.prevDist = tk.rpdist[t];
-  st.totalNeumann = tk.rtn[t];
-  const uint32_t wl = tk.rwl[t];
-  st.walkLength = (int)(wl & 0x7FFFFFFFu);
-  st.onNeumann = (wl >> 31) != 0u;
-  wsteps = tk.rsteps[t];
-  ws.state = tk.rrng[t];
-  const int sbt = prm.steps_before_tikhonov;
-  g.init(sc.absorption > 0.0f && (sbt == 0 || (sbt > 0 && st.walkLength >= sbt)), sc.absorption);
-}
-
-// computeStarRadius for one lane without the wave: the lane's cell list when the star
-// grid covers it, else the sequential group scan -- star_radius_wave's result.
-template <int DIM>
-__device__ __forceinline__ float star_radius_lane(const LGeom& G, const DevScene& sc, const DevParams& prm,
-                                                  const float* x, float maxR, bool flipOrient) {
-  const float minR = prm.min_star_radius, prec = prm.silhouette_precision;
-  if (minR > maxR) return maxR;
-  const float result = smax(maxR, minR);
-  if (sc.n_prims <= 0) return result;
-  const float r2 = maxR < kFltMax ? maxR * maxR : kFltMax, minR2 = minR * minR;
-  if (minR2 >= r2) return result;
-  if (G.sgrid != nullptr) {
-    const int cell = star_cell<DIM>(sc, x);
-    if (cell >= 0) return star_radius_cell<DIM>(G, cell, x, r2, minR2, minR, result, !flipOrient, prec);
-  }
-  return star_radius<DIM>(G, sc.n_sil, sc.n_sgroups, sc.n_prims, x, minR, maxR, prec, flipOrient);
-}
-
-// Waves with at most this many live walks (the long walks of the kernel's tail, which
-// set its critical path) run the step's queries lane by lane -- the sequential star
-// radius, ray and rejection loops, the same results -- instead of the cooperative
-// forms.  Default off: measured slower at every threshold (karman walk 2.50 -> 2.90 ms
-// at 4): even for one or two live lanes the cooperative forms have the shorter
-// dependency chains, spreading a walk's candidates over the idle lanes.
-#ifndef WOS_SEQ_LANES
-#define WOS_SEQ_LANES 0
-#endif
-
 // One iteration of the walk loop for every lane of the wave (convergent): the lanes
 // with active == false take part in the cooperative queries only.  Returns the
 // termination code (>= 0) or -1 while the walk continues.
@@ -3447,14 +2893,8 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   int code = -1;
   bool flip = false, query = false;
   if (active) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
-  const bool seq = WOS_SEQ_LANES > 0 && __popcll(__ballot(active)) <= WOS_SEQ_LANES;  // wave-uniform
   DIAG_T0(t_star);
-  float starQ = 0.0f;
-  if (seq) {
-    if (active && code < 0 && query) starQ = star_radius_lane<DIM>(G, sc, prm, st.pt, ddist, flip);
-  } else {
-    starQ = star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, st.pt, ddist, flip, starL, lane);
-  }
+  const float starQ = star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, st.pt, ddist, flip, starL, lane);
   DIAG_ADD(D_STAR, t_star);
   const bool live = active && code < 0;
   float dir[DIM], org[DIM], starR = 0.0f;
@@ -3464,11 +2904,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   DIAG_ADD(D_MID, t_mid);
   Hit ip;
   DIAG_T0(t_ray);
-  bool hit;
-  if (WOS_RAY_WAVE && !seq)
-    hit = !WOS_ABL_NO_RAY && ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
-  else
-    hit = live && !WOS_ABL_NO_RAY && sc.n_prims > 0 && ray_hit<DIM>(G, sc.n_prims, sc.n_pgroups, org, dir, starR, &ip);
+  const bool hit = ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
   DIAG_ADD(D_RAY, t_ray);
   DIAG_T0(t_end);
   if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
@@ -3476,13 +2912,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   float sp[DIM], pdf_unused;
   for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
   DIAG_T0(t_smp);
-  if (!prm.ignore_source) {
-    if (seq) {
-      if (live) sample_volume<DIM>(prm, g, dir, ws, &pdf_unused, sp, c_iters, false);
-    } else {
-      sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, c_iters, false, rejL, lane);
-    }
-  }
+  if (!prm.ignore_source) sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, c_iters, false, rejL, lane);
   DIAG_ADD(D_SAMPLE, t_smp);
   DIAG_T0(t_tail);
   if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
@@ -3507,89 +2937,6 @@ __device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams&
   atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);
 }
 
-// A task of point pidx has finished (its record is stored): count it; the walk that
-// completes the point queues it for the in-kernel fold.  Release on the count orders
-// this walk's record stores before it; the completing walk's acquire-release sees every
-// other walk's, and its release store of the queue entry passes them to the folder.
-// (The count itself is relaxed behind a release fence -- this wave's stores complete --
-// and only the completing walk takes the acquire: an acquire per walk would invalidate
-// the CU's L1 under every walker.)
-__device__ __forceinline__ void task_done(const DevTasks& tk, uint32_t pidx) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  const uint32_t old = __hip_atomic_fetch_add(&tk.pdone[pidx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old + 1u == (uint32_t)tk.wpp) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint32_t slot = atomicAdd(&tk.rqc[0], 1u);
-    __hip_atomic_store(&tk.rq[slot], pidx, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// wos_fold_kernel's statistics for one point by one lane, records read straight from
-// memory kFoldBatch at a time (the same operations in the same order: bit-identical)
-constexpr int kFoldBatch = 8;
-template <int DIM>
-__device__ void fold_point(const DevParams& prm, const DevTasks& tk, uint32_t i) {
-  const int64_t T = tk.T;
-  const int wpp = tk.wpp;
-  const int ps = tk.pstate[i];
-  const bool estimate = ps & kPtEstimate;
-  float mean[DIM + 1];
-  for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
-  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
-  int sN = 0;
-  uint32_t steps = 0;
-  if (estimate) {
-    for (int c0 = 0; c0 < wpp; c0 += kFoldBatch) {
-      uint32_t vc[kFoldBatch];
-      float vt[kFoldBatch], vf[kFoldBatch], vb[kFoldBatch][DIM], vs[kFoldBatch][DIM];
-#pragma unroll
-      for (int j = 0; j < kFoldBatch; j++) {
-        const int64_t t = (int64_t)i * wpp + c0 + j;
-        if (c0 + j < wpp) {
-          vc[j] = tk.code[t];
-          vt[j] = tk.total[t];
-          vf[j] = tk.first[t];
-          for (int k = 0; k < DIM; k++) { vb[j][k] = tk.bdir[k * T + t]; vs[j][k] = tk.sdir[k * T + t]; }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kFoldBatch; j++) {
-        const int r = c0 + j;
-        if (r >= wpp) break;
-        if (r % prm.n_anti == 0) {
-          cvb = mean[0];
-          cvs = sFirst / (float)(sN > 1 ? sN : 1);
-          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
-        }
-        const uint32_t code = vc[j];
-        steps += code >> 1;
-        if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
-        const float total = vt[j];
-        const float first = vf[j];
-        sN += 1;
-        const float fN = (float)sN;
-        {
-          const float delta = total - mean[0];
-          mean[0] += delta / fN;
-        }
-        for (int k = 0; k < DIM; k++) {
-          const float be = (total - first - cvb) * vb[j][k];
-          const float se = (first - cvs) * vs[j][k];
-          const float delta = (be + se) - mean[k + 1];
-          mean[k + 1] += delta / fN;
-        }
-        sFirst += first;
-      }
-    }
-  }
-  const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
-  tk.p_out[i] = maskP ? 0.0f : mean[0];
-  for (int k = 0; k < DIM; k++) tk.g_out[(int64_t)i * DIM + k] = maskG ? 0.0f : mean[k + 1];
-  if (tk.nest_out) tk.nest_out[i] = sN;
-  if (tk.steps_out) tk.steps_out[i] = (int32_t)steps;
-  tk.pdone[i] = (uint32_t)wpp + 1u;  // folded: the fold kernel that follows skips the point
-}
-
 __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters, const unsigned int* s_ctr) {
   if (threadIdx.x < C_NUM && threadIdx.x != C_ITERS && threadIdx.x != C_PTS) {
     unsigned int v = threadIdx.x == C_REC ? s_ctr[C_RR] + s_ctr[C_DIR] : s_ctr[threadIdx.x];
@@ -3602,40 +2949,7 @@ __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters
 #endif
 constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
 
-// experiment (0 = off): WOS_PRIO=n raises the wave priority with the age of its
-// oldest walk (steps / n) -- within noise on karman, slower on C and the cube
-#ifndef WOS_PRIO
-#define WOS_PRIO 0
-#endif
-// 1: the staged ring also carries each task's record (pt, throughput, source total,
-// Dirichlet distance), loaded one iteration ahead; 0 (default, measured faster on
-// every config: the staged records cost registers the step needs): only the task
-// index and its point's state are staged, the record is loaded at hand-out
-// 1: refill the ring right after the hand-out instead of at the end of the iteration
-// (the staged tasks' loads get a whole step to land): within noise on karman / C / D,
-// with the staged records as well (WOS_TASK_RING) slower (profiles/r2e_ab_refill.log)
-// 1: compile the in-kernel fold into the walk kernel (used when DevParams::tail_fold).
-// It is best effort: a folding wave waits at most kTailFoldSpins sleeps for a claimed
-// point's last walk, and wos_fold_kernel (always launched after the walk kernel) folds
-// every point not marked folded -- so a slow tail costs time, never results.
-// Off: bit-identical (tests/test_gpu_switches.py) but the per-walk completion count
-// needs a device-scope release, i.e. an L2 write-back on MI355X's per-XCD L2s, for
-// every walk: karman walk kernel 2.4 -> 6.0 ms, cube 3.2 -> 16 ms
-// (profiles/r2t_ab_tail_fold*.log), whatever the folders' wait.
-#ifndef WOS_TAIL_FOLD
-#define WOS_TAIL_FOLD 0
-#endif
-#ifndef WOS_TAIL_SPINS
-#define WOS_TAIL_SPINS (1u << 16)
-#endif
-constexpr uint32_t kTailFoldSpins = WOS_TAIL_SPINS;
-#ifndef WOS_EARLY_REFILL
-#define WOS_EARLY_REFILL 0
-#endif
-#ifndef WOS_TASK_RING
-#define WOS_TASK_RING 0
-#endif
-// 4 waves per SIMD (<= 128 VGPRs): latency hiding for the walk's long dependent chains
+
 #ifndef WOS_WALK_WAVES_PER_EU
 #define WOS_WALK_WAVES_PER_EU 4
 #endif
@@ -3645,9 +2959,7 @@ constexpr uint32_t kTailFoldSpins = WOS_TAIL_SPINS;
 // BSTART: the tasks are boundary-start walks (estimateSolution, walk_on_stars.h:353-464:
 // start normal, first sphere radius, on-Neumann flag from DevTasks::n0/r0/sflags, no
 // first ball, walk stream tag 6) -- boundary value caching (wos_bvc.hip).
-// RESUME: the queue is the survivor list of wos_walk_first_kernel (tk.surv, length
-// tk.shist[2 kCostBuckets]) and each task continues from its saved state.
-template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool RESUME = false, bool NEU = true>
+template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool NEU = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_kernel(
     const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
@@ -3657,9 +2969,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const DevParams& prm = prm_arg;
   const DevTasks& tk = tk_arg;
   const int lane = threadIdx.x & (kWave - 1);
-  // the in-kernel fold (DevParams::tail_fold) belongs to the first-ball walks
-  constexpr bool TAILF = WOS_TAIL_FOLD && !BSTART && !RESUME;
-  const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
+  stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
   // per-wave scratch shared by the star and ray queries (used one after the other)
   const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // wave-uniform: SGPR address
@@ -3667,18 +2977,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
   RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
-  (void)rayL;
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
 
-  // queue length: every task, or (RESUME) the survivors of the first step
-  const uint32_t T = RESUME ? tk.shist[2 * kCostBuckets] : (uint32_t)tk.T;
+  const uint32_t T = (uint32_t)tk.T;
   const uint32_t wpp = (uint32_t)tk.wpp;
   // x / wpp as a shift when walks-per-point is a power of two (every shipped config)
-  const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
+  const int wsh = (wpp & (wpp - 1u)) == 0u ? __builtin_ctz(wpp) : -1;
   auto divw = [&](uint32_t x) -> uint32_t { return wsh >= 0 ? x >> wsh : x / wpp; };
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
   uint32_t c_iters = 0;
@@ -3687,18 +2995,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // ---- task supply: a window [wq, we) of the global queue (wave-uniform; lane i
   // holds perm[wp0 + i]) feeds a 64-slot ring of staged tasks, one per lane: ring
   // position (lane - head) & 63, positions [0, S) valid.  The ring is refilled at
-  // the end of every iteration, so the loads of a staged task (its record and its
-  // point's state) are in flight during a whole step and a lane that finishes a
-  // walk starts the next one from registers (cross-lane shuffles) instead of a
-  // chain of dependent global loads.
-  // <= 64 points per window (RESUME: 64 survivors, lane i holds surv[window + i])
-  const uint32_t G_win = RESUME ? (uint32_t)kWave : (kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp);
+  // the end of every iteration, so the loads of a staged task's point state are in
+  // flight during a whole step and a lane that finishes a walk starts the next one
+  // from registers (cross-lane shuffles) instead of a chain of dependent global loads.
+  // <= 64 points per window
+  const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;
   uint32_t wq = 0, we = 0, wp0 = 0, wperm = 0;
   bool exhausted = false;
   int head = 0, S = 0;
   uint32_t s_t = 0, s_ok = 0;  // staged task index, its point is estimated
-  float s_pt[DIM], s_thr = 0.0f, s_tsrc = 0.0f, s_dd = 0.0f;
-  for (int k = 0; k < DIM; k++) s_pt[k] = 0.0f;
   auto refill = [&](const DevTasks& tk) {
     while (S < kWave && !exhausted) {
       if (wq >= we) {
@@ -3708,35 +3013,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         if (c >= T) { exhausted = true; break; }
         wq = c;
         we = (T - c) < G_win ? T : c + G_win;
-        if (RESUME) {
-          wp0 = c;
-          wperm = (uint32_t)lane < we - c ? tk.surv[c + lane] : 0u;
-        } else {
-          wp0 = divw(c);
-          const uint32_t np = divw(we - 1) - wp0 + 1;
-          wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
-        }
+        wp0 = divw(c);
+        const uint32_t np = divw(we - 1) - wp0 + 1;
+        wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;
       }
       const int avail = (int)(we - wq);
       const int take = (kWave - S) < avail ? (kWave - S) : avail;
       const int pos = ((lane - head) & (kWave - 1)) - S;
       const bool mine = pos >= 0 && pos < take;
-      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = RESUME ? q : divw(q);
+      const uint32_t q = wq + (mine ? (uint32_t)pos : 0u), qp = divw(q);
       const uint32_t pidx = (uint32_t)__shfl((int)wperm, (int)(qp - wp0));  // queue position -> permuted point
       if (mine) {
-        if (RESUME) {
-          s_t = pidx;  // the survivor's task index
-          s_ok = 1u;
-        } else {
-          s_t = pidx * wpp + (q - qp * wpp);
-          s_ok = tk.pstate[pidx] & kPtEstimate;
-        }
-        if (WOS_TASK_RING) {
-          for (int k = 0; k < DIM; k++) s_pt[k] = tk.pt[k * tk.T + s_t];
-          s_thr = tk.thr[s_t];
-          s_tsrc = tk.tsrc[s_t];
-          s_dd = (BSTART || sc.n_dprims > 0) ? tk.dd[s_t] : bbox_far_dist<DIM>(sc, s_pt);
-        }
+        s_t = pidx * wpp + (q - qp * wpp);
+        s_ok = tk.pstate[pidx] & kPtEstimate;
       }
       S += take;
       wq += (uint32_t)take;
@@ -3744,7 +3033,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   };
   refill(tk);
   int64_t t = -1;           // this lane's task
-  int wmax = 0;             // longest live walk of the wave (steps), wave-uniform
   WalkState<DIM> st;
   Gfn<DIM, RB> g;
   Pcg32 ws;
@@ -3759,7 +3047,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
     const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
     const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
-    const LGeom G = WOS_KVIEW ? geometry_view<DIM, GG>(sc, smem, true, false) : G0;
+    const LGeom G = geometry_view<DIM, GG>(sc, smem, true, false);
     // ---- hand staged tasks to idle lanes (uniform control flow)
     {
       const uint64_t need = __ballot(t < 0);
@@ -3772,12 +3060,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         const uint32_t v_t = (uint32_t)__shfl((int)s_t, src);
         const uint32_t v_ok = (uint32_t)__shfl((int)s_ok, src);
         float v_pt[DIM], v_thr = 0.0f, v_tsrc = 0.0f, v_dd = 0.0f;
-        if (WOS_TASK_RING) {
-          for (int kk = 0; kk < DIM; kk++) v_pt[kk] = __shfl(s_pt[kk], src);
-          v_thr = __shfl(s_thr, src);
-          v_tsrc = __shfl(s_tsrc, src);
-          v_dd = __shfl(s_dd, src);
-        } else if (!RESUME && t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
+        if (t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
           for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];
           v_thr = tk.thr[v_t];
           v_tsrc = tk.tsrc[v_t];
@@ -3788,57 +3071,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
           t = (int64_t)v_t;
           if (!v_ok) {  // point outside the domain: no walks
             tk.code[t] = 0u;
-            if (TAILF && prm.tail_fold) task_done(tk, divw(v_t));
             t = -1;
           } else {
-            if constexpr (RESUME) {
-              walk_resume<DIM, RB>(sc, prm, tk, t, st, g, ws, ddist, wsteps);
-              firstR = 0.0f;
-            } else {
-              const uint32_t pidx = divw(v_t);
-              const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
-              walk_start<DIM, BSTART, RB>(sc, prm, tk, t, pidx, w, v_pt, v_thr, v_tsrc, v_dd, base, stride, yuk0, st,
-                                          g, ws, ddist, wsteps, firstR);
-            }
+            const uint32_t pidx = divw(v_t);
+            const uint32_t w = (v_t - pidx * wpp) >> (prm.n_anti - 1);  // n_anti is 1 or 2
+            walk_start<DIM, BSTART, RB>(sc, prm, tk, t, pidx, w, v_pt, v_thr, v_tsrc, v_dd, base, stride, yuk0, st,
+                                        g, ws, ddist, wsteps, firstR);
           }
         }
         head = (head + take) & (kWave - 1);
         S -= take;
       }
     }
-    // early refill: the ring is topped up right after the hand-out, so the loads of the
-    // staged tasks (queue window, permutation, point state) have the whole step to land
-    // before the next hand-out reads them
-    if (WOS_EARLY_REFILL) refill(tk);
     if (__ballot(t >= 0) == 0) {
       if (S == 0 && exhausted) break;  // queue drained and every lane idle
       refill(tk);
       continue;
     }
-#if WOS_PRIO
-    {
-      int wl = t >= 0 ? st.walkLength : 0;
-      for (int off = kWave / 2; off > 0; off >>= 1) wl = smax(wl, __shfl_xor(wl, off));
-      wmax = __builtin_amdgcn_readfirstlane(wl);
-    }
-#endif
-#if WOS_PRIO
-    if (wmax >= 3 * WOS_PRIO) __builtin_amdgcn_s_setprio(3);
-    else if (wmax >= 2 * WOS_PRIO) __builtin_amdgcn_s_setprio(2);
-    else if (wmax >= WOS_PRIO) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#endif
-
     DIAG_COUNT(D_ITERS, 1);
     DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
     const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
-      if (TAILF && prm.tail_fold) task_done(tk, divw((uint32_t)t));
       t = -1;
     }
-    if (!WOS_EARLY_REFILL) refill(tk);
+    refill(tk);
     DIAG_ADD(D_LOOP, t_loop);
 #if WOS_DIAG
     if (exhausted) {
@@ -3847,32 +3105,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       DIAG_ADD(D_XLOOP, t_loop);
     }
 #endif
-  }
-
-  // ---- in-kernel fold: this wave has nothing left to walk; it folds finished points
-  // (64 queue slots per claim, a lane per point) while the last walks run elsewhere.
-  // Every slot below the point count is eventually written (each point's last walk
-  // queues it), so the waits end; they sleep instead of spinning hot.
-  if (TAILF && prm_arg.tail_fold) {
-    const uint32_t npts = (uint32_t)(tk_arg.T / tk_arg.wpp);
-    for (;;) {
-      uint32_t h = 0;
-      if (lane == 0) h = atomicAdd(&tk_arg.rqc[1], (uint32_t)kWave);
-      h = (uint32_t)__shfl((int)h, 0);
-      if (h >= npts) break;
-      const uint32_t slot = h + (uint32_t)lane;
-      if (slot < npts) {
-        uint32_t p;
-        uint32_t spins = 0;  // bounded: a point whose walks outlast the wait is left to the fold kernel
-        // relaxed polling (an acquire per poll would invalidate the CU's L1 under the
-        // walkers' feet), then one acquire fence before the records are read
-        while ((p = __hip_atomic_load(&tk_arg.rq[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0xFFFFFFFFu &&
-               ++spins < kTailFoldSpins)
-          __builtin_amdgcn_s_sleep(8);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (p != 0xFFFFFFFFu) fold_point<DIM>(prm_arg, tk_arg, p);
-      }
-    }
   }
   DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
   flush_counter(counters, C_ITERS, c_iters, lane);
@@ -3886,133 +3118,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   flush_walk_counters(counters, s_ctr);
 }
 
-// ---- two-phase walks: the first walk-kernel step of every task --------------
-// Most walks end in their first walk-kernel step (karman: 86 %), so the persistent
-// kernel's machinery -- the queue window, the staged ring, the hand-out, a task per
-// lane per iteration -- is paid per walk.  wos_walk_first_kernel runs that first
-// step for 64 consecutive tasks per wave and iteration (tasks in point-major order:
-// coalesced loads of the start records, every lane busy, no queue), writes the
-// records of the walks that ended, and saves the state of the others (walk_save),
-// counting them per cost bucket of their point.  wos_surv_offsets_kernel /
-// wos_surv_scatter_kernel list the survivors longest-expected-first, and the walk
-// kernel in RESUME mode finishes them.  Same arithmetic, same draws, same records.
-template <int DIM, bool GG, bool RB = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_first_kernel(
-    const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
-    unsigned long long* __restrict__ counters, int geom_floats) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ unsigned int s_ctr[C_NUM];
-  __shared__ uint32_t s_shist[kCostBuckets];
-  const DevScene& sc = sc_arg;
-  const DevParams& prm = prm_arg;
-  const DevTasks& tk = tk_arg;
-  const int lane = threadIdx.x & (kWave - 1);
-  const LGeom G0 = stage_geometry<DIM, GG>(sc, smem, true);
-  stage_rej_jump(prm);
-  const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();
-  StarLDS<DIM>* starL = reinterpret_cast<StarLDS<DIM>*>(wscratch);
-  RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
-  RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
-  if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
-  if (threadIdx.x < kCostBuckets) s_shist[threadIdx.x] = 0u;
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
-#endif
-  __syncthreads();
-  const int64_t T = tk.T;
-  const uint32_t wpp = (uint32_t)tk.wpp;
-  const int wsh = (WOS_FASTDIV && (wpp & (wpp - 1u)) == 0u) ? __builtin_ctz(wpp) : -1;
-  const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
-  uint32_t c_iters = 0;
-  const int64_t nchunks = (T + kWave - 1) / kWave;
-  const int64_t nwaves = (int64_t)gridDim.x * (kBlock / kWave);
-  for (int64_t chunk = (int64_t)blockIdx.x * (kBlock / kWave) + wave_u; chunk < nchunks; chunk += nwaves) {
-    KernArgsPtr ka = kernargs_opaque();
-    const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
-    const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
-    const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
-    const LGeom G = WOS_KVIEW ? geometry_view<DIM, GG>(sc, smem, true, false) : G0;
-    const int64_t t = chunk * kWave + lane;
-    const bool valid = t < T;
-    const uint32_t pidx = valid ? (wsh >= 0 ? (uint32_t)t >> wsh : (uint32_t)t / wpp) : 0u;
-    const int ps = valid ? tk.pstate[pidx] : 0;
-    const bool ok = (ps & kPtEstimate) != 0;
-    if (valid && !ok) tk.code[t] = 0u;  // point outside the domain: no walks
-    WalkState<DIM> st;
-    Gfn<DIM, RB> g;
-    Pcg32 ws;
-    float ddist = 0.0f, firstR = 0.0f;
-    uint32_t wsteps = 0;
-    for (int k = 0; k < DIM; k++) st.pt[k] = 0.0f;
-    if (ok) {
-      float v_pt[DIM];
-      for (int k = 0; k < DIM; k++) v_pt[k] = tk.pt[k * T + t];
-      const uint32_t w = ((uint32_t)t - pidx * wpp) >> (prm.n_anti - 1);
-      walk_start<DIM, false, RB>(sc, prm, tk, t, pidx, w, v_pt, tk.thr[t], tk.tsrc[t],
-                                 sc.n_dprims > 0 ? tk.dd[t] : bbox_far_dist<DIM>(sc, v_pt), base, stride, yuk0,
-                                 st, g, ws, ddist, wsteps, firstR);
-    }
-    if (__ballot(ok) == 0) continue;
-    DIAG_COUNT(D_ITERS, 1);
-    DIAG_COUNT(D_LANES, __popcll(__ballot(ok)));
-    const int code = walk_iteration<DIM, GG, false, RB>(sc, prm, G, ok, st, g, ws, ddist, wsteps, firstR, starL, rayL,
-                                                        rejL, &c_iters, lane);
-    if (ok) {
-      if (code >= 0) {
-        walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
-      } else {
-        walk_save<DIM>(tk, t, st, ws, ddist, wsteps);
-        atomicAdd(&s_shist[(ps >> 8) & (kCostBuckets - 1)], 1u);
-      }
-    }
-  }
-  flush_counter(counters, C_ITERS, c_iters, lane);
-  __syncthreads();
-#if WOS_DIAG
-  if (threadIdx.x < D_NUM) {
-    if (diag_is_max(threadIdx.x)) atomicMax(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-    else atomicAdd(&g_diag[threadIdx.x], s_diag[threadIdx.x]);
-  }
-#endif
-  if (threadIdx.x < kCostBuckets && s_shist[threadIdx.x]) atomicAdd(&tk.shist[threadIdx.x], s_shist[threadIdx.x]);
-  flush_walk_counters(counters, s_ctr);
-}
-
-// survivor bucket offsets, highest bucket (longest expected walks) first, and the total
-// (templates only for the linkage: instantiated by wos_kernel.hip and wos_robust.hip)
-template <int N = 0>
-__global__ void wos_surv_offsets_kernel(uint32_t* __restrict__ shist) {
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int b = kCostBuckets - 1; b >= 0; b--) { shist[kCostBuckets + b] = acc; acc += shist[b]; }
-    shist[2 * kCostBuckets] = acc;
-  }
-}
-
-// the survivors (code == kInFlight) into tk.surv in bucket order; block-aggregated like
-// wos_lpt_scatter_kernel (order inside a bucket is immaterial: results do not depend on it)
-template <int N = 0>
-__global__ __launch_bounds__(256) void wos_surv_scatter_kernel(const DevTasks tk) {
-  __shared__ uint32_t cnt[kCostBuckets], base[kCostBuckets];
-  if (threadIdx.x < kCostBuckets) cnt[threadIdx.x] = 0u;
-  __syncthreads();
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int b = 0;
-  uint32_t local = 0;
-  const bool in = t < tk.T && tk.code[t] == kInFlight;
-  if (in) {
-    b = (tk.pstate[t / tk.wpp] >> 8) & (kCostBuckets - 1);
-    local = atomicAdd(&cnt[b], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < kCostBuckets && cnt[threadIdx.x])
-    base[threadIdx.x] = atomicAdd(&tk.shist[kCostBuckets + threadIdx.x], cnt[threadIdx.x]);
-  __syncthreads();
-  if (in) tk.surv[base[b] + local] = (uint32_t)t;
-}
-
-// ---- kernel 3: statistics + outputs ----------------------------------------
 // One thread per point, kFoldPoints points per block.  The records of the
 // block's points are contiguous (point-major tasks), so they are staged through
 // LDS in chunks of kFoldChunk records per point with coalesced 64-B loads, then
@@ -4043,11 +3148,8 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   const int64_t i = p0 + tid;
   const int64_t T = tk.T;
   const int wpp = tk.wpp;
-  // points already folded by the walk kernel's idle waves (DevParams::tail_fold)
-  const bool folded = prm.tail_fold && tid < nb && tk.pdone[i] == (uint32_t)wpp + 1u;
-  if (__syncthreads_and(folded || tid >= nb)) return;
   const int ps = tid < nb ? tk.pstate[i] : 0;
-  const bool estimate = (ps & kPtEstimate) && !folded;
+  const bool estimate = (ps & kPtEstimate) != 0;
   float mean[DIM + 1];
   for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
   float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
@@ -4094,7 +3196,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
         }
         const uint32_t code = __float_as_uint(lds[0][tid][j]);
         steps += code >> 1;
-        if (!(code & 1u) || WOS_ABL_NO_STATS) continue;
+        if (!(code & 1u)) continue;
         const float total = lds[1][tid][j];
         const float first = lds[2][tid][j];
         sN += 1;
@@ -4114,7 +3216,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
     }
     __syncthreads();
   }
-  if (tid >= nb || folded) return;
+  if (tid >= nb) return;
   const bool maskP = ps & kPtMaskP, maskG = ps & kPtMaskG;
   p_out[i] = maskP ? 0.0f : mean[0];
   for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];

@@ -570,45 +570,7 @@ double yukawa_f(int dim, double s) {
   return std::max(best, std::max(fc, fd));
 }
 
-// magnitude of the two terms of x Q_s(x) (their float evaluation error scales with it)
-double yukawa_m(int dim, double s, double x) {
-  if (dim == 2) return x * (bessk0(s * x) + bessk0(s) / bessi0(s) * bessi0(s * x));
-  const double sx = s * x;
-  const double sh = 0.5 * (std::exp(sx) - std::exp(-sx));
-  const double shs = 0.5 * (std::exp(s) - std::exp(-s));
-  return x * (std::exp(-sx) + std::exp(-s) * sh / shs);
-}
-
 }  // namespace
-
-void rejection_envelope_table(int dim, float* tab) {
-  for (int k = 0; k < kRejTabBins; k++) {
-    float* row = tab + (size_t)k * kRejEnvX * 2;
-    if (k == 0) {  // s -> 0: x Q_s(x) is unbounded across the bin -- no envelope
-      for (int j = 0; j < kRejEnvX; j++) { row[2 * j] = 3.0e38f; row[2 * j + 1] = 0.0f; }
-      continue;
-    }
-    const double s0 = ((double)k / kRejTabScale) * ((double)k / kRejTabScale);
-    const double s1 = ((double)(k + 1) / kRejTabScale) * ((double)(k + 1) / kRejTabScale);
-    for (int j = 0; j < kRejEnvX; j++) {
-      double fmax = 0.0, fmin = 1e300, mmax = 0.0;
-      for (int a = 0; a <= 16; a++) {
-        const double sv = s0 + (s1 - s0) * a / 16.0;
-        for (int b = 0; b <= 32; b++) {
-          const double x = std::max(1e-9, ((double)j + b / 32.0) / kRejEnvX);
-          const double f = x * yukawa_q(dim, sv, x);
-          fmax = std::max(fmax, f);
-          fmin = std::min(fmin, f);
-          mmax = std::max(mmax, yukawa_m(dim, sv, x));
-        }
-      }
-      const double hi = 1.02 * fmax + 2e-5 * mmax;
-      const double lo = 0.98 * fmin - 2e-5 * mmax;
-      row[2 * j] = (float)hi;
-      row[2 * j + 1] = lo > 0.0 ? (float)lo : 0.0f;
-    }
-  }
-}
 
 void rejection_bound_table(int dim, float* tab) {
   for (int k = 0; k < kRejTabBins; k++) {

@@ -93,16 +93,6 @@ bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget
 // discretisations and the float rounding of the kernel's exact test).
 void rejection_bound_table(int dim, float* tab);
 
-// Two-sided envelope of the accept threshold per cell of (s, x): for s-bin k (as above)
-// and x-bin j = floor(kRejEnvX * x), tab[(k * kRejEnvX + j) * 2] >= x Q_s(x) (hi) and
-// tab[... + 1] <= x Q_s(x) (lo) over the whole cell: the maximum / minimum over a 17 x 33
-// grid of the cell, widened by 2 % and by 2e-5 of the magnitude x (|K0| + |rho I0|) of the
-// two terms (2D; 3D the exponentials), far beyond the grid's interpolation error and the
-// float rounding of the kernel's exact test.  Bin 0 (s -> 0, unbounded) has none.
-// The kernel decides u > hi R / (norm bound) as a reject and u < lo R / (norm bound) as an
-// accept without evaluating the Green's function (tests/test_rejection_bounds.py checks
-// both against the exact threshold on dense grids of balls).
-void rejection_envelope_table(int dim, float* tab);
 
 bool prepare_scene(const HostSceneInput& in, HostScene& out, std::string& err);
 bool load_obj(const std::string& path, int dim, bool flip, bool normalize_domain, std::vector<float>& verts,

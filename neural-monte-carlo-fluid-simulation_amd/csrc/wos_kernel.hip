@@ -1,8 +1,8 @@
 // wos_kernel.hip -- gfx950 walk-on-stars solve: the kernel instantiations and their
 // host launchers (device code in wos_device.h).
 //
-// One projection = wos_first_ball_kernel (point setup + first balls), the walk-queue
-// order (wos_lpt_*), the persistent wos_walk_kernel and wos_fold_kernel (statistics
+// One projection = wos_point_setup_kernel, the walk-queue order (wos_lpt_scatter_kernel),
+// wos_first_ball_kernel, the persistent wos_walk_kernel and wos_fold_kernel (statistics
 // + masked outputs), all on the caller's stream.
 #include "wos_device.h"
 #include "wos_launch.h"
@@ -39,55 +39,26 @@ __global__ __launch_bounds__(256) void wos_lpt_scatter_kernel(const DevTasks tk,
   if (i < n) tk.perm[base[b] + local] = (uint32_t)i;
 }
 
-template __global__ void wos_first_ball_kernel<2, false>(const DevScene, const DevParams, const float*, int64_t,
-                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
-                                                           unsigned int*, int, int);
-template __global__ void wos_walk_kernel<2, false>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                                     unsigned long long*, unsigned int*, int);
-#define WOS_INERT_WALK(D, G)                                                                                      \
-  template __global__ void wos_walk_kernel<D, G, false, false, false, false>(const DevScene, const DevParams,     \
-                                                                             const DevTasks, int64_t, int64_t,     \
-                                                                             unsigned long long*, unsigned int*, int)
-WOS_INERT_WALK(2, false);
-WOS_INERT_WALK(2, true);
-WOS_INERT_WALK(3, false);
-WOS_INERT_WALK(3, true);
-#undef WOS_INERT_WALK
-template __global__ void wos_first_ball_kernel<2, true>(const DevScene, const DevParams, const float*, int64_t,
-                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
-                                                           unsigned int*, int, int);
-template __global__ void wos_walk_kernel<2, true>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                                     unsigned long long*, unsigned int*, int);
-template __global__ void wos_first_ball_kernel<3, false>(const DevScene, const DevParams, const float*, int64_t,
-                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
-                                                           unsigned int*, int, int);
-template __global__ void wos_walk_kernel<3, false>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                                     unsigned long long*, unsigned int*, int);
-template __global__ void wos_first_ball_kernel<3, true>(const DevScene, const DevParams, const float*, int64_t,
-                                                           int64_t, int64_t, const DevTasks, unsigned long long*,
-                                                           unsigned int*, int, int);
-template __global__ void wos_walk_kernel<3, true>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t,
-                                                     unsigned long long*, unsigned int*, int);
-#define WOS_TWO_PHASE(D, G)                                                                                   \
-  template __global__ void wos_walk_first_kernel<D, G, false>(const DevScene, const DevParams, const DevTasks,      \
-                                                              int64_t, int64_t, unsigned long long*, int);        \
-  template __global__ void wos_walk_kernel<D, G, false, false, true>(const DevScene, const DevParams, const DevTasks, \
-                                                                     int64_t, int64_t, unsigned long long*,       \
-                                                                     unsigned int*, int)
-WOS_TWO_PHASE(2, false);
-WOS_TWO_PHASE(2, true);
-WOS_TWO_PHASE(3, false);
-WOS_TWO_PHASE(3, true);
-#undef WOS_TWO_PHASE
-#define WOS_PRE_FB(D)                                                                                          \
-  template __global__ void wos_first_ball_kernel<D, false, false, true>(const DevScene, const DevParams, const float*, \
-                                                                        int64_t, int64_t, int64_t, const DevTasks,    \
-                                                                        unsigned long long*, unsigned int*, int, int); \
-  template __global__ void wos_point_setup_kernel<D>(const DevScene, const DevParams, const float*, int64_t,         \
-                                                     const DevTasks)
-WOS_PRE_FB(2);
-WOS_PRE_FB(3);
-#undef WOS_PRE_FB
+template __global__ void wos_first_ball_kernel<2>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                                   int64_t, const DevTasks, unsigned long long*, unsigned int*, int);
+template __global__ void wos_first_ball_kernel<3>(const DevScene, const DevParams, const float*, int64_t, int64_t,
+                                                   int64_t, const DevTasks, unsigned long long*, unsigned int*, int);
+template __global__ void wos_point_setup_kernel<2>(const DevScene, const DevParams, const float*, int64_t,
+                                                   const DevTasks);
+template __global__ void wos_point_setup_kernel<3>(const DevScene, const DevParams, const float*, int64_t,
+                                                   const DevTasks);
+// walk kernels: <DIM, GG> with the Neumann term, and the Neumann-inert <DIM, GG, false, false, false>
+#define WOS_WALK(D, G)                                                                                            \
+  template __global__ void wos_walk_kernel<D, G>(const DevScene, const DevParams, const DevTasks, int64_t, int64_t, \
+                                                 unsigned long long*, unsigned int*, int);                        \
+  template __global__ void wos_walk_kernel<D, G, false, false, false>(const DevScene, const DevParams,            \
+                                                                      const DevTasks, int64_t, int64_t,           \
+                                                                      unsigned long long*, unsigned int*, int)
+WOS_WALK(2, false);
+WOS_WALK(2, true);
+WOS_WALK(3, false);
+WOS_WALK(3, true);
+#undef WOS_WALK
 template __global__ void wos_fold_kernel<2>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
                                             int32_t*);
 template __global__ void wos_fold_kernel<3>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
@@ -138,26 +109,15 @@ __global__ void wos_math_selftest_kernel(int which, const double* x, double* out
 // ---------------------------------------------------------------------------
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
-                              unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                              bool pre, hipStream_t s) {
+                              unsigned int* work, int grid, size_t shmem, int lhs_floats, hipStream_t s) {
   if (prm.robust)
-    return launch_first_balls_rb(dim, sc, prm, pts, n, base, stride, tk, counters, work, grid, shmem, geom_floats,
-                                 lhs_floats, pre, s);
-#define WOS_LAUNCH_FB(D, G)                                                                                  \
-  hipLaunchKernelGGL((wos_first_ball_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, \
-                     tk, counters, work, geom_floats, lhs_floats)
-#define WOS_LAUNCH_PRE(D)                                                                                          \
-  hipLaunchKernelGGL((wos_first_ball_kernel<D, false, false, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, \
-                     n, base, stride, tk, counters, work, 0, lhs_floats)
-  if (pre) {
-    if (dim == 2) WOS_LAUNCH_PRE(2); else WOS_LAUNCH_PRE(3);
-  } else if (dim == 2) {
-    if (sc.geom_global) WOS_LAUNCH_FB(2, true); else WOS_LAUNCH_FB(2, false);
-  } else {
-    if (sc.geom_global) WOS_LAUNCH_FB(3, true); else WOS_LAUNCH_FB(3, false);
-  }
-#undef WOS_LAUNCH_FB
-#undef WOS_LAUNCH_PRE
+    return launch_first_balls_rb(dim, sc, prm, pts, n, base, stride, tk, counters, work, grid, shmem, lhs_floats, s);
+  if (dim == 2)
+    hipLaunchKernelGGL(wos_first_ball_kernel<2>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, tk,
+                       counters, work, lhs_floats);
+  else
+    hipLaunchKernelGGL(wos_first_ball_kernel<3>, dim3(grid), dim3(kBlock), shmem, s, sc, prm, pts, n, base, stride, tk,
+                       counters, work, lhs_floats);
   return hipGetLastError();
 }
 
@@ -184,7 +144,7 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
 #define WOS_LAUNCH_WALK(D, G)                                                                                    \
   do {                                                                                                           \
     if (prm.neumann_inert)                                                                                       \
-      hipLaunchKernelGGL((wos_walk_kernel<D, G, false, false, false, false>), dim3(grid), dim3(kBlock), shmem, s, sc, \
+      hipLaunchKernelGGL((wos_walk_kernel<D, G, false, false, false>), dim3(grid), dim3(kBlock), shmem, s, sc, \
                          prm, tk, base, stride, counters, tqueue, geom_floats);                                  \
     else                                                                                                         \
       hipLaunchKernelGGL((wos_walk_kernel<D, G>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, stride,  \
@@ -196,38 +156,6 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
     if (sc.geom_global) WOS_LAUNCH_WALK(3, true); else WOS_LAUNCH_WALK(3, false);
   }
 #undef WOS_LAUNCH_WALK
-  return hipGetLastError();
-}
-
-// two-phase walks: the first step of every task, the survivors in cost order, the rest
-hipError_t launch_walks_two_phase(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
-                                  int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
-                                  size_t shmem, int geom_floats, hipStream_t s) {
-  if (prm.robust)
-    return launch_walks_two_phase_rb(dim, sc, prm, tk, base, stride, counters, tqueue, grid, shmem, geom_floats, s);
-  hipError_t e = hipMemsetAsync(tk.shist, 0, (2 * kCostBuckets + 1) * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-#define WOS_LAUNCH_FIRST(D, G)                                                                                  \
-  hipLaunchKernelGGL((wos_walk_first_kernel<D, G, false>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, base, \
-                     stride, counters, geom_floats)
-#define WOS_LAUNCH_RESUME(D, G)                                                                                 \
-  hipLaunchKernelGGL((wos_walk_kernel<D, G, false, false, true>), dim3(grid), dim3(kBlock), shmem, s, sc, prm, tk, \
-                     base, stride, counters, tqueue, geom_floats)
-  if (dim == 2) {
-    if (sc.geom_global) WOS_LAUNCH_FIRST(2, true); else WOS_LAUNCH_FIRST(2, false);
-  } else {
-    if (sc.geom_global) WOS_LAUNCH_FIRST(3, true); else WOS_LAUNCH_FIRST(3, false);
-  }
-  hipLaunchKernelGGL(wos_surv_offsets_kernel<0>, dim3(1), dim3(64), 0, s, tk.shist);
-  const int sgrid = (int)((tk.T + 255) / 256);
-  if (sgrid > 0) hipLaunchKernelGGL(wos_surv_scatter_kernel<0>, dim3(sgrid), dim3(256), 0, s, tk);
-  if (dim == 2) {
-    if (sc.geom_global) WOS_LAUNCH_RESUME(2, true); else WOS_LAUNCH_RESUME(2, false);
-  } else {
-    if (sc.geom_global) WOS_LAUNCH_RESUME(3, true); else WOS_LAUNCH_RESUME(3, false);
-  }
-#undef WOS_LAUNCH_FIRST
-#undef WOS_LAUNCH_RESUME
   return hipGetLastError();
 }
 
@@ -249,17 +177,10 @@ size_t first_ball_wave_lds_bytes(int lhs_floats) {
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks, bool robust) {
-  if (robust) return occupancy_rb(which == 2 ? 3 : which, dim, geom_global, shmem, blocks);
-  if (which == 2)
-    return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, false, false, true>, kBlock, shmem)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, false, false, true>, kBlock, shmem);
-  if (which == 0) {
-    if (dim == 2)
-      return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, true>, kBlock, shmem)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2, false>, kBlock, shmem);
-    return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, true>, kBlock, shmem)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3, false>, kBlock, shmem);
-  }
+  if (robust) return occupancy_rb(which, dim, geom_global, shmem, blocks);
+  if (which == 0)
+    return dim == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<2>, kBlock, shmem)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_first_ball_kernel<3>, kBlock, shmem);
   if (dim == 2)
     return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, true>, kBlock, shmem)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, false>, kBlock, shmem);

@@ -7,37 +7,28 @@ namespace wos {
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlockHost = 4;
 constexpr int kNumCounters = 9;
-// at most this many chunks of points are in flight on concurrent streams (pipelines)
-constexpr int kMaxPipes = 4;
-// queue slots after the counters: per pipeline i, [kNumCounters + 2i] point queue,
-// [kNumCounters + 2i + 1] task queue
-constexpr int kNumCounterSlots = kNumCounters + 2 * kMaxPipes;
+// queue slots after the counters: [kNumCounters] point queue, [kNumCounters + 1] task queue
+constexpr int kNumCounterSlots = kNumCounters + 2;
 
+// the first balls of every estimated point (after launch_point_setup)
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
-                              unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                              bool pre, hipStream_t s);
-// presorted first balls (pre = true above): per-point setup, pstate + first-ball radius
-// + bucket histogram, before launch_lpt_order
+                              unsigned int* work, int grid, size_t shmem, int lhs_floats, hipStream_t s);
+// per-point setup: pstate + first-ball radius + bucket histogram, before launch_lpt_order
 hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               const DevTasks& tk, hipStream_t s);
-// bucket offsets + point permutation for the walk queue (after the first-ball kernel)
+// bucket offsets + point permutation for the walk queue
 hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s);
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                         int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid, size_t shmem,
                         int geom_floats, hipStream_t s);
-// two-phase walks (wos_walk_first_kernel + survivor order + the walk kernel in resume
-// mode), replacing launch_lpt_order + launch_walks
-hipError_t launch_walks_two_phase(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
-                                  int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
-                                  size_t shmem, int geom_floats, hipStream_t s);
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s);
-// per-wave LDS scratch of the first-ball kernel (after the staged geometry)
+// per-wave LDS scratch of the first-ball kernel
 size_t first_ball_wave_lds_bytes(int lhs_floats);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
-// which: 0 first-ball kernel, 1 walk kernel, 2 presorted first-ball kernel (the instantiation for LDS-staged or global geometry);
+// which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry);
 // robust: the robust-float instantiations (wos_robust.hip)
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks,
                                    bool robust = false);
@@ -61,14 +52,10 @@ hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const
 // the launchers above dispatch here when prm.robust is set
 hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                                  int64_t base, int64_t stride, const DevTasks& tk, unsigned long long* counters,
-                                 unsigned int* work, int grid, size_t shmem, int geom_floats, int lhs_floats,
-                                 bool pre, hipStream_t s);
+                                 unsigned int* work, int grid, size_t shmem, int lhs_floats, hipStream_t s);
 hipError_t launch_walks_rb(int dim, bool bstart, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                            int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                            size_t shmem, int geom_floats, hipStream_t s);
-hipError_t launch_walks_two_phase_rb(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk,
-                                     int64_t base, int64_t stride, unsigned long long* counters, unsigned int* tqueue,
-                                     int grid, size_t shmem, int geom_floats, hipStream_t s);
-// which: 0 first-ball, 1 walk, 2 boundary-start walk, 3 presorted first-ball
+// which: 0 first-ball, 1 walk, 2 boundary-start walk
 hipError_t occupancy_rb(int which, int dim, bool geom_global, size_t shmem, int* blocks);
 }  // namespace wos

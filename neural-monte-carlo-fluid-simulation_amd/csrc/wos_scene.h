@@ -109,9 +109,7 @@ struct DevParams {
   int32_t ignore_neumann;
   int32_t ignore_source;
   int32_t robust;           // wos_solver_params.robust_float (Gfn::scaled)
-  int32_t fb_order;         // presorted first balls: 0 point order, 1 walk-queue order, 2 reversed
   int32_t neumann_inert;    // 1: no ball can reach the float-overflow regime (walk kernel without the Neumann term)
-  int32_t tail_fold;        // 1: walk-kernel waves with nothing left to walk fold finished points (no fold kernel)
   uint64_t seed;
   // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
   // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the
@@ -121,16 +119,11 @@ struct DevParams {
   // certain-reject bounds of the Yukawa rejection threshold by bin of s = mu R
   // (wos_host_scene.h rejection_bound_table), kRejTabBins floats; nullptr: none
   const float* rej_tab;
-  // two-sided envelope of the accept threshold, [2D | 3D][kRejTabBins][kRejEnvX][hi, lo]
-  // (wos_host_scene.h rejection_envelope_table); nullptr: none
-  const float* rej_env;
 };
 
 // bins of the rejection bound table: bin = floor(kRejTabScale * sqrt(mu R))
 constexpr int kRejTabBins = 96;
 constexpr float kRejTabScale = 8.0f;
-// x-bins of the two-sided rejection envelope (wos_host_scene.h rejection_envelope_table)
-constexpr int kRejEnvX = 32;
 
 // Walk-task workspace of one batch of points, SoA over T = n_points * wpp tasks
 // (task t = point * wpp + pair * n_anti + member).  Written by the first-ball
@@ -158,36 +151,10 @@ struct DevTasks {
   float* n0;
   float* r0;
   uint32_t* sflags;
-  // Two-phase walks (wos_walk_first_kernel, then the walk kernel in resume mode): the
-  // walks still running after their first walk-kernel step keep pt / thr / tsrc / dd
-  // in the arrays above and the rest of their state here; code[t] = kInFlight marks
-  // them until they finish.  surv lists them in walk-queue order (cost buckets
-  // descending, shist = [bucket counts | bucket offsets | total]).
-  uint64_t* rrng;    // [T] walk stream state
-  float* rn;         // [DIM][T] current normal
-  float* rpd;        // [DIM][T] previous direction
-  float* rpdist;     // [T] previous distance
-  float* rtn;        // [T] Neumann total
-  uint32_t* rwl;     // [T] walkLength | onNeumann << 31
-  uint32_t* rsteps;  // [T] ball steps so far
-  uint32_t* surv;    // [T] survivor task indices
-  // In-kernel fold (DevParams::tail_fold): walks finished per point (pdone, [n], aliases
-  // prad, which only the first-ball kernel reads), the queue of points whose walks have
-  // all finished (rq, [n], 0xFFFFFFFF until written), its cursors rqc = [tail, head],
-  // and the fold's outputs (wos_fold_kernel's arguments).
-  uint32_t* pdone;
-  uint32_t* rq;
-  uint32_t* rqc;
-  float* p_out;
-  float* g_out;
-  int32_t* nest_out;
-  int32_t* steps_out;
-  uint32_t* shist;   // [2 * kCostBuckets + 1]
 };
 
-constexpr uint32_t kInFlight = 0xFFFFFFFFu;
-// floats per task: the record / start fields, then the two-phase state (rrng first, 8-B aligned)
-constexpr int task_floats(int dim) { return (3 * dim + 6) + (2 * dim + 7); }
+// floats per task: start state pt[DIM] thr tsrc dd, record first bdir[DIM] sdir[DIM] total code
+constexpr int task_floats(int dim) { return 3 * dim + 6; }
 constexpr int kCostBuckets = 32;
 
 }  // namespace wos

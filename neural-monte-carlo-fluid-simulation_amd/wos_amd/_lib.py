@@ -9,8 +9,9 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 6  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 7  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
+WOS_E_CAPACITY = -4
 WOS_PTRS_DEVICE = 0x1
 WOS_ASYNC = 0x2
 
@@ -56,7 +57,14 @@ class SolverParams(C.Structure):
         ("ignore_neumann", C.c_int32), ("ignore_source", C.c_int32),
         ("seed", C.c_uint64),
         ("robust_float", C.c_int32),
+        ("schedule", C.c_uint32),
     ]
+
+
+# wos_solver_params.schedule bits (include/wos.h): scheduling only, results bit-identical
+SCHED_GEOM_GLOBAL = 0x1
+SCHED_FULL_NEUMANN = 0x2
+SCHED_NO_STAR_GRID = 0x4
 
 
 class BvcParams(C.Structure):

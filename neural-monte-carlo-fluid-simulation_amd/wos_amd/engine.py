@@ -39,7 +39,7 @@ def _get_opt(d, key, default, typ):
     return typ(v)
 
 
-def solver_params(solver=None, output=None, seed=None):
+def solver_params(solver=None, output=None, seed=None, schedule=0):
     """Parse the reference's wost.json "solver" / "output" sections (demo.cpp:121-137,
     grid.h:159), same keys (including the misspelled `setps...`) and defaults."""
     s = dict(solver or {})
@@ -64,6 +64,8 @@ def solver_params(solver=None, output=None, seed=None):
     p.seed = int(seed if seed is not None else s.get("seed", _DEFAULT_SEED)) & 0xFFFFFFFFFFFFFFFF
     # extension key (no reference analogue): robust float semantics, SURVEY.md 7.2 hard part 4
     p.robust_float = int(bool(s.get("robustFloatSemantics", False)))
+    # GPU scheduling switches (_lib.SCHED_*): never change a result
+    p.schedule = int(schedule)
     return p
 
 
@@ -209,21 +211,26 @@ class WosScene:
             g = torch.empty(n, self.dim, dtype=torch.float32, device=x.device)
             ne = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
             sp = torch.empty(n, dtype=torch.int32, device=x.device) if counts else None
+            cur = torch.cuda.current_stream(x.device)
+            ts = None
             if stream is None:
-                s = torch.cuda.current_stream(x.device).cuda_stream
-            elif isinstance(stream, torch.cuda.Stream):
-                s = stream.cuda_stream
+                s = cur.cuda_stream
             else:
-                s = int(stream)
+                ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(int(stream),
+                                                                                                    device=x.device)
+                s = ts.cuda_stream
+                # the points and the fresh output buffers belong to torch's current stream:
+                # the solve on `stream` starts after the work queued there (the kernel that
+                # produced x, the allocator's last user of p / g)
+                ts.wait_stream(cur)
             flags = _lib.WOS_PTRS_DEVICE | (0 if sync else _lib.WOS_ASYNC)
             check(L.wos_solve(self._h, C.byref(params), x.data_ptr(), n, index_base, index_stride,
                               p.data_ptr(), g.data_ptr(), ne.data_ptr() if counts else None,
                               sp.data_ptr() if counts else None, C.byref(st), s, flags), "wos_solve")
-            if not sync and stream is not None:
+            if not sync and ts is not None:
                 # the buffers were allocated on torch's current stream but the enqueued
                 # solve uses them on `stream`: keep the caching allocator from handing
                 # their memory out again before that stream has finished with them
-                ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(s, device=x.device)
                 for t in (x, p, g, ne, sp):
                     if t is not None:
                         t.record_stream(ts)
@@ -266,8 +273,17 @@ class WosScene:
         if samples:
             cap = 2 * int(bvc.boundary_cache_size) + 4 * int(bvc.domain_cache_size) + 16
             buf = np.empty(cap * 8, np.float32)
-        check(L.wos_bvc(self._h, C.byref(params), C.byref(bvc), sol.ctypes.data, grad.ctypes.data,
-                        buf.ctypes.data if samples else None, cap, counts.ctypes.data, C.byref(st)), "wos_bvc")
+        rc = L.wos_bvc(self._h, C.byref(params), C.byref(bvc), sol.ctypes.data, grad.ctypes.data,
+                       buf.ctypes.data if samples else None, cap, counts.ctypes.data, C.byref(st))
+        if rc == _lib.WOS_E_CAPACITY and samples and int(counts[3]) > cap:
+            # the domain sampler keeps more candidates than the first guess (non-watertight
+            # scenes, small |signedVolume|): wos_bvc failed before the walks with the exact
+            # count in counts[3] -- retry once with a buffer of that size
+            cap = int(counts[3])
+            buf = np.empty(cap * 8, np.float32)
+            rc = L.wos_bvc(self._h, C.byref(params), C.byref(bvc), sol.ctypes.data, grad.ctypes.data,
+                           buf.ctypes.data, cap, counts.ctypes.data, C.byref(st))
+        check(rc, "wos_bvc")
         info = {"counts": {"boundary": int(counts[0]), "boundary_aligned": int(counts[1]), "domain": int(counts[2]),
                            "total": int(counts[3])}, "stats": st.as_dict()}
         if samples:

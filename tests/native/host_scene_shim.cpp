@@ -163,10 +163,6 @@ extern "C" int hs_star_grid_check(int dim, const float* v, int nv, const int* ix
 }
 
 // the rejection bound table of the kernels' certain-reject screen (wos_host_scene.h)
-extern "C" int hs_rej_env(int dim, float* out) {
-  wos::rejection_envelope_table(dim, out);
-  return wos::kRejTabBins * wos::kRejEnvX * 2;
-}
 
 extern "C" int hs_rej_table(int dim, float* out) {
   wos::rejection_bound_table(dim, out);

@@ -13,6 +13,7 @@ import pytest
 
 import objparse
 from wos_amd import WosScene, selftest_math, solver_params, workloads
+from wos_amd._lib import SCHED_GEOM_GLOBAL
 
 pytestmark = pytest.mark.gpu
 
@@ -87,10 +88,10 @@ def _pair(cfg, oracle, dim=2):
     return osc, sc
 
 
-def _compare(oracle, osc, sc, cfg, pts, seed=0x5EED0001):
+def _compare(oracle, osc, sc, cfg, pts, seed=0x5EED0001, schedule=0):
     prm_o = oracle.make_params(cfg["solver"], cfg["output"], seed=seed, math_mode=0)
     p0, g0, ne0, st0, s0 = oracle.solve(osc, prm_o, pts)
-    prm = solver_params(cfg["solver"], cfg["output"], seed=seed)
+    prm = solver_params(cfg["solver"], cfg["output"], seed=seed, schedule=schedule)
     p1, g1, s1, ne1, st1 = sc.solve(pts, prm, counts=True)
     np.testing.assert_array_equal(ne1, ne0)
     np.testing.assert_array_equal(st1, st0)
@@ -271,10 +272,9 @@ def test_karman_full_size_properties(gpu, oracle):
 
 
 @pytest.mark.parametrize("scene", ["karman", "gear", "cube", "dirichlet"])
-def test_geometry_from_global_memory_bit_exact(gpu, oracle, scene, monkeypatch):
-    """WOS_GEOM_GLOBAL=1: the kernels read the geometry records through L2 instead of
+def test_geometry_from_global_memory_bit_exact(gpu, oracle, scene):
+    """WOS_SCHED_GEOM_GLOBAL: the kernels read the geometry records through L2 instead of
     staging them in LDS (the path of scenes too large for LDS) -- same results."""
-    monkeypatch.setenv("WOS_GEOM_GLOBAL", "1")
     if scene == "karman":
         cfg = workloads.karman_config(n_walks=64)
         osc, sc = _pair(cfg, oracle)
@@ -294,7 +294,7 @@ def test_geometry_from_global_memory_bit_exact(gpu, oracle, scene, monkeypatch):
         osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
         sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], cfg["absorption"], **kw)
         pts = cfg["points"]
-    _, _, st = _compare(oracle, osc, sc, cfg, pts)
+    _, _, st = _compare(oracle, osc, sc, cfg, pts, schedule=SCHED_GEOM_GLOBAL)
     assert st["geom_global"] == 1
     sc.close()
 

@@ -201,22 +201,3 @@ def test_async_stats_two_streams_alternating(gpu):
         torch.cuda.synchronize()
         assert torch.equal(p, pw) and torch.equal(g, gw)
     sc.close()
-
-
-def test_async_stats_split_pipelines(gpu, monkeypatch):
-    """WOS_SPLIT=2: the chunks run on two pipelines (aux streams, their own boundary
-    events); stats and outputs equal a blocking unsplit solve."""
-    cfg, v, ix, pts = _cfg()
-    dev = torch.device("cuda", 0)
-    prm = solver_params(cfg["solver"], cfg["output"])
-    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
-    x = torch.from_numpy(np.ascontiguousarray(pts[:1500])).to(dev)
-    p_ref, g_ref, st_ref = sc.solve(x, prm)
-    monkeypatch.setenv("WOS_SPLIT", "2")
-    enq = [sc.solve(x, prm, sync=False) for _ in range(3)]
-    for p, g, st0 in enq:
-        st = sc.solve_stats(st0["ticket"])
-        _stats_equal(st, st_ref)
-        assert st["walk_launches"] >= 2
-        assert torch.equal(p, p_ref) and torch.equal(g, g_ref)
-    sc.close()

@@ -1,36 +1,28 @@
-"""The engine's performance switches change the schedule, never the result.
+"""The engine's scheduling switches change how a solve runs, never its result.
 
-Each switch below is read by wos_solve at every call (csrc/wos_capi.hip), so one
-process can solve the same points under every setting and compare p, grad p, the
-per-point walk counts and step counts bit for bit:
-* WOS_FB_SORT      presorted first balls (point-setup kernel + queue order first) vs
-                   the setup inside the first-ball kernel;
-* WOS_FB_ORDER     the presorted first-ball queue order (point / walk-queue / reversed);
-* WOS_NEUMANN_INERT the walk kernel without the Neumann term's code for scenes that
-                   cannot reach the float-overflow regime vs the full kernel;
-* WOS_TAIL_FOLD    the statistics folded inside the walk kernel by its idle waves vs
-                   the separate fold kernel.
-Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance),
-the Dirichlet obstacle (stored distance) and the cube (3D)."""
-import os
-
+wos_solver_params.schedule (include/wos.h WOS_SCHED_*) selects, per solve:
+* WOS_SCHED_GEOM_GLOBAL  geometry records read through L2 (the path of scenes too large
+                         for LDS) instead of staged in LDS;
+* WOS_SCHED_FULL_NEUMANN the walk kernel with the Neumann term's code even where the
+                         term is provably +0 (the "Neumann-inert" instantiation is the
+                         default for such scenes);
+* WOS_SCHED_NO_STAR_GRID the cooperative silhouette-group scan alone, without the
+                         star-radius cell grid.
+One process solves the same points with every bit off (the default) and on, alone and
+combined, and compares p, grad p, the per-point walk counts and step counts bit for bit.
+Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance), the
+Dirichlet obstacle (stored distance) and the cube (3D)."""
 import numpy as np
 import pytest
 
 import objparse
 from wos_amd import WosScene, solver_params, workloads
+from wos_amd._lib import SCHED_FULL_NEUMANN, SCHED_GEOM_GLOBAL, SCHED_NO_STAR_GRID
 
 pytestmark = pytest.mark.gpu
 
-SETTINGS = [
-    {},
-    {"WOS_FB_SORT": "0"},
-    {"WOS_FB_ORDER": "1"},
-    {"WOS_FB_ORDER": "2"},
-    {"WOS_NEUMANN_INERT": "0"},
-    {"WOS_FB_SORT": "0", "WOS_NEUMANN_INERT": "0"},
-    {"WOS_TAIL_FOLD": "0"},
-]
+SETTINGS = [0, SCHED_GEOM_GLOBAL, SCHED_FULL_NEUMANN, SCHED_NO_STAR_GRID,
+            SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID]
 
 
 def _scenes():
@@ -51,26 +43,18 @@ def _scenes():
 @pytest.mark.parametrize("name,cfg,make,pts", _scenes(), ids=["karman", "dirichlet", "cube"])
 def test_switches_are_bit_identical(gpu, name, cfg, make, pts):
     sc = make()
-    prm = solver_params(cfg["solver"], cfg["output"])
     ref = None
-    saved = {k: os.environ.get(k) for s in SETTINGS for k in s}
-    try:
-        for setting in SETTINGS:
-            for k in saved:
-                os.environ.pop(k, None)
-            os.environ.update(setting)
-            p, g, _, n_est, steps = sc.solve(np.ascontiguousarray(pts, np.float32), prm, counts=True)
-            out = [np.asarray(p).view(np.uint32), np.asarray(g).view(np.uint32), np.asarray(n_est),
-                   np.asarray(steps)]
-            if ref is None:
-                ref = out
-                assert np.isfinite(np.asarray(p)).all()
-                continue
-            for a, b in zip(ref, out):
-                assert np.array_equal(a, b), setting
-    finally:
-        for k, v in saved.items():
-            os.environ.pop(k, None)
-            if v is not None:
-                os.environ[k] = v
-        sc.close()
+    for sched in SETTINGS:
+        prm = solver_params(cfg["solver"], cfg["output"], schedule=sched)
+        p, g, st, n_est, steps = sc.solve(np.ascontiguousarray(pts, np.float32), prm, counts=True)
+        assert st["geom_global"] == (1 if sched & SCHED_GEOM_GLOBAL else 0)
+        if sched & SCHED_NO_STAR_GRID:
+            assert st["star_grid"] == 0
+        out = [np.asarray(p).view(np.uint32), np.asarray(g).view(np.uint32), np.asarray(n_est), np.asarray(steps)]
+        if ref is None:
+            ref = out
+            assert np.isfinite(np.asarray(p)).all()
+            continue
+        for a, b in zip(ref, out):
+            assert np.array_equal(a, b), sched
+    sc.close()

@@ -160,102 +160,3 @@ def test_tabulated_bound_dominates_exact_threshold(rej_table, dim, lam):
     # the subtracted term); near the closed form for large mu R, where the kernel
     # keeps the smaller of the two
     assert tighter and min(tighter) < 0.01
-
-
-@pytest.fixture(scope="module")
-def rej_env(tmp_path_factory):
-    out = str(tmp_path_factory.mktemp("re") / "libhs.so")
-    subprocess.run(["g++", "-std=c++17", "-O1", "-fPIC", "-shared", "-ffp-contract=off", "-I", CSRC,
-                    os.path.join(HERE, "native", "host_scene_shim.cpp"), os.path.join(CSRC, "wos_host_scene.cpp"),
-                    os.path.join(CSRC, "wos_fcpw_bvh.cpp"),
-                    "-o", out], check=True)
-    lib = C.CDLL(out)
-    envs = {}
-    for dim in (2, 3):
-        t = np.zeros(96 * 32 * 2, np.float32)
-        n = lib.hs_rej_env(dim, t.ctypes.data_as(C.POINTER(C.c_float)))
-        envs[dim] = t[:n].reshape(96, 32, 2).copy()
-    return envs
-
-
-@pytest.mark.parametrize("dim", [2, 3])
-@pytest.mark.parametrize("lam", [50.0, 350.0, 2000.0])
-def test_envelope_brackets_exact_threshold(rej_env, dim, lam):
-    """the two-sided envelope of the kernel's rejection test (rejection_envelope_table):
-    for every ball and radius draw x, lo R / (norm bound) <= T(x) <= hi R / (norm bound),
-    with T evaluated in the kernel's float/double steps -- so u above hi is the exact
-    test's reject and u below lo its accept; and it decides most draws"""
-    env = rej_env[dim]
-    rng = np.random.default_rng(23 + dim)
-    radii = np.concatenate([np.exp(rng.uniform(np.log(2e-3), np.log(3.0), 36)), [1e-3, 0.02, 0.05, 0.5, 2.0]])
-    undecided = []
-    for R in radii.astype(np.float32):
-        xs = np.unique(np.concatenate([np.linspace(1e-4, 0.99999, 700), rng.uniform(0, 1, 300),
-                                       (np.arange(32) / 32.0), (np.arange(1, 32) / 32.0) - 1e-7]))
-        xs = xs[(xs > 0) & (xs < 1.0)].astype(np.float32)
-        T, q, (muR, inv_nb) = (_thresholds_2d if dim == 2 else _thresholds_3d)(f32(R), f32(lam), xs)
-        if dim == 2 and not muR < 80:   # the 2D envelope is used on the fast path only (mu R < 80)
-            continue
-        k = int(f32(8.0) * f32(np.sqrt(f32(muR))))
-        if k == 0 or k >= 96 or not (inv_nb > 0 and np.isfinite(inv_nb)):
-            continue
-        c = f32(R * inv_nb)
-        j = (xs * f32(32.0)).astype(np.int32)
-        hi = (env[k, j, 0] * c).astype(np.float32)
-        lo = (env[k, j, 1] * c).astype(np.float32)
-        ok = np.isfinite(T)
-        assert (T[ok] <= hi[ok]).all(), (dim, lam, float(R), float((T - hi)[ok].max()))
-        assert (T[ok] >= lo[ok]).all(), (dim, lam, float(R), float((lo - T)[ok].max()))
-        undecided.append(float(np.mean(np.minimum(hi, min(float(q), 1.0)) - np.minimum(lo, min(float(q), 1.0)))))
-    # the draws the exact path still has to decide: a few percent of the items
-    assert undecided and np.mean(undecided) < 0.12, np.mean(undecided)
-
-
-def _xbound(dim, R, lam, x, inv_nb):
-    """rej_xbound_reject's bound in numpy float32 (the kernel: exp2f / sqrtf hardware
-    approximations, ~1 ulp; the 0.1 % margin covers them): +inf where it is not used"""
-    sl = f32(np.sqrt(f32(lam)))
-    muR = f32(R * sl)
-    if dim == 2:
-        xb = f32(f32(np.sqrt(f32(f32(f32(1.57079637) * R) / sl))) * inv_nb)
-    else:
-        xb = f32(R * inv_nb)
-    z = (x * muR).astype(np.float32)
-    e = np.exp2(z * f32(-1.44269502)).astype(np.float32)
-    shape = np.sqrt(x).astype(np.float32) if dim == 2 else x
-    b = (xb * shape * e).astype(np.float32) * f32(1.001) + f32(1e-6) * f32(R * inv_nb)
-    return np.where(z < 80.0, b, np.inf)
-
-
-@pytest.mark.parametrize("dim", [2, 3])
-@pytest.mark.parametrize("lam", [50.0, 350.0, 2000.0])
-def test_x_bound_dominates_exact_threshold(dim, lam):
-    """the x-dependent certain-reject bound of the cooperative sampler (rej_xbound_reject:
-    2D x R K0(mu x R) < sqrt(pi x R / 2 mu) e^{-mu x R}, 3D x R e^{-mu x R}) is above the
-    exact threshold at every radius draw, and rejects most of the draws the exact test
-    rejects"""
-    rng = np.random.default_rng(31 + dim)
-    radii = np.concatenate([np.exp(rng.uniform(np.log(1e-4), np.log(3.0), 40)), [1e-3, 0.02, 0.05, 0.5, 2.0]])
-    caught = []
-    for R in radii.astype(np.float32):
-        mu = np.sqrt(lam)
-        peak = min(1.0, 0.6 / (mu * float(R)))
-        xs = np.unique(np.concatenate([np.linspace(1e-5, 1.0, 600), rng.uniform(0, 1, 300),
-                                       peak * np.linspace(0.3, 1.7, 141)]))
-        xs = xs[(xs > 0) & (xs <= 1.0)].astype(np.float32)
-        T, q, (muR, inv_nb) = (_thresholds_2d if dim == 2 else _thresholds_3d)(f32(R), f32(lam), xs)
-        if dim == 2 and not muR < 80:   # the 2D sampler is cooperative on the fast path only
-            continue
-        if not (inv_nb > 0 and np.isfinite(inv_nb)):
-            continue
-        B = _xbound(dim, f32(R), f32(lam), xs, inv_nb)
-        ok = np.isfinite(T)
-        assert (T[ok] <= B[ok]).all(), (dim, lam, float(R), float((T - B)[ok].max()))
-        # fraction of the u-interval above T that the bound resolves (u uniform on [0, min(q, 1)))
-        top = min(float(q), 1.0)
-        Tc, Bc = np.clip(T[ok], 0, top), np.clip(B[ok], 0, top)
-        if top - Tc.mean() > 0 and muR > 2.0:
-            caught.append(float(np.mean(top - Bc) / np.mean(top - Tc)))
-    # useful once mu R >~ 2 (karman's balls: mu R ~ 2-20); for small balls the table
-    # bound q is the tighter one
-    assert caught and np.mean(caught) > 0.6, caught

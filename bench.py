@@ -15,6 +15,10 @@ RNG is keyed by the global point index so results do not depend on N.
 Scaling: "weak" (default for B) gives every rank one 64k-point batch of an
 N x 64k projection; "strong" (default for the grid configs C, D, E -- BASELINE's
 8-GPU configs are fixed-size problems) shards the config's fixed point set.
+Config B's line carries both views: `value` (weak) and a `strong` object (the fixed
+65398-point projection stride-sharded over the N ranks + its all-gather); at N=1 it
+also times `strong_shard_ms`, the 1/8 stride shard rank 0 of an 8-GPU strong run
+solves, alone on this GPU (the per-rank latency that bounds 8-GPU strong scaling).
 
 Prints ONE JSON line on rank 0.  `value` counts the ball steps of recorded walks
 (the first ball + every walk() iteration, walk_on_stars.h:523,182); steps of
@@ -53,6 +57,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-projection-wall", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the product path); gloo stages the all-gather through host "
+                         "memory and lets N ranks share one GPU (tests/test_bench_dist.py)")
     ap.add_argument("--blocking", action="store_true",
                     help="wait for every solve before enqueueing the next (default: the next projection is "
                          "enqueued while the previous one runs; its stats are read after)")
@@ -169,6 +176,110 @@ def cpu_baseline(cfg, n_threads, budget_s):
     }
 
 
+def make_gather(world, dist, n_local, n_pad, dim, dev, torch):
+    """The one all-gather of [p, grad] per projection: every rank sends its shard
+    padded to n_pad rows into a (world * n_pad, 1 + dim) buffer.  With the gloo
+    backend (CPU-only rehearsal of the N-rank path, tests/test_bench_dist.py) the
+    payload is staged through host memory; with nccl (RCCL) it stays in HBM."""
+    if world == 1:
+        return None
+    staged = dist.get_backend() == "gloo" and dev.type != "cpu"
+    bdev = torch.device("cpu") if staged else dev
+    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=bdev)
+    buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=bdev)
+
+    def gather(p, g):
+        send[:n_local, 0] = p.to(bdev)
+        send[:n_local, 1:] = g.to(bdev)
+        dist.all_gather_into_tensor(buf, send)
+
+    gather.buf = buf
+    return gather
+
+
+def timed_projections(scene, x, params, base, stride, steps, warmup, blocking, world, dist, torch, gather=None):
+    """Time `steps` projections of the points `x` (global indices base + i * stride),
+    each followed by `gather(p, grad)` (the RCCL all-gather for N > 1), bracketed by a
+    barrier + device sync on both sides; returns (max-over-ranks seconds, per-solve
+    stats).  One projection stays in flight behind the one whose counters are read
+    (device counters, copied per solve; wos_solve_stats waits only for that solve)."""
+    sync = torch.cuda.synchronize if x.device.type == "cuda" else (lambda: None)
+
+    def step():
+        p, g, st = scene.solve(x, params, index_base=base, index_stride=stride, sync=blocking)
+        if gather is not None:
+            gather(p, g)
+        return st["ticket"]
+
+    for _ in range(warmup):
+        scene.solve_stats(step())
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    tickets, stats = [step()], []
+    for k in range(steps):
+        if k + 1 < steps:
+            tickets.append(step())
+        stats.append(scene.solve_stats(tickets[k]))
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=x.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, stats
+
+
+def reduce_steps(steps_rec, steps_all, world, dist, torch, dev):
+    """Whole-job step counts (sum over ranks)."""
+    if world == 1:
+        return float(steps_rec), float(steps_all)
+    t = torch.tensor([float(steps_rec), float(steps_all)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t[0].item()), float(t[1].item())
+
+
+def strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, workloads):
+    """Config B's fixed 65398-point projection stride-sharded over the N ranks (rank r
+    solves points r, r + N, ...) + the one all-gather of [p, grad]: the strong-scaling
+    view of the same metric beside the weak `value` (at N = 1 it is the same workload
+    as the weak line)."""
+    pts = workloads.config_by_name("B")["points"]
+    n_all = pts.shape[0]
+    local = np.ascontiguousarray(pts[rank::world])
+    n_local = local.shape[0]
+    n_pad = (n_all + world - 1) // world
+    x = torch.from_numpy(local).to(dev)
+    gather = make_gather(world, dist, n_local, n_pad, dim, dev, torch)
+
+    elapsed, stats = timed_projections(scene, x, params, rank, world, a.steps, a.warmup, a.blocking,
+                                       world, dist, torch, gather)
+    rec, _ = reduce_steps(sum(s["walk_steps"] for s in stats),
+                              sum(s["walk_steps"] + s["wasted_steps"] for s in stats), world, dist, torch, dev)
+    return {"points": n_all, "n_gpus": world, "value": rec / elapsed, "unit": "walk-steps/s",
+            "ms_per_step": elapsed / a.steps * 1e3, "walk_steps_per_projection": rec / a.steps,
+            "kernel_ms_rank0": float(np.mean([s["kernel_ms"] for s in stats])),
+            "note": "fixed point set (total work fixed as N grows), stride-sharded, + 1 RCCL all-gather"}
+
+
+def shard_projection(a, scene, params, dim, torch, dev, workloads, shards=8):
+    """One GPU timing the 1/8 stride shard an 8-GPU strong-scaled projection of config B
+    gives rank 0 (points 0, 8, 16, ... with their global RNG indices): the per-rank
+    latency floor that bounds 8-GPU strong scaling."""
+    pts = workloads.config_by_name("B")["points"]
+    x = torch.from_numpy(np.ascontiguousarray(pts[0::shards])).to(dev)
+    elapsed, stats = timed_projections(scene, x, params, 0, shards, a.steps, a.warmup, a.blocking,
+                                       1, None, torch)
+    return {"shards": shards, "shard_points": int(x.shape[0]), "ms": elapsed / a.steps * 1e3,
+            "kernel_ms": float(np.mean([s["kernel_ms"] for s in stats])),
+            "walk_ms": float(np.mean([s["walk_ms"] for s in stats]))}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -180,17 +291,21 @@ def main():
     import torch
     import torch.distributed as dist
     from wos_amd import WosScene, solver_params, workloads
+    # one rank per GPU; more ranks than GPUs (the gloo rehearsal on a 1-GPU box) share them
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev)
 
     cfg = workloads.config_by_name(a.config, n_points=a.points * world if scaling == "weak" else None)
     pts_all = cfg["points"]
     n_all = pts_all.shape[0]
     dim = cfg["dim"]
     scene = WosScene(cfg["vertices"], cfg["prims"], torch.from_numpy(cfg["source"]).to(dev), cfg["absorption"],
-                     watertight=True, device=local_rank, **cfg["scene_kw"])
+                     watertight=True, device=dev.index, **cfg["scene_kw"])
     info = scene.info()
     params = solver_params(cfg["solver"], cfg["output"])
 
@@ -199,34 +314,13 @@ def main():
     n_local = local.shape[0]
     n_pad = (n_all + world - 1) // world
     x = torch.from_numpy(local).to(dev)
-    gather_buf = torch.empty(world, n_pad, 1 + dim, dtype=torch.float32, device=dev)
-    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=dev)
+    gather = make_gather(world, dist, n_local, n_pad, dim, dev, torch)
 
-    def step():
-        """Enqueue one projection (+ the all-gather); returns its stats ticket."""
-        p, g, st = scene.solve(x, params, index_base=rank, index_stride=world, sync=a.blocking)
-        if world > 1:
-            send[:n_local, 0] = p
-            send[:n_local, 1:] = g
-            dist.all_gather_into_tensor(gather_buf, send)
-        return st["ticket"]
-
-    for _ in range(a.warmup):
-        scene.solve_stats(step())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    elapsed, stats = timed_projections(scene, x, params, rank, world, a.steps, a.warmup, a.blocking,
+                                       world, dist, torch, gather)
     steps_rec = steps_all = rej_iters = 0
     kernel_ms, walk_ms, fb_ms, fold_ms, walk_kernel_steps, launches = [], [], [], [], 0, 0
-    # one projection in flight behind the one whose counters are read (device counters,
-    # copied per solve; wos_solve_stats waits only for that solve)
-    tickets = [step()]
-    for k in range(a.steps):
-        if k + 1 < a.steps:
-            tickets.append(step())
-        st = scene.solve_stats(tickets[k])
+    for st in stats:
         steps_rec += st["walk_steps"]
         steps_all += st["walk_steps"] + st["wasted_steps"]
         rej_iters += st["rejection_iters"]
@@ -238,20 +332,13 @@ def main():
         # every walk has exactly one first-ball step (taken in wos_first_ball_kernel)
         n_walks_run = st["walks_recorded"] + st["walks_escaped"] + st["walks_max_length"]
         walk_kernel_steps += st["walk_steps"] + st["wasted_steps"] - n_walks_run
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    steps_rec, steps_all = reduce_steps(steps_rec, steps_all, world, dist, torch, dev)
 
-    tot = torch.tensor([elapsed, float(steps_rec), float(steps_all)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = tot[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        sums = tot[1:].clone()
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax.item())
-        steps_rec, steps_all = float(sums[0].item()), float(sums[1].item())
+    strong = shard = None
+    if a.config == "B" and scaling == "weak":
+        strong = strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, workloads)
+        if world == 1:
+            shard = shard_projection(a, scene, params, dim, torch, dev, workloads)
 
     if rank == 0:
         kms = float(np.mean(kernel_ms))
@@ -312,6 +399,14 @@ def main():
             "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
                                 "fold": float(np.mean(fold_ms)), "total": kms},
         }
+        if strong is not None:
+            line["strong"] = strong
+        if shard is not None:
+            full_ms = elapsed / a.steps * 1e3
+            line["strong_shard_ms"] = shard["ms"]
+            line["strong_shard"] = dict(shard, full_ms=full_ms, implied_8gpu_speedup=full_ms / shard["ms"],
+                                        note="rank 0's share of an 8-GPU strong-scaled config B projection, "
+                                             "timed alone on this GPU (all-gather excluded)")
         if sq:
             line["valu_issue"] = {"kernel": sq["kernel"], "frac": sq["valu_issue_frac"],
                                   "wait_any_frac": sq["wait_any_frac"], "wait_inst_frac": sq["wait_inst_frac"],

@@ -296,13 +296,18 @@ def _with_geometry(cfg, dim, flip=False):
 #   C  unit box + Dirichlet disk (synthetic), 512^2 points, 256 walks
 #   D  cube 3D, 128^3 points, 64 walks
 #   E  cube 3D, 256^3 points, 128 walks
-CONFIG_NAMES = ("A", "B", "B_grid", "C", "D", "E")
+CONFIG_NAMES = ("A", "A_robust", "B", "B_grid", "C", "D", "E")
 
 
 def config_by_name(name, n_points=None):
-    if name == "A":
+    if name in ("A", "A_robust"):
         cfg = _with_geometry(taylorgreen_config(n_walks=32, res=32, flip=True), 2, flip=True)
         desc = "taylorgreen2d (flipped square.obj), 32x32 cell-centred points, 32 walks, maxWalkLength 10000"
+        if name == "A_robust":
+            # the same config with robust float semantics (solver extension key): finite
+            # Yukawa members where the reference's overflow to NaN (SURVEY.md 7.2 part 4)
+            cfg["solver"] = dict(cfg["solver"], robustFloatSemantics=True)
+            desc += ", robust float semantics"
     elif name == "B":
         cfg = _with_geometry(karman_config(n_walks=128, n_points=n_points or 65536), 2)
         desc = (f"karman2d: geometry_1cyl_long_open.obj, lambda=350, RR 0.99, {cfg['points'].shape[0]} random "

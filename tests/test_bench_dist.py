@@ -1,0 +1,122 @@
+"""bench.py's N-rank path (world_size 2, gloo): the timing helpers, the padded
+all-gather and the strong (fixed point set) line beside the weak one.
+
+CPU: the helpers run with a stand-in scene whose "solution" is the global point
+index, so the gathered buffer shows which point every row came from.  GPU: bench.py
+itself under torch.distributed.run, two ranks sharing GPU 0 over gloo, HIP engine.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from test_distributed import _free_port
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _IndexScene:
+    """solve() returns p = global index, grad = (index, -index); stats count points."""
+
+    def __init__(self):
+        self.pending = {}
+        self.next = 0
+
+    def solve(self, x, params, index_base=0, index_stride=1, sync=False):
+        import torch
+        idx = index_base + index_stride * torch.arange(x.shape[0], dtype=torch.float64)
+        p = idx.float()
+        g = torch.stack([p, -p], 1)
+        t = self.next
+        self.next += 1
+        self.pending[t] = {"walk_steps": int(x.shape[0]) * 3, "wasted_steps": 1, "kernel_ms": 1.0}
+        return p, g, {"ticket": t}
+
+    def solve_stats(self, ticket):
+        return self.pending.pop(ticket)
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "neural-monte-carlo-fluid-simulation_amd"))
+    import torch
+    import torch.distributed as dist
+    import bench
+    from wos_amd import workloads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+    n_all = 1001
+    pts = np.zeros((n_all, 2), np.float32)
+    local = pts[rank::world]
+    n_pad = (n_all + world - 1) // world
+    gather = bench.make_gather(world, dist, local.shape[0], n_pad, 2, dev, torch)
+    scene = _IndexScene()
+    el, stats = bench.timed_projections(scene, torch.from_numpy(local), None, rank, world, 4, 1, False,
+                                        world, dist, torch, gather)
+    assert len(stats) == 4 and el > 0 and not scene.pending
+
+    class A:
+        steps, warmup, blocking = 3, 1, False
+    strong = bench.strong_projection(A, _IndexScene(), None, world, rank, 2, dist, torch, dev, workloads)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), buf=gather.buf.numpy(), n_pad=n_pad,
+             strong=json.dumps(strong))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_gather_and_strong_line(tmp_path, world):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True, start_method="spawn")
+    n_all = 1001
+    for r in range(world):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        n_pad = int(d["n_pad"])
+        buf = d["buf"].reshape(world, n_pad, 3)
+        got = np.concatenate([buf[q, :len(range(q, n_all, world)), 0] for q in range(world)])
+        assert sorted(got.astype(np.int64).tolist()) == list(range(n_all))
+        for q in range(world):
+            rows = buf[q, :len(range(q, n_all, world))]
+            np.testing.assert_array_equal(rows[:, 0], np.arange(q, n_all, world, dtype=np.float32))
+            np.testing.assert_array_equal(rows[:, 2], -rows[:, 1])
+        s = json.loads(str(d["strong"]))
+        # fixed config-B point set; whole-job step count = 3 per point (sum over ranks)
+        assert s["points"] == 65398 and s["n_gpus"] == world
+        assert s["walk_steps_per_projection"] == 3 * 65398
+        assert s["value"] > 0 and s["ms_per_step"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_hip_engine(tmp_path, gpu):
+    """bench.py --gpus 2 over gloo with both ranks on GPU 0: one JSON line with the
+    weak value and the strong object, whose step count equals a one-process engine
+    solve of the same fixed point set (RNG keyed by global index, so sharding does
+    not change the work)."""
+    import torch
+    from wos_amd import WosScene, solver_params, workloads
+    out = tmp_path / "bench.json"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--points", "8192", "--dist-backend", "gloo",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    out.write_text(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["config"]["points"] > 16000
+    s = line["strong"]
+    assert s["points"] == 65398 and s["n_gpus"] == 2 and s["value"] > 0
+    cfg = workloads.config_by_name("B")
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0, watertight=True)
+    _, _, st = sc.solve(cfg["points"], solver_params(cfg["solver"], cfg["output"]))
+    sc.close()
+    assert s["walk_steps_per_projection"] == st["walk_steps"]

@@ -48,7 +48,10 @@ __device__ __forceinline__ void wave_sync() {
 // (s_memtime) and lane-packing counters of the walk kernel.
 enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, D_SCALLS, D_SGVISIT, D_SCAND, D_SEXACT,
        D_FB_PTS, D_FB_SETUP, D_FB_LHS, D_FB_BALLS, D_FB_TOTAL, D_FB_MAX, D_WMAXLEN, D_WAVEMAX, D_RCALLS, D_RGENS, D_RITEMS, D_RQUICK, D_RUND, D_RLANES, D_MID, D_END, D_TAIL,
-       D_XITERS, D_XLANES, D_XLOOP, D_NUM };  // X: iterations after the wave's task queue ran dry
+       D_XITERS, D_XLANES, D_XLOOP,
+       // the same sections over iterations with <= 2 live lanes (a lone walk's critical path)
+       D_L_ITERS, D_L_STEP, D_L_STAR, D_L_MID, D_L_RAY, D_L_END, D_L_SAMPLE, D_L_TAIL, D_L_LOOP,
+       D_L_S_CELL, D_L_S_PFX, D_L_S_WIN, D_L_S_FIN, D_L_S_BUILD, D_L_S_PRE, D_L_S_POST, D_NUM };  // X: iterations after the wave's task queue ran dry
 // slots holding maxima (folded with atomicMax)
 __host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 static __device__ unsigned long long g_diag[D_NUM];
@@ -69,12 +72,30 @@ static __shared__ unsigned long long s_diag[D_NUM];
     if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
       atomicAdd(&s_diag[slot], n_);                                                    \
   } while (0)
+#define DIAG_ADD_LONE(slot, lslot, v, lone)                                            \
+  do {                                                                                 \
+    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - (v);                           \
+    if ((int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) { \
+      atomicAdd(&s_diag[slot], (unsigned long long)dt_);                               \
+      if (lone) atomicAdd(&s_diag[lslot], (unsigned long long)dt_);                    \
+    }                                                                                  \
+  } while (0)
+#define DIAG_LONE(v, pred) const bool v = __popcll(__ballot(pred)) <= 2
+#define DIAG_ADD_IF(slot, v, cond)                                                     \
+  do {                                                                                 \
+    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - (v);                           \
+    if ((cond) && (int)(threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63))) \
+      atomicAdd(&s_diag[slot], (unsigned long long)dt_);                               \
+  } while (0)
 #define DIAG_LANE(slot) atomicAdd(&s_diag[slot], 1ull)
 #define DIAG_MAX(slot, v) atomicMax(&s_diag[slot], (unsigned long long)(v))
 #else
 #define DIAG_T0(v)
 #define DIAG_ADD(slot, v)
 #define DIAG_COUNT(slot, n)
+#define DIAG_ADD_LONE(slot, lslot, v, lone)
+#define DIAG_LONE(v, pred)
+#define DIAG_ADD_IF(slot, v, cond)
 #define DIAG_LANE(slot)
 #define DIAG_MAX(slot, v)
 #endif
@@ -824,6 +845,11 @@ __device__ __forceinline__ float k1_fast(float x);
 #ifndef WOS_PK_REUSE
 #define WOS_PK_REUSE 0
 #endif
+// 1: a walk step's source texel is consumed at the next step (or when the walk ends),
+// so its global load overlaps the next step's queries instead of stalling the tail
+#ifndef WOS_DEFER_TEXEL
+#define WOS_DEFER_TEXEL 1
+#endif
 // ---------------------------------------------------------------------------
 // Robust float semantics (Gfn::yukawa == kYukScaled): the reference's Yukawa members
 // rewritten with exponentially scaled Bessels (bessel_scaled) and e^{2(mu r - mu R)} <= 1,
@@ -1252,6 +1278,16 @@ __device__ __forceinline__ void k0i0_fast(float x, float* k0, float* i0) {
 #ifndef WOS_QUICK_REJ
 #define WOS_QUICK_REJ 1
 #endif
+// the rejection bound table (both dimensions) in LDS: read on every sampler call,
+// one global round trip less on a walk step's critical path (WOS_REJ_TAB_LDS)
+#ifndef WOS_REJ_TAB_LDS
+#define WOS_REJ_TAB_LDS 1
+#endif
+static __shared__ float s_rej_tab[WOS_REJ_TAB_LDS ? 2 * kRejTabBins : 1];
+__device__ __forceinline__ float rej_tab_at(int i, const DevParams& prm) {
+  return WOS_REJ_TAB_LDS ? s_rej_tab[i] : prm.rej_tab[i];
+}
+
 template <int DIM>
 __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, float muR, float sqrtL, float invNB) {
   if (!WOS_QUICK_REJ) return 3.0e38f;
@@ -1260,7 +1296,8 @@ __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, 
   if (prm.rej_tab != nullptr && muR >= 0.0f) {
     const int k = (int)(kRejTabScale * __builtin_sqrtf(muR));
     if (k < kRejTabBins) {
-      const float qt = R * prm.rej_tab[(DIM == 3 ? kRejTabBins : 0) + k] * invNB;
+      // staged in LDS by stage_rej_jump (every kernel that samples)
+      const float qt = R * rej_tab_at((DIM == 3 ? kRejTabBins : 0) + k, prm) * invNB;
       q = qt < q ? qt : q;
     }
   }
@@ -1383,6 +1420,8 @@ static __shared__ unsigned long long s_rej_jump[2 * kRejJumpLds];
 
 __device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
   for (int i = threadIdx.x; i < 2 * kRejJumpLds; i += blockDim.x) s_rej_jump[i] = prm.jump[4 * (i >> 1) + (i & 1)];
+  if (WOS_REJ_TAB_LDS && prm.rej_tab != nullptr)
+    for (int i = threadIdx.x; i < 2 * kRejTabBins; i += blockDim.x) s_rej_tab[i] = prm.rej_tab[i];
 }
 
 // stream state before rejection iteration j (draw 2j) from stream start s0
@@ -1626,7 +1665,26 @@ struct WalkState {
   bool onNeumann;
   int walkLength;
   float totalNeumann, totalSource;
+#if WOS_DEFER_TEXEL
+  // the source contribution of the last step, added once its texel has arrived:
+  // totalSource += pThr * (pNrm * pTex) in the reference's order (walk_on_stars.h:270-275)
+  float pThr, pNrm, pTex;
+  bool pend;
+#endif
 };
+
+// Fold a deferred source contribution into totalSource (a no-op without one)
+template <int DIM>
+__device__ __forceinline__ void flush_source(WalkState<DIM>& st) {
+#if WOS_DEFER_TEXEL
+  if (st.pend) {
+    st.totalSource += st.pThr * (st.pNrm * st.pTex);
+    st.pend = false;
+  }
+#else
+  (void)st;
+#endif
+}
 
 template <int DIM>
 __device__ __forceinline__ float prim_area(const float* P) {
@@ -1862,10 +1920,20 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
                                               Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, const float* dir,
                                               bool hit, const Hit& ip, const float* sp) {
   if (!prm.ignore_source) {
+#if WOS_DEFER_TEXEL
+    flush_source<DIM>(st);
+    if (g.r <= ip.d) {
+      st.pNrm = g.norm();
+      st.pThr = st.throughput;
+      st.pTex = source_value<DIM>(sc, sp);
+      st.pend = true;
+    }
+#else
     if (g.r <= ip.d) {
       float contrib = g.norm() * source_value<DIM>(sc, sp);
       st.totalSource += st.throughput * contrib;
     }
+#endif
   }
   if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
   st.prevDist = ip.d;
@@ -2043,6 +2111,11 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
 // union of every lane's groups) become ~(total work)/64 wave iterations.
 // ---------------------------------------------------------------------------
 constexpr int kStarChunk = 16;  // groups per compaction round: at most 64 * 16 list entries
+// 1: the star query's cell lists are copied to the wave list 16 entries per LDS round
+// trip (dword reads + alignbyte) instead of one byte read per entry
+#ifndef WOS_STAR_BATCH
+#define WOS_STAR_BATCH 1
+#endif
 
 template <int DIM>
 struct StarLDS {
@@ -2131,6 +2204,7 @@ template <int DIM, bool TREE = false>
 __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene& sc, const DevParams& prm,
                                                   bool query, const float* x, float maxR, bool flipOrient,
                                                   StarLDS<DIM>* L, int lane) {
+  DIAG_T0(t_sp);
   const float minR = prm.min_star_radius, prec = prm.silhouette_precision;
   float result = 0.0f, r2 = 0.0f, minR2 = 0.0f;
   bool need = false;
@@ -2148,6 +2222,9 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
   }
   // lanes inside the star grid take their cell's short candidate list; the rest
   // (no grid, outside it) share the wave-cooperative group scan below
+  DIAG_LONE(lone, query);
+  DIAG_ADD_IF(D_L_S_PRE, t_sp, lone);
+  DIAG_T0(t_s0);
   int c_beg = 0, c_end = 0;
   bool use_cell = false;
   if (need && G.sgrid != nullptr) {
@@ -2168,6 +2245,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     L->brk[lane] = 0xFFFFFFFFu;
     L->best[lane] = ~0ull;
   }
+  DIAG_ADD_IF(D_L_S_CELL, t_s0, lone);
+  DIAG_T0(t_s1);
   if (__ballot(use_cell) != 0) {
     // the (lane, candidate) pairs of all cell lists, spread over the wave in windows
     // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
@@ -2181,13 +2260,42 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     }
     const uint32_t total = __shfl(incl, kWave - 1);
     const uint32_t first = incl - cnt;
+    DIAG_ADD_IF(D_L_S_PFX, t_s1, lone);
+    DIAG_T0(t_s2);
     constexpr uint32_t kWin = kWave * kStarChunk;
     for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
+#if WOS_STAR_BATCH
+      // this lane's entries inside the window, 16 at a time: the list bytes of a batch
+      // come from five dword reads issued together (one LDS round trip per batch
+      // instead of one per entry), realigned with alignbyte; reads are clamped to the
+      // list's last dword
+      {
+        const uint32_t lo = first < w0 ? w0 - first : 0u;
+        const uint32_t hi0 = first + cnt <= w0 + kWin ? cnt : (first < w0 + kWin ? w0 + kWin - first : 0u);
+        const uint32_t* lw = G.sgrid + G.sgrid_off_words;
+        const uint32_t last_w = cnt > 0u ? ((uint32_t)c_end - 1u) >> 2 : 0u;
+        for (uint32_t i = lo; i < hi0; i += 16u) {
+          const uint32_t b0 = (uint32_t)c_beg + i, wa = b0 >> 2;
+          uint32_t wv[5];
+#pragma unroll
+          for (int j = 0; j < 5; j++) wv[j] = lw[(wa + (uint32_t)j) < last_w ? wa + (uint32_t)j : last_w];
+          uint32_t al[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) al[j] = __builtin_amdgcn_alignbyte(wv[j + 1], wv[j], b0 & 3u);
+          const uint32_t tag = (uint32_t)lane << 26;
+#pragma unroll
+          for (int j = 0; j < 16; j++)
+            if (i + (uint32_t)j < hi0) L->list[first + i + (uint32_t)j - w0] = tag | ((al[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        }
+      }
+#else
       for (uint32_t i = 0; i < cnt; i++) {
         const uint32_t q = first + i;
         if (q >= w0 && q < w0 + kWin) L->list[q - w0] = ((uint32_t)lane << 26) | (uint32_t)lst[c_beg + i];
       }
+#endif
       wave_sync();
+      DIAG_ADD_IF(D_L_S_BUILD, t_s2, lone);
       const uint32_t items = (total - w0) < kWin ? (total - w0) : kWin;
       for (uint32_t k = lane; k < items; k += kWave) {
         const uint32_t e = L->list[k];
@@ -2203,6 +2311,7 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
       }
       wave_sync();
     }
+    DIAG_ADD_IF(D_L_S_WIN, t_s2, lone);
   }
   const bool scan_groups = need && !use_cell;
   const int nsg = sc.n_sgroups, ns = sc.n_sil;
@@ -2259,6 +2368,7 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     }
     wave_sync();
   }
+  DIAG_T0(t_s3);
   if (need) {
     const uint32_t b = L->brk[lane];
     const unsigned long long key = L->best[lane];
@@ -2268,6 +2378,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     if (s >= 0) result = smax(star_candidate_dist<DIM>(G, s, x), minR);
   }
   wave_sync();
+  DIAG_ADD_IF(D_L_S_FIN, t_s3, lone);
+  DIAG_ADD_IF(D_L_S_POST, t_sp, lone);
   return result;
 }
 
@@ -2864,6 +2976,9 @@ __device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& 
   st.walkLength = 0;
   st.totalNeumann = 0.0f;
   st.totalSource = v_tsrc;
+#if WOS_DEFER_TEXEL
+  st.pend = false;
+#endif
   ddist = v_dd;
   g.init(yuk0, sc.absorption);
   if constexpr (BSTART) {
@@ -2891,41 +3006,43 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
                                               RayLDS<DIM>* rayL, RejLDS* rejL, uint32_t* c_iters, int lane) {
   DIAG_T0(t_step);
   int code = -1;
+  DIAG_LONE(lone, active);
   bool flip = false, query = false;
   if (active) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
   DIAG_T0(t_star);
   const float starQ = star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, st.pt, ddist, flip, starL, lane);
-  DIAG_ADD(D_STAR, t_star);
+  DIAG_ADD_LONE(D_STAR, D_L_STAR, t_star, lone);
   const bool live = active && code < 0;
   float dir[DIM], org[DIM], starR = 0.0f;
   for (int k = 0; k < DIM; k++) { dir[k] = 1.0f; org[k] = 0.0f; }
   DIAG_T0(t_mid);
   if (live) starR = walk_step_mid<DIM>(prm, ddist, ws, g, st, &wsteps, query, starQ, dir, org, BSTART ? firstR : 0.0f);
-  DIAG_ADD(D_MID, t_mid);
+  DIAG_ADD_LONE(D_MID, D_L_MID, t_mid, lone);
   Hit ip;
   DIAG_T0(t_ray);
   const bool hit = ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
-  DIAG_ADD(D_RAY, t_ray);
+  DIAG_ADD_LONE(D_RAY, D_L_RAY, t_ray, lone);
   DIAG_T0(t_end);
   if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
-  DIAG_ADD(D_END, t_end);
+  DIAG_ADD_LONE(D_END, D_L_END, t_end, lone);
   float sp[DIM], pdf_unused;
   for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
   DIAG_T0(t_smp);
   if (!prm.ignore_source) sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, c_iters, false, rejL, lane);
-  DIAG_ADD(D_SAMPLE, t_smp);
+  DIAG_ADD_LONE(D_SAMPLE, D_L_SAMPLE, t_smp, lone);
   DIAG_T0(t_tail);
   if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
   if (BSTART) firstR = 0.0f;  // firstStep = false (walk_on_stars.h:325)
-  DIAG_ADD(D_TAIL, t_tail);
-  DIAG_ADD(D_STEP, t_step);
+  DIAG_ADD_LONE(D_TAIL, D_L_TAIL, t_tail, lone);
+  DIAG_ADD_LONE(D_STEP, D_L_STEP, t_step, lone);
   return code;
 }
 
 // the record of a finished walk (walk_on_stars.h:583-585: escaped and over-length walks are dropped)
 template <int DIM>
 __device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t t,
-                                            int code, const WalkState<DIM>& st, uint32_t wsteps, unsigned int* s_ctr) {
+                                            int code, WalkState<DIM>& st, uint32_t wsteps, unsigned int* s_ctr) {
+  flush_source<DIM>(st);
   const bool recorded = code == WC_DIRICHLET || code == WC_RR;
   if (recorded) {
     const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
@@ -3090,6 +3207,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     }
     DIAG_COUNT(D_ITERS, 1);
     DIAG_COUNT(D_LANES, __popcll(__ballot(t >= 0)));
+#if WOS_DIAG
+    const bool lone_it = __popcll(__ballot(t >= 0)) <= 2;
+    if (lone_it) DIAG_COUNT(D_L_ITERS, 1);
+#endif
     const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
@@ -3097,7 +3218,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       t = -1;
     }
     refill(tk);
-    DIAG_ADD(D_LOOP, t_loop);
+#if WOS_DIAG
+    DIAG_ADD_LONE(D_LOOP, D_L_LOOP, t_loop, lone_it);
+#endif
 #if WOS_DIAG
     if (exhausted) {
       DIAG_COUNT(D_XITERS, 1);

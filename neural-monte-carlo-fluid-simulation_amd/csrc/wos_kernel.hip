@@ -214,6 +214,14 @@ void diag_dump(const char* tag) {
   fprintf(stderr, "[diag %s] after the queue ran dry: %llu iterations (%.1f%%), lanes/iter %.2f, %.1f%% of loop cycles\n",
           tag, d[D_XITERS], 100.0 * d[D_XITERS] / (d[D_ITERS] ? d[D_ITERS] : 1),
           (double)d[D_XLANES] / (d[D_XITERS] ? d[D_XITERS] : 1), 100.0 * d[D_XLOOP] / (d[D_LOOP] ? d[D_LOOP] : 1));
+  const double li = (double)(d[D_L_ITERS] ? d[D_L_ITERS] : 1);
+  fprintf(stderr, "[diag %s] <=2 live lanes: %llu iterations, cycles/iter: loop %.0f step %.0f star %.0f (cell %.0f prefix %.0f "
+                  "window %.0f final %.0f) mid %.0f ray %.0f end %.0f sample %.0f tail %.0f\n",
+          tag, d[D_L_ITERS], d[D_L_LOOP] / li, d[D_L_STEP] / li, d[D_L_STAR] / li, d[D_L_S_CELL] / li, d[D_L_S_PFX] / li,
+          d[D_L_S_WIN] / li, d[D_L_S_FIN] / li, d[D_L_MID] / li, d[D_L_RAY] / li, d[D_L_END] / li, d[D_L_SAMPLE] / li,
+          d[D_L_TAIL] / li);
+  fprintf(stderr, "[diag %s] <=2 live lanes star detail: prologue %.0f  list build+sync %.0f  star total (in-function) %.0f\n", tag,
+          d[D_L_S_PRE] / li, d[D_L_S_BUILD] / li, d[D_L_S_POST] / li);
   unsigned long long z[D_NUM] = {};
   hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
 #else

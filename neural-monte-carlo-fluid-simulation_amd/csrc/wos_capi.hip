@@ -853,8 +853,9 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     const int64_t bbase = index_base + b0 * index_stride;
     unsigned long long* qslot = c.d_counters + wos::kNumCounters;
     unsigned int* q_points = (unsigned int*)qslot;
-    unsigned int* q_tasks = (unsigned int*)(qslot + 1);
-    if (k > 0) HIP_TRY(hipMemsetAsync(qslot, 0, 2 * sizeof(unsigned long long), st));
+    unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
+    if (k > 0)
+      HIP_TRY(hipMemsetAsync(qslot, 0, (wos::kNumCounterSlots - wos::kNumCounters) * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(tk.hist, 0, 2 * wos::kCostBuckets * sizeof(uint32_t), st));
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, st));
@@ -1089,7 +1090,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     int bpc = 0;
     HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc, dp.robust != 0));
     const int grid = (int)std::min<int64_t>((int64_t)std::max(1, bpc) * std::max(1, c.num_cus), (tk.T + 63) / 64);
-    unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kNumCounters + 1);
+    unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
     HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, 0, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,
                                      wl.geom_floats_walk, st));
     HIP_TRY(hipEventRecord(q.bev[2], st));

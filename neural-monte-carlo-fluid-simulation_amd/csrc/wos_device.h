@@ -3062,9 +3062,27 @@ __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters
 }
 
 #ifndef WOS_TASK_GRAB
-#define WOS_TASK_GRAB 128
+#define WOS_TASK_GRAB 64
 #endif
 constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
+// The walk queue is dealt round-robin over kTaskQueues counters in windows of kTaskGrab
+// tasks (queue x serves windows x, x + Q, x + 2Q, ... of the cost order): a wave draws
+// from the counter of its block's home queue and, once that one is exhausted, from the
+// others in turn.  Each counter sits on its own 64-byte line (kTaskQueueStride u32), so
+// the device-scope atomics of small windows do not serialize on one address.
+#ifndef WOS_TASK_QUEUES
+#define WOS_TASK_QUEUES 8
+#endif
+constexpr unsigned int kTaskQueues = WOS_TASK_QUEUES;
+#ifndef WOS_TASK_GRAB_HEAD
+#define WOS_TASK_GRAB_HEAD 32
+#endif
+#ifndef WOS_TASK_HEAD
+#define WOS_TASK_HEAD 1
+#endif
+constexpr unsigned int kTaskGrabHead = WOS_TASK_GRAB_HEAD;  // window of the queue's head
+constexpr unsigned int kTaskHead = WOS_TASK_HEAD;           // head windows per wave of the grid
+static_assert((kTaskQueues & (kTaskQueues - 1)) == 0 && kTaskQueues <= (unsigned)kMaxTaskQueues, "power of two");
 
 
 #ifndef WOS_WALK_WAVES_PER_EU
@@ -3117,19 +3135,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // from registers (cross-lane shuffles) instead of a chain of dependent global loads.
   // <= 64 points per window
   const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;
+  // the head of the cost order (the hardest points) is dealt in smaller windows, so the
+  // long walks of one point spread over more waves: kTaskHead windows of kTaskGrabHead
+  // tasks per wave of the grid, then windows of G_win
+  const uint32_t G_head = kTaskGrabHead < G_win ? kTaskGrabHead : G_win;
+  const uint32_t n_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)(kTaskHead * gridDim.x * (blockDim.x / kWave)));
+  const uint32_t NH = G_head > 0u ? ((T + G_head - 1u) / G_head < n_head ? (T + G_head - 1u) / G_head : n_head) : 0u;
+  const uint64_t H = (uint64_t)NH * G_head < (uint64_t)T ? (uint64_t)NH * G_head : (uint64_t)T;
   uint32_t wq = 0, we = 0, wp0 = 0, wperm = 0;
   bool exhausted = false;
+  const uint32_t qhome = blockIdx.x & (kTaskQueues - 1u);
+  uint32_t qdone = 0u;  // queues found exhausted (wave-uniform)
   int head = 0, S = 0;
   uint32_t s_t = 0, s_ok = 0;  // staged task index, its point is estimated
   auto refill = [&](const DevTasks& tk) {
     while (S < kWave && !exhausted) {
       if (wq >= we) {
-        unsigned int c = 0;
-        if (lane == 0) c = atomicAdd(tqueue, G_win);
+        unsigned int c = 0xFFFFFFFFu, len = 0u;
+        if (lane == 0) {
+          for (uint32_t k = 0; k < kTaskQueues; k++) {
+            const uint32_t x = (qhome + k) & (kTaskQueues - 1u);
+            if ((qdone >> x) & 1u) continue;
+            // queue x's draws: its head windows x, x + Q, ... (< NH), then its tail windows
+            const uint32_t d = atomicAdd(tqueue + x * kTaskQueueStride, 1u);
+            const uint32_t nhx = NH > x ? (NH - x + kTaskQueues - 1u) / kTaskQueues : 0u;
+            const uint64_t st = d < nhx ? (uint64_t)(d * kTaskQueues + x) * G_head
+                                        : H + (uint64_t)((uint64_t)(d - nhx) * kTaskQueues + x) * G_win;
+            if (st < (uint64_t)T) {
+              c = (unsigned int)st;
+              len = d < nhx ? G_head : G_win;
+              break;
+            }
+            qdone |= 1u << x;  // exhausted: never drawn from again by this wave
+          }
+        }
         c = __shfl(c, 0);
-        if (c >= T) { exhausted = true; break; }
+        len = __shfl(len, 0);
+        qdone = (uint32_t)__shfl((int)qdone, 0);
+        if (c == 0xFFFFFFFFu) { exhausted = true; break; }
         wq = c;
-        we = (T - c) < G_win ? T : c + G_win;
+        we = (T - c) < len ? T : c + len;
         wp0 = divw(c);
         const uint32_t np = divw(we - 1) - wp0 + 1;
         wperm = (uint32_t)lane < np ? tk.perm[wp0 + lane] : 0u;

@@ -7,8 +7,10 @@ namespace wos {
 constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlockHost = 4;
 constexpr int kNumCounters = 9;
-// queue slots after the counters: [kNumCounters] point queue, [kNumCounters + 1] task queue
-constexpr int kNumCounterSlots = kNumCounters + 2;
+// queue slots (u64) after the counters: [kNumCounters] point queue, then the walk kernel's
+// task queues from slot kNumCounters + 8 on, one per 64-byte line (wos_walk_kernel)
+constexpr int kTaskQueueSlot0 = kNumCounters + 8;
+constexpr int kNumCounterSlots = kTaskQueueSlot0 + kMaxTaskQueues * 8;
 
 // the first balls of every estimated point (after launch_point_setup)
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,

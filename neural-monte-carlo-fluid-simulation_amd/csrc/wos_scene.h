@@ -122,6 +122,10 @@ struct DevParams {
 };
 
 // bins of the rejection bound table: bin = floor(kRejTabScale * sqrt(mu R))
+// the walk kernel's task-queue counters (wos_launch.h kTaskQueueSlot0): at most
+// kMaxTaskQueues, kTaskQueueStride u32 words (64 B) apart
+constexpr int kMaxTaskQueues = 32;
+constexpr unsigned int kTaskQueueStride = 16;
 constexpr int kRejTabBins = 96;
 constexpr float kRejTabScale = 8.0f;
 

@@ -51,7 +51,9 @@ enum { D_ITERS = 0, D_LANES, D_STAR, D_RAY, D_SAMPLE, D_STEP, D_LOOP, D_RAYOVF, 
        D_XITERS, D_XLANES, D_XLOOP,
        // the same sections over iterations with <= 2 live lanes (a lone walk's critical path)
        D_L_ITERS, D_L_STEP, D_L_STAR, D_L_MID, D_L_RAY, D_L_END, D_L_SAMPLE, D_L_TAIL, D_L_LOOP,
-       D_L_S_CELL, D_L_S_PFX, D_L_S_WIN, D_L_S_FIN, D_L_S_BUILD, D_L_S_PRE, D_L_S_POST, D_NUM };  // X: iterations after the wave's task queue ran dry
+       D_L_S_CELL, D_L_S_PFX, D_L_S_WIN, D_L_S_FIN, D_L_S_BUILD, D_L_S_PRE, D_L_S_POST,
+       // first-ball parts: ball update, member a's source sample, the rest of member a, member b, task stores
+       D_FB_UPD, D_FB_SMP, D_FB_MA, D_FB_MB, D_FB_ST, D_FB_ITSUM, D_FB_ITMAX, D_NUM };  // X: iterations after the wave's task queue ran dry
 // slots holding maxima (folded with atomicMax)
 __host__ __device__ constexpr bool diag_is_max(int k) { return k == D_FB_MAX || k == D_WMAXLEN || k == D_WAVEMAX; }
 static __device__ unsigned long long g_diag[D_NUM];
@@ -998,6 +1000,18 @@ struct Gfn {
     }
   }
 
+  // 2D Yukawa (reference members): evaluate() and gradient_norm() from the Bessel values at
+  // mu r, operation for operation -- for callers that evaluate all four orders at once
+  __device__ __forceinline__ float evaluate_k0i0(double k0, double i0) const {
+    const float K0mur = (float)k0, I0mur = (float)i0;
+    return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
+  }
+  __device__ __forceinline__ float gradient_norm_k1i1(double k1, double i1) const {
+    const float K1mur = (float)k1, I1mur = (float)i1;
+    const float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
+    return (float)((double)Qr / (kTwoPi * (double)r));
+  }
+
   __device__ __forceinline__ float poisson_kernel() const {
     if (!yukawa) return DIM == 2 ? (float)(1.0 / kTwoPi) : (float)(1.0 / kFourPi);
     if (scaled()) return scaled_poisson_kernel<DIM>(muR, A1);
@@ -1308,7 +1322,8 @@ __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, 
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
 template <int DIM, bool RB>
 __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>& g, const float* dir, Pcg32& s,
-                                              float* pdf, float* out, uint32_t* iters, bool need_pdf) {
+                                              float* pdf, float* out, uint32_t* iters, bool need_pdf,
+                                              float* r_pre = nullptr) {
   const float R = g.R;
   if (DIM == 3 && !g.yukawa) {
     float u1 = s.nextf(), u2 = s.nextf();
@@ -1365,6 +1380,7 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
     if (decided == 1) break;
   } while (iter < 1000);
   if (need_pdf) *pdf = g.evaluate() / nrm;  // pdf of the last sampled radius (before the clamps)
+  if (r_pre) *r_pre = g.r;
   *iters += (uint32_t)iter;
   g.r = smax(Gfn<DIM>::rClamp, g.r);
   if (g.r > R) g.r = R / 2.0f;
@@ -1402,6 +1418,7 @@ constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
 template <int DIM, bool FB>
 constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : (FB ? WOS_REJ_BMIN3_FB : WOS_REJ_BMIN3);
 static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 16, "RejLDS::surv holds 64 * 16 items");
+
 
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
@@ -1455,7 +1472,7 @@ struct RejLDS {
   float rho3[kWave], inv3[kWave];  // 3D: A0/A1, 1/(norm*bound) (fast path)
   float qb[kWave];                 // certain-reject bound (rej_quick_bound)
   float nrm[kWave], bound[kWave];
-  uint32_t base[kWave], acc[kWave], und[kWave];
+  uint32_t acc[kWave], und[kWave];
   uint32_t owner_of[kWave];
 };
 
@@ -1537,6 +1554,9 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
   }
   if (__ballot(coop) != 0) {
     const uint64_t s0 = s.state;
+    // every unfinished lane is handed B iterations per generation and advances by B
+    // when it does not accept among them, so all unfinished lanes stand at the same
+    // iteration j0: wave-uniform (no per-owner base in LDS)
     int j0 = 0, jacc = -1;
     bool done = !coop;
     DIAG_COUNT(D_RCALLS, 1);
@@ -1576,7 +1596,6 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pend >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)pend, 0u));
         L->owner_of[rank] = (uint32_t)lane;
-        L->base[lane] = (uint32_t)j0;
         L->acc[lane] = 0u;
         L->und[lane] = 0u;
       }
@@ -1586,7 +1605,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         const int orank = rej_div(item, B, mB), b = item - orank * B;
         if (orank < nact) {
           const int owner = (int)L->owner_of[orank];
-          const int j = (int)L->base[owner] + b;
+          const int j = j0 + b;
           if (j < kRejMax) {
             const uint64_t st = rej_state(prm, L->s0[owner], j);
             const float u = draw_float(st);
@@ -1633,11 +1652,9 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           if (u < pdfRadius / bound) { jacc = j0 + b; done = true; break; }
           b++;
         }
-        if (!done) {
-          j0 += B;
-          if (j0 >= kRejMax) { jacc = kRejMax - 1; done = true; }
-        }
+        if (!done && j0 + B >= kRejMax) { jacc = kRejMax - 1; done = true; }
       }
+      j0 += B;
       wave_sync();
     }
     if (coop) {
@@ -2251,7 +2268,6 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     // the (lane, candidate) pairs of all cell lists, spread over the wave in windows
     // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
     // the longest list; accepted candidates fold into the owner like the group scan
-    const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
     const uint32_t cnt = use_cell ? (uint32_t)(c_end - c_beg) : 0u;
     uint32_t incl = cnt;
     for (int dlt = 1; dlt < kWave; dlt <<= 1) {
@@ -2289,6 +2305,7 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
         }
       }
 #else
+      const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
       for (uint32_t i = 0; i < cnt; i++) {
         const uint32_t q = first + i;
         if (q >= w0 && q < w0 + kWin) L->list[q - w0] = ((uint32_t)lane << 26) | (uint32_t)lst[c_beg + i];
@@ -2549,6 +2566,12 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 // 2D keeps the per-lane loop: measured faster for first balls, r1d);
 // lanes with active == false run pair 0's arithmetic for nothing (helping the
 // cooperative sampler) and write and count nothing.
+// 2D first balls: K0, I0, K1, I1 at the sampled radius from one fused Bessel evaluation
+// (pdf and gradient norm), and the second member reuses the first's gradient norm when its
+// radius is the same float -- identical values, fewer double-precision exp / sqrt / divisions
+#ifndef WOS_FB_FUSED_BESSEL
+#define WOS_FB_FUSED_BESSEL 1
+#endif
 template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
@@ -2566,10 +2589,15 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   fs.seed(seed32(prm.seed, (uint64_t)gidx, (uint64_t)w, 1));
   // the first ball (centre x, radius firstR) is the same for both members: its
   // Bessel constants are evaluated once (identical values either way)
+  DIAG_T0(t_upd);
   Gfn<DIM, RB> g0;
   g0.init(yuk0, sc.absorption);
   g0.update_ball(x, firstR, prm.robust != 0);
+  DIAG_ADD(D_FB_UPD, t_upd);
+  // 2D: member a's sampled radius and its gradient norm (r_a < 0: none), reused by member b
+  float r_a = -1.0f, gn_a = 0.0f;
   for (int a = 0; a < prm.n_anti; a++) {
+    DIAG_T0(t_mem);
     const int64_t t = t0 + a;
     Gfn<DIM, RB> g = g0;
     float throughput = 1.0f, totalSource = 0.0f, firstSource = 0.0f;
@@ -2577,12 +2605,48 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
     for (int k = 0; k < DIM; k++) sdir[k] = 0.0f;
     if (!prm.ignore_source) {
       if (a == 0) {
+        DIAG_T0(t_smp);
         float dir[DIM];
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
-        if constexpr (DIM == 3)
+        if constexpr (DIM == 3) {
           sample_volume_wave<DIM, RB, true>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
-        else
+        } else if (WOS_FB_FUSED_BESSEL && g.yukawa == 1) {
+          // the pdf (K0, I0 at the sampled mu r, before the clamps) and the gradient norm
+          // (K1, I1 at the clamped mu r) from one fused evaluation when the clamps kept r
+          float rpre;
+#if WOS_DIAG
+          const uint32_t it0 = *iters;
+#endif
+          sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, false, &rpre);
+#if WOS_DIAG
+          {
+            const uint32_t itn = *iters - it0;
+            uint32_t mx = itn, sm = itn;
+            for (int off = kWave / 2; off > 0; off >>= 1) {
+              mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+              sm += (uint32_t)__shfl_xor((int)sm, off);
+            }
+            if (lane == 0) { atomicAdd(&s_diag[D_FB_ITSUM], (unsigned long long)sm); atomicAdd(&s_diag[D_FB_ITMAX], (unsigned long long)mx); }
+          }
+#endif
+          const float nrm = g.norm();
+          if (rpre == g.r) {
+            double i0, k0, i1, k1;
+            bessel_ik<true, true>((double)(g.r * g.sqrtLambda), &i0, &k0, &i1, &k1);
+            sourcePdf = g.evaluate_k0i0(k0, i0) / nrm;
+            gn_a = g.gradient_norm_k1i1(k1, i1);
+          } else {
+            const float rc = g.r;
+            g.r = rpre;
+            sourcePdf = g.evaluate() / nrm;
+            g.r = rc;
+            gn_a = g.gradient_norm();
+          }
+          r_a = g.r;
+        } else {
           sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, true);
+        }
+        DIAG_ADD(D_FB_SMP, t_smp);
       } else {
         float sdv[DIM];
         for (int k = 0; k < DIM; k++) sdv[k] = sourcePt[k] - x[k];
@@ -2594,7 +2658,12 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       totalSource += throughput * contrib;
       firstSource = contrib;
       float gr[DIM];
-      g.gradient(gr);
+      if (WOS_FB_FUSED_BESSEL && DIM == 2 && g.yukawa == 1 && g.r == r_a) {
+        // gradient() with the norm of member a's identical radius (same value)
+        for (int k = 0; k < DIM; k++) gr[k] = (g.yVol[k] - g.c[k]) * gn_a;
+      } else {
+        g.gradient(gr);
+      }
       float den = sourcePdf * gnorm;
       for (int k = 0; k < DIM; k++) sdir[k] = gr[k] / den;
     }
@@ -2655,7 +2724,9 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       float den = boundaryPdf * throughput;
       for (int k = 0; k < DIM; k++) bdir[k] = pg[k] / den;
     }
+    DIAG_ADD(a == 0 ? D_FB_MA : D_FB_MB, t_mem);
     if (!active) continue;
+    DIAG_T0(t_st);
     tk.first[t] = firstSource;
     for (int k = 0; k < DIM; k++) {
       tk.bdir[k * T + t] = bdir[k];
@@ -2667,6 +2738,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
     // without Dirichlet geometry the distance is the bbox far corner of the walk start,
     // recomputed by the walk kernel from the same floats instead of stored and reloaded
     if (sc.n_dprims > 0) tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
+    DIAG_ADD(D_FB_ST, t_st);
   }
 }
 

@@ -199,6 +199,10 @@ void diag_dump(const char* tag) {
   const double fp = (double)(d[D_FB_PTS] ? d[D_FB_PTS] : 1);
   fprintf(stderr, "[diag %s] first-ball: points %llu cycles/point: setup %.0f lhs %.0f balls %.0f total %.0f\n", tag,
           d[D_FB_PTS], d[D_FB_SETUP] / fp, d[D_FB_LHS] / fp, d[D_FB_BALLS] / fp, d[D_FB_TOTAL] / fp);
+  fprintf(stderr, "[diag %s] first-ball parts cycles/point: ball update %.0f  sample (member a) %.0f  member a %.0f  member b %.0f  stores %.0f\n",
+          tag, d[D_FB_UPD] / fp, d[D_FB_SMP] / fp, d[D_FB_MA] / fp, d[D_FB_MB] / fp, d[D_FB_ST] / fp);
+  fprintf(stderr, "[diag %s] first-ball source samples: rejection iterations per point: sum over lanes %.1f, max over lanes %.1f\n",
+          tag, d[D_FB_ITSUM] / fp, d[D_FB_ITMAX] / fp);
   fprintf(stderr, "[diag %s] step parts cycles/iter: mid (ball update) %.0f  end %.0f  tail %.0f\n", tag,
           (double)d[D_MID] / (d[D_ITERS] ? d[D_ITERS] : 1), (double)d[D_END] / (d[D_ITERS] ? d[D_ITERS] : 1),
           (double)d[D_TAIL] / (d[D_ITERS] ? d[D_ITERS] : 1));

@@ -37,27 +37,37 @@ def main():
            "--no-projection-wall"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
                    stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=300)
-    per, dur = {}, {}
+    per, dur, kname = {}, {}, {}
     for f in glob.glob(os.path.join(OUT, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "wos_walk_kernel" not in r["Kernel_Name"]:
-                continue
             d = r["Dispatch_Id"]
+            kname[d] = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("wos::", "")
             per.setdefault(d, {}).setdefault(r["Counter_Name"], 0.0)
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
             dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    if not per:
+
+    def summary(name):
+        ds = [d for d in per if kname[d] == name]
+        n = len(ds)
+        mean = {c: sum(per[d].get(c, 0.0) for d in ds) / n for c in COUNTERS}
+        t = sum(dur[d] for d in ds) / n
+        return {"kernel": name, "config": CONFIG, "lib_sha16": lib_sha16(), "dispatches": n, "kernel_s": t,
+                "counters": mean,
+                "valu_issue_frac": mean["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS),
+                "wait_any_frac": mean["SQ_WAIT_ANY"] / max(mean["SQ_WAVE_CYCLES"], 1.0),
+                "wait_inst_frac": mean["SQ_WAIT_INST_ANY"] / max(mean["SQ_WAVE_CYCLES"], 1.0),
+                "active_frac": mean["SQ_ACTIVE_INST_ANY"] / max(mean["SQ_WAVE_CYCLES"], 1.0),
+                "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass), bench.py --steps 2 --warmup 1; "
+                          "VALU issue = INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs)"}
+
+    if "wos_walk_kernel" not in kname.values():
         raise SystemExit(f"no wos_walk_kernel records under {OUT}")
-    n = len(per)
-    mean = {c: sum(p.get(c, 0.0) for p in per.values()) / n for c in COUNTERS}
-    t = sum(dur.values()) / n
-    res = {"kernel": "wos_walk_kernel", "config": CONFIG, "lib_sha16": lib_sha16(), "dispatches": n, "kernel_s": t, "counters": mean,
-           "valu_issue_frac": mean["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS),
-           "wait_any_frac": mean["SQ_WAIT_ANY"] / mean["SQ_WAVE_CYCLES"],
-           "wait_inst_frac": mean["SQ_WAIT_INST_ANY"] / mean["SQ_WAVE_CYCLES"],
-           "active_frac": mean["SQ_ACTIVE_INST_ANY"] / mean["SQ_WAVE_CYCLES"],
-           "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass), bench.py --steps 2 --warmup 1; "
-                     "VALU issue = INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs)"}
+    # every kernel of the projection (the first-ball and setup kernels too)
+    allk = {k: summary(k) for k in sorted(set(kname.values()))}
+    json.dump(allk, open(os.path.join(REPO, "gpurun_out", f"{TAG}_all_sq.json"), "w"), indent=1)
+    for k, v in allk.items():
+        print(k, json.dumps({x: v[x] for x in ("kernel_s", "valu_issue_frac", "wait_any_frac", "active_frac")}))
+    res = allk["wos_walk_kernel"]
     path = os.path.join(REPO, "gpurun_out", f"{TAG}_walk_sq.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res))

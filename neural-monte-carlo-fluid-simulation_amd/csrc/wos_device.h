@@ -376,6 +376,27 @@ __device__ __forceinline__ int wave_min_int(int v) {
   return v;
 }
 
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// a lane's float value, wave-uniform
+__device__ __forceinline__ float lane_bcast(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 // computeDistToDirichlet (fcpw_scene_loader.h:299-315) over the Dirichlet
 // primitives, groups of kGroup culled by their boxes.  The sequential `<=` scan
 // returns d of the highest-index primitive attaining the minimum computed d^2;
@@ -1534,6 +1555,13 @@ __device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, floa
   return u < pdfRadius / bound ? 1 : 0;
 }
 
+// 1: queries with exactly one querying lane (a lone walk in its wave) take the
+// register-only solo forms (sampler, star radius, ray): every lane works on the one
+// owner's items, owner data broadcast with readlane, results by ballot / wave reduction
+#ifndef WOS_SOLO
+#define WOS_SOLO 1
+#endif
+
 // Convergent: every lane calls it.  Inactive lanes do nothing.  2D: certified float
 // decisions by any lane, undecided ones by the owner (exact); 3D: certified float
 // decisions by any lane, undecided ones by the same lane with the exact test (cheap
@@ -1552,7 +1580,77 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
     nrm = g.norm();
     coop = true;
   }
-  if (__ballot(coop) != 0) {
+  const uint64_t cmask = __ballot(coop);
+  if (WOS_SOLO && cmask != 0 && (cmask & (cmask - 1)) == 0) {
+    // one sampling lane (a lone walk): lane l evaluates iteration j0 + l of the owner's
+    // stream with the owner's constants broadcast from registers; the decisions come
+    // back as ballots and are scanned in order -- no LDS, no wave syncs
+    const int ol = __builtin_ctzll(cmask);
+    const uint64_t s0 = s.state;
+    const uint64_t s0o = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s0 >> 32), ol) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s0, ol);
+    const float invNB = 1.0f / (nrm * bound);
+    const float oR = lane_bcast(g.R, ol), oSL = lane_bcast(g.sqrtLambda, ol);
+    const float oQB = lane_bcast(coop ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 0.0f, ol);
+    const float oRho = lane_bcast(coop ? g.A0 / g.A1 : 0.0f, ol), oInv = lane_bcast(invNB, ol);
+    float oA0 = 0.0f, oA1 = 0.0f, oNrm = 0.0f, oBound = 0.0f;
+    if constexpr (DIM == 3) {
+      oA0 = lane_bcast(g.A0, ol); oA1 = lane_bcast(g.A1, ol); oNrm = lane_bcast(nrm, ol); oBound = lane_bcast(bound, ol);
+    }
+    DIAG_COUNT(D_RCALLS, 1);
+    DIAG_COUNT(D_RLANES, 1);
+    int jacc = -1;
+    for (int j0 = 0; jacc < 0; j0 += kWave) {
+      DIAG_COUNT(D_RGENS, 1);
+      const int j = j0 + lane;
+      int dcs = 0;
+      if (j < kRejMax) {
+        const uint64_t st = rej_state(prm, s0o, j);
+        const float u = draw_float(st);
+        DIAG_LANE(D_RITEMS);
+        if (u > oQB) {
+          DIAG_LANE(D_RQUICK);
+        } else {
+          const float x = draw_float(st * kPcgMult + kPcgInc);
+          if constexpr (DIM == 2) {
+            dcs = rej_fast_decide(u, x * oR, oSL, oRho, oInv);
+          } else {
+            const float rr = x * oR;
+            dcs = rej_fast_decide3(u, rr, oSL, oRho, oInv);
+            if (dcs < 0) dcs = rej_exact_decide3(u, rr, oR, oSL, oA0, oA1, oNrm, oBound);
+          }
+        }
+      }
+      const uint64_t acc = __ballot(dcs == 1), und = __ballot(dcs < 0);
+      for (uint64_t m = acc | und; m != 0; m &= m - 1) {
+        const int b = __builtin_ctzll(m);
+        if ((acc >> b) & 1ull) { jacc = j0 + b; break; }
+        // undecided: the exact test of sample_volume, by the owner
+        int ok = 0;
+        if (lane == ol) {
+          float u, x;
+          rej_draws(prm, s0, j0 + b, &u, &x);
+          g.r = x * g.R;
+          const float pr = g.evaluate() / nrm;
+          const float pdfRadius = pr / pdf_sphere_uniform<DIM>(g.r);
+          ok = u < pdfRadius / bound ? 1 : 0;
+        }
+        if (__builtin_amdgcn_readlane(ok, ol)) { jacc = j0 + b; break; }
+      }
+      if (jacc < 0 && j0 + kWave >= kRejMax) jacc = kRejMax - 1;  // limit: last radius kept
+    }
+    if (coop) {
+      float u, x;
+      rej_draws(prm, s0, jacc, &u, &x);
+      g.r = x * g.R;
+      s.state = rej_state(prm, s0, jacc + 1);
+      *iters += (uint32_t)(jacc + 1);
+      if (need_pdf) *pdf = g.evaluate() / nrm;
+      g.r = smax(Gfn<DIM>::rClamp, g.r);
+      if (g.r > g.R) g.r = g.R / 2.0f;
+      for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
+    }
+  } else if (cmask != 0) {
     const uint64_t s0 = s.state;
     // every unfinished lane is handed B iterations per generation and advances by B
     // when it does not accept among them, so all unfinished lanes stand at the same
@@ -2037,12 +2135,54 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
   if (__ballot(need) == 0) return false;
   float inv[DIM];
   for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
+  const bool tree = TREE && sc.ptree.levels > 0;
+  const uint64_t nmask = __ballot(need);
+  if (WOS_SOLO && !tree && (nmask & (nmask - 1)) == 0) {
+    // one querying lane: lane l tests group g0 + l against the owner's ray, then the
+    // primitives of the accepted groups, kGroup lanes per group; the minimum key by a
+    // wave reduction instead of LDS atomics
+    const int ol = __builtin_ctzll(nmask);
+    float oo[DIM], od[DIM], oi[DIM];
+    for (int k = 0; k < DIM; k++) { oo[k] = lane_bcast(o[k], ol); od[k] = lane_bcast(dir[k], ol); oi[k] = lane_bcast(inv[k], ol); }
+    const float ot = lane_bcast(tmax, ol);
+    unsigned long long best = ~0ull;
+    for (int g0 = 0; g0 < ng; g0 += kWave) {
+      const int gi = g0 + lane;
+      uint64_t gm = __ballot(gi < ng && ray_box_maybe<DIM>(G.pgroup + gi * kGroupStride, oo, oi, ot));
+      while (gm != 0) {
+        // lanes [kGroup q, kGroup (q + 1)) take the q-th accepted group of this round
+        uint64_t mm = gm;
+        for (int q = lane / kGroup; q > 0 && mm != 0; q--) mm &= mm - 1;
+        for (int q = 0; q < kWave / kGroup && gm != 0; q++) gm &= gm - 1;
+        if (mm != 0) {
+          const int p = (g0 + __builtin_ctzll(mm)) * kGroup + (lane & (kGroup - 1));
+          if (p < np) {
+            float rt = ot;
+            Hit hh;
+            if (ray_prim_filtered<DIM>(G.prim + p * PS, oo, od, rt, &hh)) {
+              const unsigned long long key =
+                  ((unsigned long long)__float_as_uint(hh.d + 0.0f) << 32) | (0xFFFFFFFFu - (uint32_t)p);
+              best = key < best ? key : best;
+            }
+          }
+        }
+      }
+    }
+    best = wave_min_u64(best);
+    bool found = false;
+    if (need && best != ~0ull) {
+      const int p = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+      float rt = tmax;
+      found = ray_prim_exact<DIM>(G.prim + p * PS, o, dir, rt, h);
+      if (found) normalize_rcp<DIM>(h->n);
+    }
+    return found;
+  }
   if (need) {
     for (int k = 0; k < DIM; k++) { L->qo[k][lane] = o[k]; L->qd[k][lane] = dir[k]; }
     L->rt[lane] = tmax;
     L->best[lane] = ~0ull;
   }
-  const bool tree = TREE && sc.ptree.levels > 0;
   int cL = (tree && need) ? sc.ptree.levels : -1, ci = 0;
   for (int g0 = 0;; g0 += kRayChunk) {
     uint32_t mask = 0;
@@ -2253,7 +2393,44 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
       use_cell = true;
     }
   }
-  if (__ballot(need) == 0) return result;
+  const uint64_t nmask = __ballot(need);
+  if (nmask == 0) return result;
+  if (WOS_SOLO && (nmask & (nmask - 1)) == 0 &&
+      __builtin_amdgcn_readlane((int)use_cell, __builtin_ctzll(nmask)) != 0) {
+    // one querying lane inside the cell grid: lane l judges entry l of the owner's cell
+    // list (64 at a time) against the owner's query; (d^2, ~index) minimum and the
+    // lowest index within minR by wave reductions instead of the LDS list and atomics
+    const int ol = __builtin_ctzll(nmask);
+    float xo[DIM];
+    for (int k = 0; k < DIM; k++) xo[k] = lane_bcast(x[k], ol);
+    const float r2o = lane_bcast(r2, ol), minR2o = lane_bcast(minR2, ol);
+    const bool flo = __builtin_amdgcn_readlane((int)flipOrient, ol) == 0;  // computeStarRadius passes !flip
+    const int cb = __builtin_amdgcn_readlane(c_beg, ol), ce = __builtin_amdgcn_readlane(c_end, ol);
+    const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
+    unsigned long long best = ~0ull;
+    uint32_t brk = 0xFFFFFFFFu;
+    for (int k0 = cb; k0 < ce; k0 += kWave) {
+      const int k = k0 + lane;
+      if (k < ce) {
+        const int sidx = (int)lst[k];
+        float d2;
+        if (star_candidate<DIM>(G, sidx, xo, r2o, flo, prec, &d2)) {
+          const unsigned long long key = ((unsigned long long)__float_as_uint(d2) << 32) | (0xFFFFFFFFu - (uint32_t)sidx);
+          best = key < best ? key : best;
+          if (d2 <= minR2o) brk = (uint32_t)sidx < brk ? (uint32_t)sidx : brk;
+        }
+      }
+    }
+    best = wave_min_u64(best);
+    brk = wave_min_u32(brk);
+    if (need) {
+      int sw = -1;
+      if (brk != 0xFFFFFFFFu) sw = (int)brk;
+      else if (best != ~0ull) sw = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+      if (sw >= 0) result = smax(star_candidate_dist<DIM>(G, sw, x), minR);
+    }
+    return result;
+  }
   if (need) {
     for (int k = 0; k < DIM; k++) L->qx[k][lane] = x[k];
     L->r2[lane] = r2;
@@ -3368,10 +3545,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #ifndef WOS_FOLD_CHUNK
 #define WOS_FOLD_CHUNK 16
 #endif
-#ifndef WOS_FOLD_UNROLL
-#define WOS_FOLD_UNROLL 4
+// staging slots in flight per thread: 2D 8 (fold -10 % on karman, -13 % on config C),
+// 3D 4 (8 measured +4 % on the cube), profiles/r3x_ab_solo_fold.log
+#ifndef WOS_FOLD_UNROLL2
+#define WOS_FOLD_UNROLL2 8
 #endif
-constexpr int kFoldPoints = WOS_FOLD_POINTS, kFoldChunk = WOS_FOLD_CHUNK, kFoldUnroll = WOS_FOLD_UNROLL;
+#ifndef WOS_FOLD_UNROLL3
+#define WOS_FOLD_UNROLL3 4
+#endif
+constexpr int kFoldPoints = WOS_FOLD_POINTS, kFoldChunk = WOS_FOLD_CHUNK;
+template <int DIM>
+constexpr int kFoldUnroll = DIM == 2 ? WOS_FOLD_UNROLL2 : WOS_FOLD_UNROLL3;
 
 template <int DIM>
 __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams prm, const DevTasks tk, int64_t n,
@@ -3397,12 +3581,12 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   uint32_t steps = 0;
   for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
     const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
-    // kFoldUnroll staging slots in flight per thread: all their loads are issued
+    // kFoldUnroll<DIM> staging slots in flight per thread: all their loads are issued
     // before the first LDS store (one HBM round trip per kFoldUnroll slots, not per slot)
-    for (int e0 = tid; e0 < nb * kFoldChunk; e0 += kFoldPoints * kFoldUnroll) {
-      float v[kFoldUnroll][NF];
+    for (int e0 = tid; e0 < nb * kFoldChunk; e0 += kFoldPoints * kFoldUnroll<DIM>) {
+      float v[kFoldUnroll<DIM>][NF];
 #pragma unroll
-      for (int u = 0; u < kFoldUnroll; u++) {
+      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
         const int e = e0 + u * kFoldPoints;
         const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
         if (e >= nb * kFoldChunk || j >= cnt) continue;
@@ -3417,7 +3601,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
         }
       }
 #pragma unroll
-      for (int u = 0; u < kFoldUnroll; u++) {
+      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
         const int e = e0 + u * kFoldPoints;
         const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
         if (e >= nb * kFoldChunk || j >= cnt) continue;

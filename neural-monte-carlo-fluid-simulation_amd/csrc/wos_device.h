@@ -1441,6 +1441,20 @@ constexpr int kRejBmin = DIM == 2 ? WOS_REJ_BMIN2 : (FB ? WOS_REJ_BMIN3_FB : WOS
 static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 16, "RejLDS::surv holds 64 * 16 items");
 
 
+// iterations each sampling lane evaluates on its own before the cooperative generations
+// (0: none) in calls with at least WOS_REJ_OWN_MIN sampling lanes; 4 / 40 measured best
+// (karman -3 %, config C -2 %, the cube -1.5 %, the stride-8 shard unchanged;
+// profiles/r3y_ab_own_generation.log)
+#ifndef WOS_REJ_OWN
+#define WOS_REJ_OWN 4
+#endif
+constexpr int kRejOwn = WOS_REJ_OWN;
+#ifndef WOS_REJ_OWN_MIN
+#define WOS_REJ_OWN_MIN 40
+#endif
+constexpr int kRejOwnMin = WOS_REJ_OWN_MIN;  // sampling lanes for the own generation
+static_assert(WOS_REJ_OWN >= 0 && WOS_REJ_OWN <= 16 && WOS_REJ_OWN < kRejMax, "WOS_REJ_OWN");
+
 // PCG32 jump-ahead: state after k draws from s0 (DevParams::jump, built on the host)
 __device__ __forceinline__ uint64_t jump_state(const DevParams& prm, uint64_t s0, int k) {
   const uint64_t A = prm.jump[2 * k], Cc = prm.jump[2 * k + 1];
@@ -1659,6 +1673,50 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
     bool done = !coop;
     DIAG_COUNT(D_RCALLS, 1);
     DIAG_COUNT(D_RLANES, __popcll(__ballot(coop)));
+#if WOS_REJ_OWN
+    // generation 0 of a dense call (at least kRejOwnMin sampling lanes): every sampling lane
+    // evaluates the first kRejOwn iterations of its own stream in registers (no LDS
+    // broadcast, no atomics, no wave syncs); the lanes still without an accept continue
+    // cooperatively from iteration kRejOwn.  Sparse calls keep the cooperative generations
+    // from iteration 0 (shorter dependency chains for the few lanes of the tail).
+    const bool own = __popcll(cmask) >= kRejOwnMin;
+    if (own && !done) {
+      const float invNB0 = 1.0f / (nrm * bound);
+      const float qb0 = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB0);
+      uint32_t acc = 0u, und = 0u;
+#pragma unroll
+      for (int b = 0; b < kRejOwn; b++) {
+        const uint64_t st = rej_state(prm, s0, b);
+        const float u = draw_float(st);
+        int dcs = 0;
+        DIAG_LANE(D_RITEMS);
+        if (!(u > qb0)) {
+          const float x = draw_float(st * kPcgMult + kPcgInc);
+          if constexpr (DIM == 2) {
+            dcs = rej_fast_decide(u, x * g.R, g.sqrtLambda, g.A0 / g.A1, invNB0);
+          } else {
+            const float rr = x * g.R;
+            dcs = rej_fast_decide3(u, rr, g.sqrtLambda, g.A0 / g.A1, invNB0);
+            if (dcs < 0) dcs = rej_exact_decide3(u, rr, g.R, g.sqrtLambda, g.A0, g.A1, nrm, bound);
+          }
+        }
+        if (dcs == 1) acc |= 1u << b;
+        else if (dcs < 0) und |= 1u << b;
+      }
+      for (uint32_t m = acc | und; m != 0u; m &= m - 1u) {
+        const int b = __builtin_ctz(m);
+        if ((acc >> b) & 1u) { jacc = b; done = true; break; }
+        // undecided: the exact test of sample_volume
+        float u, x;
+        rej_draws(prm, s0, b, &u, &x);
+        g.r = x * g.R;
+        const float p = g.evaluate() / nrm;
+        const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
+        if (u < pdfRadius / bound) { jacc = b; done = true; break; }
+      }
+    }
+    j0 = own ? kRejOwn : 0;
+#endif
     if (!done) {
       L->s0[lane] = s0;
       L->R[lane] = g.R;

@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-projection-wall", action="store_true")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="config B: skip the strong line and the stride-8 shard (profiling passes that must "
+                         "see the weak workload's launches only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the product path); gloo stages the all-gather through host "
                          "memory and lets N ranks share one GPU (tests/test_bench_dist.py)")
@@ -341,7 +344,7 @@ def main():
     steps_rec, steps_all = reduce_steps(steps_rec, steps_all, world, dist, torch, dev)
 
     strong = shard = None
-    if a.config == "B" and scaling == "weak":
+    if a.config == "B" and scaling == "weak" and not a.no_strong:
         strong = strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, workloads)
         if world == 1:
             shard = shard_projection(a, scene, params, dim, torch, dev, workloads)

@@ -130,6 +130,16 @@ hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm,
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void wos_zero_kernel(unsigned long long* a, int n64, uint32_t* b, int n32) {
+  for (int i = threadIdx.x; i < n64; i += blockDim.x) a[i] = 0ull;
+  for (int i = threadIdx.x; i < n32; i += blockDim.x) b[i] = 0u;
+}
+
+hipError_t launch_zero(unsigned long long* a, int n64, uint32_t* b, int n32, hipStream_t s) {
+  hipLaunchKernelGGL(wos_zero_kernel, dim3(1), dim3(256), 0, s, a, n64, b, n32);
+  return hipGetLastError();
+}
+
 hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s) {
   const int grid = (int)((n + 255) / 256);
   if (grid > 0) hipLaunchKernelGGL(wos_lpt_scatter_kernel, dim3(grid), dim3(256), 0, s, tk, n);

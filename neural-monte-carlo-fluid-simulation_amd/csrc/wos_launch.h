@@ -19,6 +19,8 @@ hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm,
 // per-point setup: pstate + first-ball radius + bucket histogram, before launch_lpt_order
 hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,
                               const DevTasks& tk, hipStream_t s);
+// zero n64 u64 words at a and n32 u32 words at b (one launch)
+hipError_t launch_zero(unsigned long long* a, int n64, uint32_t* b, int n32, hipStream_t s);
 // bucket offsets + point permutation for the walk queue
 hipError_t launch_lpt_order(const DevTasks& tk, int64_t n, hipStream_t s);
 hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,

@@ -34,7 +34,7 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", *COUNTERS, "-d", OUT, "-o", "sq", "--output-format", "csv", "--",
            sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline",
-           "--no-projection-wall"]
+           "--no-projection-wall", "--no-strong"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
                    stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=300)
     per, dur, kname = {}, {}, {}

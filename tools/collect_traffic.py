@@ -34,7 +34,7 @@ def run_pass(counter):
     d = os.path.join(OUT, counter.lower())
     os.makedirs(d, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", counter.lower(), "--output-format", "csv", "--",
-           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline", "--no-projection-wall"]
+           sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline", "--no-projection-wall", "--no-strong"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
                    stdout=open(os.path.join(d, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=600)
     vals = []

@@ -4,7 +4,7 @@
 #   tools/r3_bench.sh TAG
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-TAG=${1:-r3}
+TAG=${1:-r3z}
 timeout -k 10 240 python -u -m pytest tests/test_bench_dist.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/${TAG}_bdist.log 2>&1 &&
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench_B.json 2> gpurun_out/${TAG}_bench_B.err &&
 timeout -k 10 240 python bench.py --config C --steps 20 --warmup 2 > gpurun_out/${TAG}_bench_C.json 2> gpurun_out/${TAG}_bench_C.err &&

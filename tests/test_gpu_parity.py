@@ -246,6 +246,29 @@ def test_cube3d_bit_exact(gpu, oracle):
     _compare(oracle, osc, sc, cfg, cfg["points"])
 
 
+@pytest.mark.parametrize("dim,npts", [(2, 1), (2, 3), (3, 1), (3, 3)])
+def test_lone_walks_bit_exact(gpu, oracle, dim, npts):
+    """Solves of one to three near-wall points: the long walks of such points leave the
+    walk kernel's waves with one live walk for most iterations, where the register-only
+    solo forms of the sampler, star-radius and ray queries run (round 3); the oracle must
+    still agree bit for bit."""
+    if dim == 2:
+        cfg = workloads.karman_config(n_walks=128)
+        osc, sc = _pair(cfg, oracle)
+        pts = cfg["points"]
+        # the points nearest the channel walls (y = +-0.6035) but not on them
+        d = 0.6035 - np.abs(pts[:, 1])
+        order = np.argsort(np.where(d > 2e-3, d, np.inf), kind="stable")
+    else:
+        cfg = workloads.cube_config(res=16, n_walks=128)
+        osc, sc = _pair(cfg, oracle, dim=3)
+        pts = cfg["points"]
+        order = np.argsort(1.0 - np.abs(pts).max(axis=1), kind="stable")  # nearest a face
+    sel = np.ascontiguousarray(pts[order[:npts]])
+    _, _, st = _compare(oracle, osc, sc, cfg, sel)
+    assert st["walk_steps"] > 0
+
+
 def test_karman_full_size_properties(gpu, oracle):
     """64k points x 128 walks (BASELINE config B): determinism, shard invariance,
     finiteness, and the oracle on a strided subset matches bit for bit."""

@@ -354,6 +354,9 @@ constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
 // the stream through initstate), so the increment is the constant (1 << 1) | 1
 // and a generator is one 64-bit register pair.
 constexpr uint64_t kPcgInc = 3u;
+// two steps at once: state * kPcgMult2 + kPcgInc2 == (state * kPcgMult + kPcgInc) * kPcgMult + kPcgInc
+constexpr uint64_t kPcgMult2 = kPcgMult * kPcgMult;
+constexpr uint64_t kPcgInc2 = kPcgInc * kPcgMult + kPcgInc;
 
 struct Pcg32 {
   uint64_t state;

@@ -1341,6 +1341,11 @@ __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, 
 
 // sampleVolume + rejectionSampleGreensFn (distributions.h:362-383,404-410,486-500,591-599,710-720).
 // need_pdf: the caller uses the returned pdf (first ball); walk steps ignore it.
+// the float draw Pcg32::nextf makes from a stream state (before its step)
+__device__ __forceinline__ float pcg_float_of(uint64_t state) {
+  return bits_to_float((pcg_output(state) >> 9) | 0x3f800000u) - 1.0f;
+}
+
 template <int DIM, bool RB>
 __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>& g, const float* dir, Pcg32& s,
                                               float* pdf, float* out, uint32_t* iters, bool need_pdf,
@@ -1374,15 +1379,20 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
   const float invNB = 1.0f / (nrm * bound);
   const float quick = g.yukawa ? rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB) : 3.0e38f;
   int iter = 0;
+  // the stream walks two draws per iteration with one jump (state * A2 + C2); the radius
+  // draw becomes a float only when the certain-reject test leaves u undecided (the
+  // tiny-ball loops of near-wall points run to hundreds of iterations, nearly all of
+  // them certain rejects: profiles/r3z_ab_seq_loop.log)
+  uint64_t st = s.state, st1 = st;
   do {
-    float u = s.nextf();
-    const float xd = s.nextf();
-    g.r = xd * R;
+    const float u = pcg_float_of(st);
+    st1 = st * kPcgMult + kPcgInc;
+    st = st * kPcgMult2 + kPcgInc2;
     iter++;
     int decided = -1;  // 1 accept, 0 reject, -1 undecided
-    if (u > quick) {
-      decided = 0;
-    } else if (fast) {
+    if (u > quick) continue;
+    g.r = pcg_float_of(st1) * R;
+    if (fast) {
       const float mur = g.r * g.sqrtLambda;
       float k0, i0v;
       k0i0_fast(mur, &k0, &i0v);
@@ -1400,6 +1410,8 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
     }
     if (decided == 1) break;
   } while (iter < 1000);
+  s.state = st;
+  g.r = pcg_float_of(st1) * R;  // the last iteration's radius (also when the limit ended the loop)
   if (need_pdf) *pdf = g.evaluate() / nrm;  // pdf of the last sampled radius (before the clamps)
   if (r_pre) *r_pre = g.r;
   *iters += (uint32_t)iter;

@@ -545,7 +545,7 @@ int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
   if (points > c.pstate_cap) {
     hipFree(c.d_pstate);
     c.d_pstate = nullptr; c.pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)3 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)7 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
     c.pstate_cap = points;
   }
   return WOS_OK;
@@ -568,6 +568,8 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap);
   tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap);
   tk.hist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap);
+  tk.pball = (float*)(c.d_pstate + 3 * c.pstate_cap + 2 * wos::kCostBuckets);
+  tk.pball_stride = c.pstate_cap;
   tk.T = T;
   tk.wpp = wpp;
   return tk;

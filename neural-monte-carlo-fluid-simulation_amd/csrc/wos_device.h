@@ -968,6 +968,15 @@ struct Gfn {
   // RB: the instantiation of the robust kernels; elsewhere the scaled branches are dead code
   __device__ __forceinline__ bool scaled() const { return RB && yukawa == kYukScaled; }
 
+  // update_ball of a 2D Yukawa ball (reference members) with K0 I0 K1 I1 at mu R given
+  // (the same update_ball evaluation, made by the point-setup kernel)
+  __device__ __forceinline__ void set_ball(const float* cc, float RR, const float* m) {
+    for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
+    R = RR; r = 0.0f;
+    muR = R * sqrtLambda;
+    A0 = m[0]; A1 = m[1]; B0 = m[2]; B1 = m[3];
+  }
+
   __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust) {
     for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
     R = RR; r = 0.0f;
@@ -2775,9 +2784,9 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   for (int idx = lane; idx < nd; idx += kWave) {
     const int j = sd == 1 ? idx : idx % nstrat;
     const uint32_t bound = (uint32_t)(nstrat - j);
-    const uint32_t th = (~bound + 1u) % bound;
     const uint32_t r = pcg_output(jump_state(prm, s0, nd + idx));
-    rej |= r < th;
+    // PCG's rejection threshold th = 2^32 mod bound < bound: only r < bound can fall below it
+    if (r < bound) rej |= r < (~bound + 1u) % bound;
     partner[idx] = j + (int)(r % bound);
   }
   const bool any_rej = __any(rej);
@@ -2823,7 +2832,7 @@ template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
                                             bool active, int w, int64_t t0, bool yuk0, uint32_t* iters,
-                                            RejLDS* rejL, int lane) {
+                                            RejLDS* rejL, int lane, const float* pb) {
   constexpr int sd = DIM - 1;
   if (DIM == 2 && !active) return;
   if (!active) w = 0;
@@ -2839,7 +2848,13 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
   DIAG_T0(t_upd);
   Gfn<DIM, RB> g0;
   g0.init(yuk0, sc.absorption);
-  g0.update_ball(x, firstR, prm.robust != 0);
+  if constexpr (!RB && DIM == 2) {
+    // the Bessel members at mu R from the point-setup kernel (DevTasks::pball)
+    if (g0.yukawa) g0.set_ball(x, firstR, pb);
+    else g0.update_ball(x, firstR, false);
+  } else {
+    g0.update_ball(x, firstR, prm.robust != 0);
+  }
   DIAG_ADD(D_FB_UPD, t_upd);
   // 2D: member a's sampled radius and its gradient norm (r_a < 0: none), reused by member b
   float r_a = -1.0f, gn_a = 0.0f;
@@ -3175,6 +3190,17 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
     if (sub == 0) {
       tk.pstate[i] = ps;
       tk.prad[i] = firstR;
+      if constexpr (DIM == 2) {
+        if (tk.pball != nullptr && (ps & kPtEstimate) && sc.absorption > 0.0f && prm.steps_before_tikhonov == 0) {
+          Gfn<2> g;
+          g.init(true, sc.absorption);
+          g.update_ball(x, firstR, false);
+          tk.pball[i] = g.A0;
+          tk.pball[tk.pball_stride + i] = g.A1;
+          tk.pball[2 * tk.pball_stride + i] = g.B0;
+          tk.pball[3 * tk.pball_stride + i] = g.B1;
+        }
+      }
       atomicAdd(&s_hist[bucket], 1u);
     }
   }
@@ -3217,10 +3243,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   unsigned int cend = idx + kPtGrab;
   float xn[DIM], rn = 0.0f;
   bool en = false;
+  // 2D Yukawa, reference semantics: the first ball's Bessel members come from the setup kernel
+  const bool pre = !RB && DIM == 2 && yuk0;
+  float bn[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
   if ((int64_t)idx < n) {
     rn = tk.prad[idx];
     en = (tk.pstate[idx] & kPtEstimate) != 0;
+    if (pre)
+      for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + idx];
   }
   for (;;) {
     if ((int64_t)idx >= n) break;
@@ -3230,6 +3261,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     for (int k = 0; k < DIM; k++) x[k] = xn[k];
     const float firstR = rn;
     const bool estimate = en;
+    float pb[4];
+    for (int k = 0; k < 4; k++) pb[k] = bn[k];
     const bool grab = idx + 1 >= cend;  // wave-uniform
     unsigned int nidx_l0 = 0;
     if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
@@ -3246,6 +3279,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     if ((int64_t)nidx < n) {
       rn = tk.prad[nidx];
       en = (tk.pstate[nidx] & kPtEstimate) != 0;
+      if (pre)
+        for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + nidx];
     }
     if (!estimate) { idx = nidx; cend = ncend; continue; }
     c_pts += lane == 0;
@@ -3258,7 +3293,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     for (int w0 = 0; w0 < npairs; w0 += kWave) {
       const int w = w0 + lane;
       first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
-                           (int64_t)pidx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane);
+                           (int64_t)pidx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane,
+                           pb);
     }
     DIAG_ADD(D_FB_BALLS, t_fb2);
     DIAG_ADD(D_FB_TOTAL, t_fb0);

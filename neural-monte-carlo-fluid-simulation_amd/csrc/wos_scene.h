@@ -155,6 +155,11 @@ struct DevTasks {
   float* n0;
   float* r0;
   uint32_t* sflags;
+  // [4][pball_stride] per point: the 2D Yukawa first ball's Bessel members K0 I0 K1 I1 at
+  // mu R (Gfn::update_ball), written by the point-setup kernel (one lane per point) for the
+  // reference-semantics first-ball kernel; nullptr: the first-ball kernel evaluates them
+  float* pball;
+  int64_t pball_stride;
 };
 
 // floats per task: start state pt[DIM] thr tsrc dd, record first bdir[DIM] sdir[DIM] total code

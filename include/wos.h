@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 7
+#define WOS_ABI_VERSION 8
 
 enum {
     WOS_OK = 0,
@@ -68,6 +68,15 @@ typedef struct wos_scene_desc {
     const float *source;             /* -div(u) grid: 2D [H][W] (rows ~ y); 3D [X][Y][Z] */
     int32_t source_dims[3];
     int32_t source_on_device;        /* source is a device pointer (copied d2d) */
+    /* optional image-valued Dirichlet data (2D, ABI 8), replacing dirichlet_value: g at a walk's
+       projection x onto the Dirichlet boundary is Image::get((x - x0) / ex, (y - y0) / ey)
+       (setTerminalContribution walk_on_stars.h:331-351 -> projectToDirichlet
+       fcpw_scene_loader.h:345-364 -> the upstream demo's pde.dirichlet, scene.h:202-207 commented
+       in the fork: x0, y0 = bbox.pMin, ex = ey = bbox.extent().maxCoeff(); image.h:53-58) */
+    const float *dirichlet_image;    /* [H][W] row-major, row ~ y; NULL: constant dirichlet_value */
+    int32_t dirichlet_image_dims[2]; /* H, W */
+    float dirichlet_image_box[4];    /* x0, y0, ex, ey: the rectangle the image covers */
+    int32_t dirichlet_image_on_device;
 } wos_scene_desc;
 
 typedef struct wos_scene wos_scene;

@@ -293,6 +293,7 @@ struct wos_scene {
   wos::DevScene dev{};
   float* d_source = nullptr;
   size_t source_cap = 0;  // floats
+  float* d_dimg = nullptr;  // image-valued Dirichlet data (wos_scene_desc.dirichlet_image)
   std::mutex mu;          // solve vs set_source on the same scene
 };
 
@@ -370,6 +371,16 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   if (d->source && check_source_dims(d->dim, d->source_dims, &nsrc) != WOS_OK)
     return fail(WOS_E_INVALID, "wos_scene_create: bad source dims");
   if (!(d->absorption >= 0.0f)) return fail(WOS_E_INVALID, "wos_scene_create: absorption must be >= 0");
+  size_t ndimg = 0;
+  if (d->dirichlet_image) {
+    if (d->dim != 2) return fail(WOS_E_INVALID, "wos_scene_create: dirichlet_image is 2D only");
+    if (d->dirichlet_image_dims[0] < 1 || d->dirichlet_image_dims[1] < 1 ||
+        (int64_t)d->dirichlet_image_dims[0] * d->dirichlet_image_dims[1] > (int64_t)1 << 28)
+      return fail(WOS_E_INVALID, "wos_scene_create: bad dirichlet_image dims");
+    if (!(d->dirichlet_image_box[2] > 0.0f) || !(d->dirichlet_image_box[3] > 0.0f))
+      return fail(WOS_E_INVALID, "wos_scene_create: dirichlet_image_box extent must be > 0");
+    ndimg = (size_t)d->dirichlet_image_dims[0] * d->dirichlet_image_dims[1];
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(WOS_E_DEVICE, "wos_scene_create: no HIP device available");
@@ -393,6 +404,18 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
       return fail(WOS_E_DEVICE, std::string("wos_scene_create: ") + hipGetErrorString(e));
     }
     s->source_cap = nsrc;
+  }
+  if (ndimg) {
+    hipError_t e = hipMalloc((void**)&s->d_dimg, ndimg * sizeof(float));
+    if (e == hipSuccess)
+      e = hipMemcpy(s->d_dimg, d->dirichlet_image, ndimg * sizeof(float),
+                    d->dirichlet_image_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      hipFree(s->d_dimg);
+      hipFree(s->d_source);
+      delete s;
+      return fail(WOS_E_DEVICE, std::string("wos_scene_create: ") + hipGetErrorString(e));
+    }
   }
   const wos::HostScene& h = geom->host;
   wos::DevScene& ds = s->dev;
@@ -426,6 +449,9 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   }
   ds.absorption = d->absorption;
   ds.g_dirichlet = d->dirichlet_value;
+  ds.dimg = s->d_dimg;
+  for (int k = 0; k < 2; k++) ds.ddims[k] = ndimg ? d->dirichlet_image_dims[k] : 0;
+  for (int k = 0; k < 4; k++) ds.dbox[k] = ndimg ? d->dirichlet_image_box[k] : 0.0f;
   ds.watertight = d->is_watertight;
   ds.double_sided = d->is_double_sided;
   *out = s;
@@ -469,6 +495,7 @@ int wos_scene_destroy(wos_scene* s) {
     std::lock_guard<std::mutex> lk(c.mu);
     if (c.inflight) hipEventSynchronize(c.done);  // an async solve may still read the source
     hipFree(s->d_source);
+    hipFree(s->d_dimg);
   }
   delete s;
   return WOS_OK;

@@ -403,9 +403,12 @@ __device__ __forceinline__ float lane_bcast(float v, int l) {
 // here the group with the smallest box bound is evaluated first (a tight running
 // minimum), then every other group whose bound does not exceed it, keeping
 // (min d^2, highest index) -- the same primitive, hence the same d.
-template <int DIM>
+//
+// PROJ = true also returns that primitive's closest point in proj[DIM]: projectToDirichlet
+// (fcpw_scene_loader.h:345-364) runs the same findClosestPoint scan.
+template <int DIM, bool PROJ = false>
 __device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, const float* dgroup,
-                                       const float* x) {
+                                       const float* x, float* proj = nullptr) {
   if (sc.n_dprims <= 0) return bbox_far_dist<DIM>(sc, x);
   constexpr int PS = Layout<DIM>::prim;
   const int ng = sc.n_dgroups;
@@ -422,7 +425,10 @@ __device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, c
         float pt[DIM], t0, t1;
         const float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
         const float d2 = d * d;
-        if (d2 < sr2 || (d2 == sr2 && p > bestp)) { sr2 = d2; best = d; bestp = p; }
+        if (d2 < sr2 || (d2 == sr2 && p > bestp)) {
+          sr2 = d2; best = d; bestp = p;
+          if constexpr (PROJ) for (int k = 0; k < DIM; k++) proj[k] = pt[k];
+        }
       }
     };
     {
@@ -465,7 +471,10 @@ __device__ float dirichlet_dist_culled(const DevScene& sc, const float* dprim, c
       float pt[DIM], t0, t1;
       const float d = cp_prim<DIM>(dprim + p * PS, x, pt, &t0, &t1);
       const float d2 = d * d;
-      if (d2 < sr2 || (d2 == sr2 && p > bestp)) { sr2 = d2; best = d; bestp = p; }
+      if (d2 < sr2 || (d2 == sr2 && p > bestp)) {
+        sr2 = d2; best = d; bestp = p;
+        if constexpr (PROJ) for (int k = 0; k < DIM; k++) proj[k] = pt[k];
+      }
     }
   }
   return best;
@@ -845,6 +854,28 @@ __device__ __forceinline__ float source_value(const DevScene& sc, const float* x
     int k = sclamp(cvt_trunc(uz * (float)Z), 0, Z - 1);
     return sc.source[((size_t)i * Y + j) * Z + k];
   }
+}
+
+// g at the position x where a walk reached the Dirichlet shell (setTerminalContribution,
+// walk_on_stars.h:331-351): the constant, or -- image-valued data, 2D -- the image over
+// sc.dbox at x's projection onto the Dirichlet boundary (projectToDirichlet,
+// fcpw_scene_loader.h:345-364), looked up as Image::get (image.h:53-58) with the uv of the
+// upstream demo's pde.dirichlet (scene.h:202-207).  Once per walk that reaches the shell.
+template <int DIM>
+__device__ float dirichlet_value(const DevScene& sc, const float* x) {
+  if constexpr (DIM == 2) {
+    if (sc.dimg != nullptr && sc.n_dprims > 0) {
+      float proj[2] = {x[0], x[1]};
+      dirichlet_dist_culled<DIM, true>(sc, sc.dprim, sc.dgroup, x, proj);
+      const float ux = (proj[0] - sc.dbox[0]) / sc.dbox[2];
+      const float uy = (proj[1] - sc.dbox[1]) / sc.dbox[3];
+      const int h = sc.ddims[0], w = sc.ddims[1];
+      const int i = sclamp(cvt_trunc(uy * (float)h), 0, h - 1);
+      const int j2 = sclamp(cvt_trunc(ux * (float)w), 0, w - 1);
+      return sc.dimg[(size_t)i * w + j2];
+    }
+  }
+  return sc.g_dirichlet;
 }
 
 template <int DIM>
@@ -3400,7 +3431,7 @@ __device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams&
   flush_source<DIM>(st);
   const bool recorded = code == WC_DIRICHLET || code == WC_RR;
   if (recorded) {
-    const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? sc.g_dirichlet : 0.0f;
+    const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? dirichlet_value<DIM>(sc, st.pt) : 0.0f;
     tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
   }
   tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);

@@ -81,6 +81,11 @@ struct DevScene {
   float pmin[3], pmax[3], ext[3];
   float absorption;
   float g_dirichlet;
+  // image-valued Dirichlet data (wos_scene_desc.dirichlet_image; nullptr: g_dirichlet):
+  // [ddims[0]][ddims[1]] over the rectangle dbox = (x0, y0, ex, ey)
+  const float* dimg;
+  int32_t ddims[2];
+  float dbox[4];
   int32_t watertight;
   int32_t double_sided;
   // star-radius cell grid (wos_host_scene.h StarGrid; nullptr: none): u16 cell

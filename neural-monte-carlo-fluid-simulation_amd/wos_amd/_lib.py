@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 7  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 8  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_E_CAPACITY = -4
 WOS_PTRS_DEVICE = 0x1
@@ -35,6 +35,8 @@ class SceneDesc(C.Structure):
         ("dirichlet_value", C.c_float), ("absorption", C.c_float),
         ("is_watertight", C.c_int32), ("is_double_sided", C.c_int32),
         ("source", C.c_void_p), ("source_dims", C.c_int32 * 3), ("source_on_device", C.c_int32),
+        ("dirichlet_image", C.c_void_p), ("dirichlet_image_dims", C.c_int32 * 2),
+        ("dirichlet_image_box", C.c_float * 4), ("dirichlet_image_on_device", C.c_int32),
     ]
 
 

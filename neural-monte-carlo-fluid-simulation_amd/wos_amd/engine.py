@@ -99,7 +99,12 @@ class WosScene:
     """Geometry + source field resident on one GPU."""
 
     def __init__(self, vertices, prims, source=None, absorption=0.0, *, dvertices=None, dprims=None,
-                 dirichlet_value=0.0, watertight=True, double_sided=False, device=0):
+                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, watertight=True,
+                 double_sided=False, device=0):
+        """dirichlet_image (2D, optional): g as an image [H, W] (row ~ y) over the rectangle
+        dirichlet_image_box = (x0, y0, ex, ey), evaluated at each walk's projection onto the
+        Dirichlet boundary (the upstream demo's pde.dirichlet, scene.h:202-207); replaces the
+        constant dirichlet_value."""
         L = _lib.load()
         v = np.ascontiguousarray(vertices, dtype=np.float32)
         ix = np.ascontiguousarray(prims, dtype=np.int32)
@@ -120,6 +125,23 @@ class WosScene:
             d.n_dvertices, d.n_dprims = dv.shape[0], dix.shape[0]
             keep += [dv, dix]
         d.dirichlet_value = float(dirichlet_value)
+        if dirichlet_image is not None:
+            if dirichlet_image_box is None or len(dirichlet_image_box) != 4:
+                raise WosError("dirichlet_image needs dirichlet_image_box = (x0, y0, ex, ey)")
+            if _is_torch(dirichlet_image) and dirichlet_image.is_cuda:
+                dimg = dirichlet_image.detach().to(dtype=__import__("torch").float32).contiguous()
+                d.dirichlet_image, d.dirichlet_image_on_device = dimg.data_ptr(), 1
+            else:
+                if _is_torch(dirichlet_image):
+                    dirichlet_image = dirichlet_image.detach().cpu().numpy()
+                dimg = np.ascontiguousarray(dirichlet_image, dtype=np.float32)
+                d.dirichlet_image = dimg.ctypes.data
+            if len(dimg.shape) != 2:
+                raise WosError(f"dirichlet_image must be 2-D, got shape {tuple(dimg.shape)}")
+            d.dirichlet_image_dims[0], d.dirichlet_image_dims[1] = int(dimg.shape[0]), int(dimg.shape[1])
+            for k in range(4):
+                d.dirichlet_image_box[k] = float(dirichlet_image_box[k])
+            keep.append(dimg)
         d.absorption = float(absorption)
         d.is_watertight = int(bool(watertight))
         d.is_double_sided = int(bool(double_sided))

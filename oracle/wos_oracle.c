@@ -1017,6 +1017,7 @@ typedef struct {
     float g_dirichlet, absorption;
     int watertight, double_sided;
     const float *src; int sdims[3];
+    const float *dimg; int ddims[2]; float dbox[4];
 } scene_t;
 
 static int scene_build(scene_t *sc, const oracle_scene_desc *d)
@@ -1042,6 +1043,13 @@ static int scene_build(scene_t *sc, const oracle_scene_desc *d)
     sc->watertight = d->is_watertight; sc->double_sided = d->is_double_sided;
     sc->src = d->source;
     for (int k = 0; k < 3; k++) sc->sdims[k] = d->source_dims[k];
+    if (d->dirichlet_image) {
+        if (d->dim != 2 || d->dirichlet_image_dims[0] < 1 || d->dirichlet_image_dims[1] < 1) return -1;
+        sc->dimg = d->dirichlet_image;
+        sc->ddims[0] = d->dirichlet_image_dims[0]; sc->ddims[1] = d->dirichlet_image_dims[1];
+        for (int k = 0; k < 4; k++) sc->dbox[k] = d->dirichlet_image_box[k];
+        if (!(sc->dbox[2] > 0.0f) || !(sc->dbox[3] > 0.0f)) return -1;
+    }
     return 0;
 }
 
@@ -1116,6 +1124,26 @@ static float source_value(const scene_t *sc, const float *x)
     int j = sclampi(cvt_trunc(uy * (float)Y), 0, Y - 1);
     int k = sclampi(cvt_trunc(uz * (float)Z), 0, Z - 1);
     return sc->src[((size_t)i * Y + j) * Z + k];
+}
+
+/* ------------------------------------------------------------------------- */
+/* g at a walk's last position: setTerminalContribution (walk_on_stars.h:331-351) projects it
+ * onto the Dirichlet boundary (projectToDirichlet, fcpw_scene_loader.h:345-364: findClosestPoint,
+ * the same `<=` scan as computeDistToDirichlet) and evaluates pde.dirichlet there: the upstream
+ * setPDE the fork keeps commented (scene.h:202-207), uv = (x - pMin) / maxLength -- here
+ * (x - box origin) / box extent per axis, which is that with extent = (maxLength, maxLength) --
+ * then Image::get (image.h:53-58: i = clamp(int(uv.y * h)), j = clamp(int(uv.x * w))). */
+static float dirichlet_value(const scene_t *sc, const float *x)
+{
+    if (!sc->dimg) return sc->g_dirichlet;
+    cp_t c;
+    if (closest_point(&sc->dir, x, &c, 0) < 0) return sc->g_dirichlet;
+    float ux = (c.p[0] - sc->dbox[0]) / sc->dbox[2];
+    float uy = (c.p[1] - sc->dbox[1]) / sc->dbox[3];
+    int h = sc->ddims[0], w = sc->ddims[1];
+    int i = sclampi(cvt_trunc(uy * (float)h), 0, h - 1);
+    int j = sclampi(cvt_trunc(ux * (float)w), 0, w - 1);
+    return sc->dimg[(size_t)i * w + j];
 }
 
 /* ------------------------------------------------------------------------- */
@@ -1720,7 +1748,7 @@ static void estimate_point(const scene_t *sc, const oracle_params *prm, const fl
             pc->iters += wc.iters;
             uint64_t total_steps = stepsBefore + wc.steps;
             if (code == WC_DIRICHLET || code == WC_RR) {
-                st.terminal = (code == WC_DIRICHLET && !prm->ignore_dirichlet) ? sc->g_dirichlet : 0.0f;
+                st.terminal = (code == WC_DIRICHLET && !prm->ignore_dirichlet) ? dirichlet_value(sc, st.pt) : 0.0f;
                 float total = st.throughput * st.terminal + st.totalNeumann + st.totalSource;
                 float bc = total - st.firstSource;
                 float ge[3];
@@ -1755,7 +1783,7 @@ static void estimate_point(const scene_t *sc, const oracle_params *prm, const fl
 typedef struct {
     const scene_t *sc; const oracle_params *prm;
     const float *pts; int64_t n, base, stride;
-    float *p, *grad; int32_t *n_est, *steps;
+    float *p, *grad; int32_t *n_est, *steps; float *sol_m2;
     atomic_llong next;
     pthread_mutex_t mu;
     oracle_stats tot;
@@ -1782,6 +1810,7 @@ static void solve_one(job_t *J, int64_t i, pcount_t *pc, uint64_t *nest)
     J->p[i] = maskP ? 0.0f : (estimated ? S.solMean : 0.0f);
     for (int k = 0; k < dim; k++) J->grad[i * dim + k] = maskG ? 0.0f : (estimated ? S.gMean[k] : 0.0f);
     if (J->n_est) J->n_est[i] = S.nSol;
+    if (J->sol_m2) J->sol_m2[i] = S.solM2;
     if (J->steps) J->steps[i] = (int32_t)((pc->steps - before.steps) + (pc->wasted - before.wasted));
 }
 
@@ -1812,6 +1841,14 @@ int oracle_solve(const oracle_scene_desc *scene, const oracle_params *prm,
                  const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
                  float *p, float *grad, int32_t *n_est, int32_t *steps, oracle_stats *stats)
 {
+    return oracle_solve_m2(scene, prm, pts, n, index_base, index_stride, p, grad, n_est, steps, NULL, stats);
+}
+
+int oracle_solve_m2(const oracle_scene_desc *scene, const oracle_params *prm,
+                    const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
+                    float *p, float *grad, int32_t *n_est, int32_t *steps, float *sol_m2,
+                    oracle_stats *stats)
+{
     if (!scene || !prm || (n > 0 && (!pts || !p || !grad))) return -1;
     if (prm->n_walks < 1) return -2;
     scene_t sc;
@@ -1820,7 +1857,7 @@ int oracle_solve(const oracle_scene_desc *scene, const oracle_params *prm,
     if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
     job_t J; memset(&J, 0, sizeof(J));
     J.sc = &sc; J.prm = prm; J.pts = pts; J.n = n; J.base = index_base; J.stride = index_stride;
-    J.p = p; J.grad = grad; J.n_est = n_est; J.steps = steps;
+    J.p = p; J.grad = grad; J.n_est = n_est; J.steps = steps; J.sol_m2 = sol_m2;
     atomic_init(&J.next, 0);
     pthread_mutex_init(&J.mu, NULL);
     int nt = prm->n_threads > 0 ? prm->n_threads : 1;

@@ -40,6 +40,14 @@ typedef struct oracle_scene_desc {
     /* source grid: 2D (h=dims[0] rows ~ y, w=dims[1] cols ~ x); 3D (X,Y,Z) */
     const float *source;
     int32_t source_dims[3];
+    /* optional image-valued Dirichlet data g (2D): [h][w] row-major, row ~ y, covering the
+       rectangle dirichlet_image_box = {x0, y0, ex, ey}: g(x) = Image::get((x - x0) / ex,
+       (y - y0) / ey) (image.h:53-58) at the walk's projection onto the Dirichlet boundary, as
+       the upstream demo's setPDE did (scene.h:202-207, commented in the fork: x0, y0 = bbox.pMin,
+       ex = ey = bbox.extent().maxCoeff()); NULL: the constant dirichlet_value */
+    const float *dirichlet_image;
+    int32_t dirichlet_image_dims[2];
+    float dirichlet_image_box[4];
 } oracle_scene_desc;
 
 typedef struct oracle_params {
@@ -84,6 +92,14 @@ int oracle_solve(const oracle_scene_desc *scene, const oracle_params *prm,
                  const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
                  float *p, float *grad, int32_t *n_est, int32_t *steps,
                  oracle_stats *stats);
+
+/* oracle_solve plus the per-point Welford M2 of the solution estimates (sol_m2[n], may be
+ * NULL; the sample variance is sol_m2 / (n_est - 1), SampleStatistics walk_on_stars.h:744-877)
+ * -- for the statistical pin against the reference's own engine solution. */
+int oracle_solve_m2(const oracle_scene_desc *scene, const oracle_params *prm,
+                    const float *pts, int64_t n, int64_t index_base, int64_t index_stride,
+                    float *p, float *grad, int32_t *n_est, int32_t *steps, float *sol_m2,
+                    oracle_stats *stats);
 
 /* Boundary value caching: runBoundaryValueCaching (bindings/zombie/demo/demo.cpp:
  * 265-363), 2D all-Neumann scenes.  Outputs as wos_bvc (include/wos.h). */

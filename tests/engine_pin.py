@@ -1,22 +1,16 @@
-"""Helpers for the pin against the reference's own engine-scene outputs
-(tests/golden/engine_solution_masks.npz, made by tests/golden/make_engine_mask.py
-from bindings/zombie/demo/scenes/engine/solutions/{wost,bvc}.pfm).
+"""Helpers for the pin against the reference's own engine-demo outputs
+(bindings/zombie/demo/scenes/engine/solutions/{wost,bvc}.pfm, stored with the demo's boundary
+images in tests/golden/engine_scene.npz by tests/golden/make_engine_scene.py).
 
-The reference ran its grid demo on scenes/engine/data/geometry.obj (byte-identical to
-scenes/engine_geometry.obj here) with Scene(json)'s defaults flipOrientation = true,
-isWatertight = true (scene.h:22-33) and output.boundaryDistanceMask = 1e-2
-(scenes/engine/wost.json, bvc.json).  Its writer zeroes a grid point when
-    (!insideDomain(pt) && !isDoubleSided) || min(|dDist|, |nDist|) < boundaryDistanceMask
-(grid.h:316-319, 407-409).  Which pixels that rule zeroes depends only on the geometry
-conventions (OBJ winding + flip, FLT_EPSILON-padded bbox, segment / vertex normals,
-the inside test, closest distances) and on the writer's orientation -- not on the
-estimator.  The solution values themselves need the upstream mixed-boundary scene,
-which this fork no longer builds (scene.h:28-30,43-45), so they are not compared.
-
-A point is "masked" here when the solve returns grad == (0, 0): getGradient zeroes
-exactly (!inside && !doubleSided) || |nDist| < mask (grid.h:227-228), and with no
-Dirichlet geometry dDist is the bbox far-corner distance (fcpw_scene_loader.h:312-314),
-far above the mask, so the two rules coincide.
+The upstream demo solved scenes/engine/wost.json on data/geometry.obj (byte-identical to
+scenes/engine_geometry.obj here) with a Scene that the fork has since changed: its boundary was
+split into Dirichlet and Neumann parts by data/is_neumann.png, g came from
+data/dirichlet_boundary_value.pfm, the domain was normalised (normalizeDomain, scene.h:132-142)
+and its bounding box was square (computeBoundingBox(..., makeSquare = true, ...)).  Rebuilt with
+those conventions (upstream_scene below; DESIGN.md "What pins the oracle" 4), the writer's zeroing
+rule (grid.h:316-319: outside, or within boundaryDistanceMask = 1e-2 of either boundary) reproduces
+the zero pattern of both images pixel for pixel, and the estimator's values agree with wost.pfm
+within its own Monte-Carlo error (96 walks).
 """
 import os
 
@@ -24,38 +18,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENGINE_OBJ = os.path.join(REPO, "scenes", "engine_geometry.obj")
-FIXTURE = os.path.join(REPO, "tests", "golden", "engine_solution_masks.npz")
-MASK = 1e-2
-# the solver settings only have to produce a non-zero gradient wherever the writer
-# keeps a value: a tiny absorption (mu R <= 14 on this 1000-unit scene) and roulette
-# end every walk after a few steps; a positive random source without antithetic or
-# control variates makes every estimated gradient non-zero
-SOLVER = {"nWalks": 2, "maxWalkLength": 1024, "russianRouletteThreshold": 0.99,
-          "setpsBeforeApplyingTikhonov": 0, "ignoreDirichlet": True, "ignoreNeumann": True,
-          "ignoreSource": False, "disableGradientAntitheticVariates": True,
-          "disableGradientControlVariates": True}
-OUTPUT = {"gridRes": 256, "boundaryDistanceMask": MASK}
-ABSORPTION = 1e-4
-# residual allowed against the reference's images (see DESIGN.md "What pins the oracle")
-MAX_RESIDUAL = 89
-RESIDUAL_BAND = 1.25  # grid spacings
-
-
-def source_grid():
-    return np.random.default_rng(11).uniform(0.5, 1.5, (64, 64)).astype(np.float32)
-
-
-def fixture():
-    d = np.load(FIXTURE)
-    g = int(d["grid_res"])
-    return {k: np.unpackbits(d[k + "_nonzero_bits"])[:g * g].reshape(g, g).astype(bool)
-            for k in ("wost", "bvc")}, g
-
-
-def load_geometry():
-    """Scene(json) defaults: flipOrientation = true (scene.h:33, loadOBJ :123-124)."""
-    from wos_amd import engine
-    return engine.load_obj(ENGINE_OBJ, 2, True, False)
+SCENE_FIXTURE = os.path.join(REPO, "tests", "golden", "engine_scene.npz")
+MASK = 1e-2  # scenes/engine/wost.json output.boundaryDistanceMask
 
 
 def bbox(v):
@@ -65,16 +29,14 @@ def bbox(v):
     return (v - eps).min(0).astype(np.float32), (v + eps).max(0).astype(np.float32)
 
 
-def grid_points(v, g):
+def grid_points(lo, hi, g):
     """createSolutionGrid (grid.h:35-52): point idx = i*g + j at
     ((i / float(g)) * extent.x + bMin.x, (j / float(g)) * extent.y + bMin.y), in float."""
-    lo, hi = bbox(v)
     ext = (hi - lo).astype(np.float32)
     t = (np.arange(g, dtype=np.float32) / np.float32(g)).astype(np.float32)
-    x = (t * ext[0]).astype(np.float32) + lo[0]
-    y = (t * ext[1]).astype(np.float32) + lo[1]
-    X, Y = np.meshgrid(x, y, indexing="ij")
-    return np.stack([X.ravel(), Y.ravel()], 1).astype(np.float32), ext
+    X, Y = np.meshgrid((t * ext[0]).astype(np.float32) + lo[0], (t * ext[1]).astype(np.float32) + lo[1],
+                       indexing="ij")
+    return np.stack([X.ravel(), Y.ravel()], 1).astype(np.float32)
 
 
 def boundary_distance(v, ix, pts):
@@ -83,8 +45,7 @@ def boundary_distance(v, ix, pts):
     a, b = v[ix[:, 0]], v[ix[:, 1]]
     d = b - a
     dd = (d * d).sum(1)
-    deg = dd == 0
-    dd[deg] = 1.0
+    dd[dd == 0] = 1.0
     out = np.empty(len(pts))
     for s in range(0, len(pts), 2048):
         p = pts[s:s + 2048, None, :].astype(np.float64)
@@ -94,16 +55,111 @@ def boundary_distance(v, ix, pts):
     return out
 
 
-def compare(masked, nonzero, v, ix, pts, ext, g):
-    """Pass rule: every pixel the engine masks is zero in the reference image, except
-    a residual of at most MAX_RESIDUAL pixels, each within RESIDUAL_BAND grid spacings
-    of the boundary.  Returns a report dict."""
-    masked = masked.reshape(g, g)
-    bad = masked & nonzero
-    report = {"masked": int(masked.sum()), "fixture_nonzero": int(nonzero.sum()),
-              "masked_but_nonzero": int(bad.sum()),
-              "unmasked_zero": int((~masked & ~nonzero).sum())}
-    if bad.any():
-        dist = boundary_distance(v, ix, pts.reshape(g, g, 2)[bad])
-        report["residual_max_dist_spacings"] = float(dist.max() / float(max(ext) / g))
-    return report
+# ---------------------------------------------------------------------------------------------
+# The value-level pin: the upstream engine demo's own scene (tests/golden/make_engine_scene.py)
+# ---------------------------------------------------------------------------------------------
+# scenes/engine/wost.json:3-11 as the solver reads it (demo.cpp:121-137): 96 walks,
+# maxWalkLength 1024, epsilonShell 1e-3, harmonic (no absorptionCoeff), Dirichlet on, Neumann and
+# source terms off; "minStarShapedRadius" is not a key the solver reads (minStarRadius keeps 1e-3)
+WOST_SOLVER = {"nWalks": 96, "maxWalkLength": 1024, "epsilonShell": 1e-3, "minStarShapedRadius": 1e-3,
+               "ignoreDirichlet": False, "ignoreNeumann": True, "ignoreSource": True}
+WOST_OUTPUT = {"gridRes": 256, "boundaryDistanceMask": MASK}
+WOST_WALKS = 96
+
+
+def scene_fixture():
+    d = np.load(SCENE_FIXTURE)
+    n = int(d["is_neumann_shape"][0]) * int(d["is_neumann_shape"][1])
+    out = {k: d[k] for k in ("dirichlet_image", "wost_values", "bvc_values")}
+    out["is_neumann"] = np.unpackbits(d["is_neumann_bits"])[:n].reshape(d["is_neumann_shape"]).astype(bool)
+    return out
+
+
+def _subset(v, ix, sel):
+    """separateBoundaries (upstream, restated): the selected segments in order, their vertices
+    renumbered in order of first use -- each boundary type gets its own mesh and therefore its
+    own vertex normals and silhouettes (scene.h:151-153)."""
+    remap, vv, out = {}, [], []
+    for a, b in ix[sel]:
+        for q in (a, b):
+            if q not in remap:
+                remap[q] = len(vv)
+                vv.append(v[q])
+        out.append((remap[a], remap[b]))
+    return np.asarray(vv, np.float32).reshape(-1, 2), np.asarray(out, np.int32).reshape(-1, 2)
+
+
+def square_bbox(v):
+    """computeBoundingBox(vertices, makeSquare = true, 1.0) (fcpw_scene_loader.h:75-93) in float:
+    the FLT_EPSILON-padded box, then centre +- 0.5 * extent.maxCoeff() (centroid() =
+    (pMin + pMax) * 0.5f, bounding_volumes.h:130-132)."""
+    lo, hi = bbox(v)
+    c = ((lo + hi) * np.float32(0.5)).astype(np.float32)
+    half = np.float32(np.float32(0.5) * (hi - lo).astype(np.float32).max())
+    return (c - half).astype(np.float32), (c + half).astype(np.float32)
+
+
+def image_lookup(img, pts, origin, extent):
+    """Image::get(uv) (image.h:53-58) at uv = (x - origin) / extent, in float."""
+    uv = ((np.asarray(pts, np.float32) - origin) / extent).astype(np.float32)
+    h, w = img.shape
+    i = np.clip((uv[:, 1] * np.float32(h)).astype(np.int64), 0, h - 1)
+    j = np.clip((uv[:, 0] * np.float32(w)).astype(np.int64), 0, w - 1)
+    return img[i, j]
+
+
+def upstream_scene(load_obj=None, normalize=True, square=True, flip=True):
+    """The scene the upstream engine demo solved (DESIGN.md "What pins the oracle" 4): the OBJ
+    loaded as the upstream Scene(json) did -- flipOrientation and normalizeDomain on (the OBJ
+    recentred and scaled to unit radius, scene.h:132-142) and a SQUARE bounding box
+    (computeBoundingBox(vertices, true, 1.0); the fork passes false, scene.h:144) -- split by
+    onNeumannBoundary at the segment midpoints (scene.h:79-82 with that box), and g from the
+    Dirichlet image over the same box (uv = (x - pMin) / maxLength, scene.h:202-207).
+    normalize / square / flip = False give the fork's conventions instead (negative controls).
+    Returns a dict: neumann / dirichlet meshes (v, ix), dirichlet_image, box (x0, y0, ex, ey),
+    pts (the 256^2 createSolutionGrid points over the square box, point i*256 + j),
+    values (the reference's wost.pfm, flattened the same way)."""
+    if load_obj is None:
+        from wos_amd import engine
+        load_obj = engine.load_obj
+    fx = scene_fixture()
+    v, ix = load_obj(ENGINE_OBJ, 2, flip, normalize)
+    lo, hi = square_bbox(v) if square else bbox(v)
+    ext = (hi - lo).astype(np.float32)
+    max_len = np.float32(ext.max())
+    mid = (np.float32(0.5) * (v[ix[:, 0]] + v[ix[:, 1]])).astype(np.float32)
+    neu = image_lookup(fx["is_neumann"].astype(np.float32), mid, lo, max_len) > 0
+    g = int(fx["wost_values"].shape[0])
+    pts = grid_points(lo, hi, g)
+    return {"neumann": _subset(v, ix, neu), "dirichlet": _subset(v, ix, ~neu),
+            "n_neumann": int(neu.sum()), "dirichlet_image": fx["dirichlet_image"],
+            "box": np.array([lo[0], lo[1], max_len, max_len], np.float32), "pts": pts,
+            "values": fx["wost_values"].ravel(), "bvc_values": fx["bvc_values"].ravel(), "grid_res": g,
+            "v": v, "ix": ix}
+
+
+def near_boundary(v, ix, pts, r):
+    """dist(pt, polyline) < r for every point (float64 distances): candidate pairs from a k-d
+    tree over the points, around each segment's midpoint, then the exact segment distance."""
+    from scipy.spatial import cKDTree
+    v = v.astype(np.float64)
+    P = np.asarray(pts, np.float64)
+    a, b = v[ix[:, 0]], v[ix[:, 1]]
+    half = 0.5 * np.linalg.norm(b - a, axis=1)
+    tree = cKDTree(P)
+    out = np.zeros(len(P), bool)
+    for s, cands in enumerate(tree.query_ball_point(0.5 * (a + b), half + r)):
+        if not cands:
+            continue
+        q = P[cands]
+        d = b[s] - a[s]
+        dd = float(d @ d)
+        t = np.clip(((q - a[s]) @ d) / dd, 0.0, 1.0) if dd > 0 else np.zeros(len(q))
+        out[np.asarray(cands)[np.linalg.norm(q - (a[s] + t[:, None] * d), axis=1) < r]] = True
+    return out
+
+
+def writer_mask(inside, near_dirichlet, near_neumann):
+    """saveSolutionGrid's zeroing rule (grid.h:316-319): outside, or within the mask distance
+    (output.boundaryDistanceMask) of either boundary."""
+    return ~inside | near_dirichlet | near_neumann

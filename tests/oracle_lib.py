@@ -23,6 +23,8 @@ class SceneDesc(C.Structure):
         ("dirichlet_value", C.c_float), ("absorption", C.c_float),
         ("is_watertight", C.c_int32), ("is_double_sided", C.c_int32),
         ("source", C.POINTER(C.c_float)), ("source_dims", C.c_int32 * 3),
+        ("dirichlet_image", C.POINTER(C.c_float)), ("dirichlet_image_dims", C.c_int32 * 2),
+        ("dirichlet_image_box", C.c_float * 4),
     ]
 
 
@@ -77,6 +79,10 @@ def lib():
         L.oracle_solve.argtypes = [C.POINTER(SceneDesc), C.POINTER(Params), C.c_void_p, C.c_int64,
                                    C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.POINTER(Stats)]
+        L.oracle_solve_m2.restype = C.c_int
+        L.oracle_solve_m2.argtypes = [C.POINTER(SceneDesc), C.POINTER(Params), C.c_void_p, C.c_int64,
+                                      C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.POINTER(Stats)]
         L.oracle_point_info.restype = C.c_int
         L.oracle_point_info.argtypes = [C.POINTER(SceneDesc), C.c_void_p] + [C.c_void_p] * 6
         L.oracle_bessel.restype = C.c_double
@@ -112,7 +118,8 @@ class OracleScene:
     """Keeps numpy buffers alive for the SceneDesc pointers."""
 
     def __init__(self, vertices, prims, source, absorption, *, dvertices=None, dprims=None,
-                 dirichlet_value=0.0, watertight=True, double_sided=False):
+                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, watertight=True,
+                 double_sided=False):
         self.v = np.ascontiguousarray(vertices, dtype=np.float32)
         self.ix = np.ascontiguousarray(prims, dtype=np.int32)
         self.dim = int(self.v.shape[1])
@@ -134,6 +141,12 @@ class OracleScene:
         dims = list(self.src.shape) + [0] * (3 - self.src.ndim)
         for k in range(3):
             d.source_dims[k] = dims[k]
+        self.dimg = None if dirichlet_image is None else np.ascontiguousarray(dirichlet_image, dtype=np.float32)
+        if self.dimg is not None:
+            d.dirichlet_image = _fptr(self.dimg)
+            d.dirichlet_image_dims[0], d.dirichlet_image_dims[1] = self.dimg.shape
+            for k in range(4):
+                d.dirichlet_image_box[k] = float(dirichlet_image_box[k])
         self.desc = d
 
 
@@ -175,19 +188,25 @@ def default_threads():
     return max(1, n)
 
 
-def solve(scene: OracleScene, params: Params, pts, index_base=0, index_stride=1):
+def solve(scene: OracleScene, params: Params, pts, index_base=0, index_stride=1, m2=False):
+    """(p, grad, n_est, steps, stats); with m2=True also the per-point Welford M2 of the
+    solution estimates (sample variance = m2 / (n_est - 1)) as a sixth element."""
     pts = np.ascontiguousarray(pts, dtype=np.float32)
     n = pts.shape[0]
     p = np.zeros(n, np.float32)
     g = np.zeros((n, scene.dim), np.float32)
     nest = np.zeros(n, np.int32)
     steps = np.zeros(n, np.int32)
+    sm2 = np.zeros(n, np.float32) if m2 else None
     st = Stats()
-    rc = lib().oracle_solve(C.byref(scene.desc), C.byref(params), pts.ctypes.data, n,
-                            index_base, index_stride, p.ctypes.data, g.ctypes.data,
-                            nest.ctypes.data, steps.ctypes.data, C.byref(st))
+    rc = lib().oracle_solve_m2(C.byref(scene.desc), C.byref(params), pts.ctypes.data, n,
+                               index_base, index_stride, p.ctypes.data, g.ctypes.data,
+                               nest.ctypes.data, steps.ctypes.data,
+                               sm2.ctypes.data if m2 else None, C.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle_solve failed rc={rc}")
+    if m2:
+        return p, g, nest, steps, st.as_dict(), sm2
     return p, g, nest, steps, st.as_dict()
 
 

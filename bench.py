@@ -18,7 +18,8 @@ N x 64k projection; "strong" (default for the grid configs C, D, E -- BASELINE's
 Config B's line carries both views: `value` (weak) and a `strong` object (the fixed
 65398-point projection stride-sharded over the N ranks + its all-gather); at N=1 it
 also times `strong_shard_ms`, the 1/8 stride shard rank 0 of an 8-GPU strong run
-solves, alone on this GPU (the per-rank latency that bounds 8-GPU strong scaling).
+solves, alone on this GPU (the per-rank latency that bounds 8-GPU strong scaling); the
+strong-scaled configs (C, D, E) carry the same `strong_shard` for their own point sets.
 
 Prints ONE JSON line on rank 0.  `value` counts the ball steps of recorded walks
 (the first ball + every walk() iteration, walk_on_stars.h:523,182); steps of
@@ -58,8 +59,8 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-projection-wall", action="store_true")
     ap.add_argument("--no-strong", action="store_true",
-                    help="config B: skip the strong line and the stride-8 shard (profiling passes that must "
-                         "see the weak workload's launches only)")
+                    help="skip the strong line (config B) and the stride-8 shard (profiling passes that must "
+                         "see the main workload's launches only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the product path); gloo stages the all-gather through host "
                          "memory and lets N ranks share one GPU (tests/test_bench_dist.py)")
@@ -276,11 +277,10 @@ def strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, work
             "note": "fixed point set (total work fixed as N grows), stride-sharded, + 1 RCCL all-gather"}
 
 
-def shard_projection(a, scene, params, dim, torch, dev, workloads, shards=8):
-    """One GPU timing the 1/8 stride shard an 8-GPU strong-scaled projection of config B
-    gives rank 0 (points 0, 8, 16, ... with their global RNG indices): the per-rank
-    latency floor that bounds 8-GPU strong scaling."""
-    pts = workloads.config_by_name("B")["points"]
+def shard_projection(a, scene, params, pts, torch, dev, shards=8):
+    """One GPU timing the 1/8 stride shard an 8-GPU strong-scaled projection of the config's
+    fixed point set gives rank 0 (points 0, 8, 16, ... with their global RNG indices): the
+    per-rank latency floor that bounds 8-GPU strong scaling."""
     x = torch.from_numpy(np.ascontiguousarray(pts[0::shards])).to(dev)
     elapsed, stats = timed_projections(scene, x, params, 0, shards, a.steps, a.warmup, a.blocking,
                                        1, None, torch)
@@ -347,7 +347,10 @@ def main():
     if a.config == "B" and scaling == "weak" and not a.no_strong:
         strong = strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, workloads)
         if world == 1:
-            shard = shard_projection(a, scene, params, dim, torch, dev, workloads)
+            shard = shard_projection(a, scene, params, workloads.config_by_name("B")["points"], torch, dev)
+    elif scaling == "strong" and world == 1 and not a.no_strong and a.config != "A":
+        # the fixed-size configs BASELINE runs on 8 GPUs (D, E; C alike): rank 0's 1/8 shard
+        shard = shard_projection(a, scene, params, pts_all, torch, dev)
 
     if rank == 0:
         kms = float(np.mean(kernel_ms))
@@ -414,8 +417,8 @@ def main():
             full_ms = elapsed / a.steps * 1e3
             line["strong_shard_ms"] = shard["ms"]
             line["strong_shard"] = dict(shard, full_ms=full_ms, implied_8gpu_speedup=full_ms / shard["ms"],
-                                        note="rank 0's share of an 8-GPU strong-scaled config B projection, "
-                                             "timed alone on this GPU (all-gather excluded)")
+                                        note=f"rank 0's share of an 8-GPU strong-scaled config {a.config} "
+                                             "projection, timed alone on this GPU (all-gather excluded)")
         if sq:
             line["valu_issue"] = {"kernel": sq["kernel"], "frac": sq["valu_issue_frac"],
                                   "wait_any_frac": sq["wait_any_frac"], "wait_inst_frac": sq["wait_inst_frac"],

@@ -660,7 +660,7 @@ int fill_stats(const StatSlot& q, wos_stats* stats) {
 // grid of the solver's precision / minR (if it fits), the Dirichlet primitives.
 struct WalkLayout {
   wos::DevScene dsc;          // the scene with its star grid (or none)
-  int geom_floats = 0;        // Neumann records + culling boxes (what the first-ball kernel stages)
+  int geom_floats = 0;        // Neumann records + culling boxes
   int geom_floats_walk = 0;   // + the star grid + the Dirichlet records (the walk kernel)
   size_t shmem_walk = 0;      // dynamic LDS of a walk-kernel workgroup
 };
@@ -786,15 +786,14 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     dp.rej_tab = c.d_rejtab;
   }
 
-  // LDS: staged geometry (+ per wave: stratified samples and their shuffle partners
-  // in the first-ball kernel)
+  // LDS: the walk kernel's staged geometry; per wave, the first-ball kernel's stratified
+  // samples and their shuffle partners
   WalkLayout wl;
   {
     int rc = walk_layout(s, prm, wl);
     if (rc != WOS_OK) return rc;
   }
   wos::DevScene dsc = wl.dsc;
-  const int geom_floats = wl.geom_floats;
   int geom_floats_walk = wl.geom_floats_walk;
   size_t shmem_walk = wl.shmem_walk;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
@@ -803,16 +802,19 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   // scenes beyond the LDS budget (or WOS_SCHED_GEOM_GLOBAL): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
-  if ((prm->schedule & WOS_SCHED_GEOM_GLOBAL) ||
-      std::max((size_t)geom_floats * sizeof(float) + shmem_fb, shmem_walk) > kLdsDynamicMax) {
+  // (only the walk kernel stages geometry, so only its LDS decides)
+  if ((prm->schedule & WOS_SCHED_GEOM_GLOBAL) || shmem_walk > kLdsDynamicMax) {
     dfb.geom_global = 1;
     dsc.geom_global = 1;
     geom_floats_walk = 0;
     shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(dim);
   }
-  if (std::max(shmem_fb, shmem_walk) > kLdsDynamicMax)
+  if (shmem_fb > kLdsDynamicMax)
     return fail(WOS_E_CAPACITY, "wos_solve: nWalks exceed the LDS budget of the first-ball kernel (" +
-                                    std::to_string(shmem_fb) + " bytes)");
+                                    std::to_string(shmem_fb) + " bytes of stratified samples per block)");
+  if (shmem_walk > kLdsDynamicMax)
+    return fail(WOS_E_CAPACITY, "wos_solve: the walk kernel's per-wave scratch exceeds the LDS budget (" +
+                                    std::to_string(shmem_walk) + " bytes)");
 
   // the shared workspace may still be in use by a solve enqueued on another stream
   HIP_TRY(ctx_order(c, st));
@@ -1080,6 +1082,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     if (counts) { counts[0] = smp.nb_main; counts[1] = smp.nb_aligned; counts[2] = nd_keep; counts[3] = nb + nd_keep; }
     HIP_TRY(hipStreamSynchronize(st));
     c.inflight = false;
+    q.ticket = 0;  // the slot holds no finished solve: wos_solve_stats on it reports an unknown ticket
     return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
                                     std::to_string(nb + nd_keep) + " samples (counts[3])");
   }
@@ -1185,7 +1188,12 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     if (rc != WOS_OK) return rc;
     stats->points_estimated = (uint64_t)nb;
   }
-  if (samples && nrec > 0) std::memcpy(samples, recs.data(), recs.size() * sizeof(float));
+  if (samples && nrec > 0) {
+    if (samples_capacity < nrec)
+      return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
+                                      std::to_string(nrec) + " samples (counts[3])");
+    std::memcpy(samples, recs.data(), recs.size() * sizeof(float));
+  }
   return WOS_OK;
 }
 

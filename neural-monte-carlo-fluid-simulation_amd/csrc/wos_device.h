@@ -3169,11 +3169,10 @@ constexpr int kSetupLanes = WOS_SETUP_LANES;  // lanes per point of wos_point_se
 #endif
 constexpr int kSetupLdsFloats = WOS_SETUP_LDS_FLOATS;  // 16 KB: 1024 segments / 455 triangles
 static_assert((kSetupLanes & (kSetupLanes - 1)) == 0 && kSetupLanes <= kWave, "kSetupLanes");
-// Point setup for the presorted first balls: one point per kSetupLanes lanes (the exact scans of
-// closest_lane), pstate + first-ball radius per point and the bucket histogram.  The
-// first-ball kernel then takes the points in descending radius order, so the points
-// whose 64 lanes run the longest rejection loops start first instead of anywhere in
-// the queue (a late one had set the kernel's tail).
+// Point setup: one point per kSetupLanes lanes (the exact scans of closest_lane), pstate +
+// first-ball radius per point, the cost-bucket histogram of the walk queue and (2D Yukawa,
+// reference float semantics) the first ball's Bessel members at mu R.  The first-ball kernel
+// then takes the points in plain point order from an atomic queue.
 template <int DIM>
 __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc, const DevParams prm,
                                                              const float* __restrict__ pts, int64_t n,
@@ -3222,7 +3221,10 @@ __global__ __launch_bounds__(256) void wos_point_setup_kernel(const DevScene sc,
       tk.pstate[i] = ps;
       tk.prad[i] = firstR;
       if constexpr (DIM == 2) {
-        if (tk.pball != nullptr && (ps & kPtEstimate) && sc.absorption > 0.0f && prm.steps_before_tikhonov == 0) {
+        // robust solves (RB first-ball kernels) evaluate the scaled members themselves and never
+        // read these (pre = !RB && ...): skip the double-precision work
+        if (tk.pball != nullptr && !prm.robust && (ps & kPtEstimate) && sc.absorption > 0.0f &&
+            prm.steps_before_tikhonov == 0) {
           Gfn<2> g;
           g.init(true, sc.absorption);
           g.update_ball(x, firstR, false);

@@ -8,8 +8,9 @@ wos_solver_params.schedule (include/wos.h WOS_SCHED_*) selects, per solve:
                          default for such scenes);
 * WOS_SCHED_NO_STAR_GRID the cooperative silhouette-group scan alone, without the
                          star-radius cell grid.
-One process solves the same points with every bit off (the default) and on, alone and
-combined, and compares p, grad p, the per-point walk counts and step counts bit for bit.
+One process solves the same points under all 8 combinations of the bits and compares p, grad p,
+the per-point walk counts and step counts bit for bit with the default (schedule 0), which
+itself is compared with the CPU oracle.
 Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance), the
 Dirichlet obstacle (stored distance) and the cube (3D)."""
 import numpy as np
@@ -21,27 +22,31 @@ from wos_amd._lib import SCHED_FULL_NEUMANN, SCHED_GEOM_GLOBAL, SCHED_NO_STAR_GR
 
 pytestmark = pytest.mark.gpu
 
-SETTINGS = [0, SCHED_GEOM_GLOBAL, SCHED_FULL_NEUMANN, SCHED_NO_STAR_GRID,
-            SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID]
+SETTINGS = list(range(8))  # every combination of the three bits
+assert SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID == 7
 
 
 def _scenes():
     out = []
     cfg = workloads.karman_config(n_walks=32)
     v, ix = objparse.load(cfg["obj"], 2)
-    out.append(("karman", cfg, lambda: WosScene(v, ix, cfg["source"], 350.0, watertight=True), cfg["points"][:2048]))
+    out.append(("karman", cfg, lambda: WosScene(v, ix, cfg["source"], 350.0, watertight=True), cfg["points"][:2048],
+                lambda o: o.OracleScene(v, ix, cfg["source"], 350.0)))
     c = workloads.dirichlet_obstacle_config(n_walks=32, res=48)
     out.append(("dirichlet", c, lambda: WosScene(c["vertices"], c["prims"], c["source"], c["absorption"],
                                                  dvertices=c["dvertices"], dprims=c["dprims"], dirichlet_value=1.0,
-                                                 watertight=True), c["points"][:2048]))
+                                                 watertight=True), c["points"][:2048],
+                lambda o: o.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], dvertices=c["dvertices"],
+                                        dprims=c["dprims"], dirichlet_value=1.0)))
     k = workloads.cube_config(res=12, n_walks=16)
     kv, kix = objparse.load(k["obj"], 3)
-    out.append(("cube", k, lambda: WosScene(kv, kix, k["source"], 350.0, watertight=True), k["points"]))
+    out.append(("cube", k, lambda: WosScene(kv, kix, k["source"], 350.0, watertight=True), k["points"],
+                lambda o: o.OracleScene(kv, kix, k["source"], 350.0)))
     return out
 
 
-@pytest.mark.parametrize("name,cfg,make,pts", _scenes(), ids=["karman", "dirichlet", "cube"])
-def test_switches_are_bit_identical(gpu, name, cfg, make, pts):
+@pytest.mark.parametrize("name,cfg,make,pts,make_oracle", _scenes(), ids=["karman", "dirichlet", "cube"])
+def test_switches_are_bit_identical(gpu, oracle, name, cfg, make, pts, make_oracle):
     sc = make()
     ref = None
     for sched in SETTINGS:
@@ -54,6 +59,10 @@ def test_switches_are_bit_identical(gpu, name, cfg, make, pts):
         if ref is None:
             ref = out
             assert np.isfinite(np.asarray(p)).all()
+            po, go, no, so, _ = oracle.solve(make_oracle(oracle), oracle.make_params(cfg["solver"], cfg["output"]),
+                                             np.ascontiguousarray(pts, np.float32))
+            for a, b in zip(ref, [po.view(np.uint32), go.view(np.uint32), no, so]):
+                assert np.array_equal(a, b), "default schedule vs oracle"
             continue
         for a, b in zip(ref, out):
             assert np.array_equal(a, b), sched

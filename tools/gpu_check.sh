@@ -1,7 +1,7 @@
 #!/bin/bash
-# GPU check (GPU box, repo root): the engine pin first (fast feedback), then the whole -m gpu
-# suite, then the default bench line.  Outputs in gpurun_out/<tag>_*.
-#   tools/r4_gpu_check.sh TAG
+# GPU check (GPU box, repo root): the engine pin against the reference's own outputs first
+# (fast feedback), then the whole -m gpu suite and smoke(), then the default bench line.
+# Outputs in gpurun_out/<tag>_*.        tools/gpu_check.sh TAG
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-r4}
@@ -12,4 +12,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 rc=$?
 tail -5 gpurun_out/${TAG}_tests.log
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 &&
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err

@@ -196,21 +196,28 @@ typedef struct wos_bvc_params {
     float normal_offset;            /* normalOffsetForCachedDirichletSamples (5 epsilonShell) */
     float radius_clamp;             /* radiusClampForKernels (1e-3) */
     float kernel_regularization;    /* regularizationForKernels (0) */
+    float grid_box[4];              /* evaluation grid x0, y0, ex, ey (ABI 8; extent 0: the scene's
+                                       bounding box -- createEvaluationGrid(bbox.pMin, bbox.pMax),
+                                       demo.cpp:311, grid.h:352-368) */
 } wos_bvc_params;
 
 void wos_default_bvc_params(wos_bvc_params *p);
 
-/* runBoundaryValueCaching (demo.cpp:265-363) on a 2D all-Neumann scene (the only kind
- * the reference's Scene builds: scene.h:39,68), blocking, host buffers:
+/* runBoundaryValueCaching (demo.cpp:265-363) on a 2D scene, blocking, host buffers:
  *   solution[g*g], grad[g*g*2]  the evaluation grid (point (i, j) at index i*g + j,
- *                               x = i/g * extent + bbox min, grid.h:352-368), masked as
- *                               saveEvaluationGrid does (grid.h:393-409);
+ *                               x = i/g * extent + box min over grid_box, grid.h:352-368),
+ *                               masked as saveEvaluationGrid does (grid.h:393-409);
  *   samples[k*8] (optional)     the cached samples [x y nx ny pdf value dn/dn kind], kind 0
- *                               boundary, 1 normal-aligned boundary, 2 domain (value = the
- *                               estimated solution or the source), if samples_capacity
- *                               holds them (else WOS_E_CAPACITY);
+ *                               Neumann boundary, 1 Neumann normal-aligned, 2 domain (value =
+ *                               the source), 3 Dirichlet boundary, 4 Dirichlet normal-aligned
+ *                               (the sample normalOffset inside the boundary, value = the
+ *                               estimated solution, dn/dn its estimated normal derivative),
+ *                               if samples_capacity holds them (else WOS_E_CAPACITY);
  *   counts[4] (optional)        boundary, normal-aligned, domain samples, total.
- * Scenes with Dirichlet primitives or in 3D return WOS_E_INVALID (no reference analogue). */
+ * Boundary samples cover the Neumann and the Dirichlet segments (boundary_sampler.h:87-412);
+ * evaluation points within normalOffset of the Dirichlet boundary take a pointwise
+ * estimateSolution (splatter.h:160-196).  3D scenes return WOS_E_INVALID (zombie3d exports no
+ * bvc). */
 int wos_bvc(wos_scene *scene, const wos_solver_params *params, const wos_bvc_params *bvc,
             float *solution, float *grad, float *samples, int64_t samples_capacity, int64_t *counts,
             wos_stats *stats);

@@ -77,16 +77,20 @@ __global__ __launch_bounds__(256) void wos_bvc_point_info_kernel(const DevScene 
 }
 
 // The first sphere radius of estimateSolution (walk_on_stars.h:390-419) for every
-// boundary sample, then its walk tasks: WalkState(pt, n, prevDirection = n, FLT_MAX,
-// 1, onNeumann) for each of the wpp walks.  Double-sided normal-aligned samples walk
-// with the flipped normal and query the star radius with flipNormalOrientation.
+// sample, then its walk tasks: WalkState(pt, n, prevDirection = n, FLT_MAX, 1, onNeumann)
+// for each of the wpp walks.  on_neumann: a boundary sample (SampleType::OnNeumannBoundary);
+// else a point in the domain (an evaluation point near the Dirichlet boundary,
+// splatter.h:160-196, or a finite-difference Dirichlet sample).  Double-sided
+// normal-aligned boundary samples walk with the flipped normal and query the star radius
+// with flipNormalOrientation.  Walk w of sample i is seeded seed32(key, base + i, w, tag);
+// from inside the epsilon shell only walk 0 runs (walk_on_stars.h:383-386).
 template <int DIM>
 __global__ __launch_bounds__(kBlock) void wos_bvc_start_kernel(const DevScene sc, const DevParams prm,
                                                                const float* __restrict__ bpt,
                                                                const float* __restrict__ bnrm,
                                                                const uint8_t* __restrict__ aligned,
                                                                const float* __restrict__ bdd, int64_t nb,
-                                                               const DevTasks tk) {
+                                                               const DevTasks tk, int on_neumann, uint32_t tag) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -99,9 +103,9 @@ __global__ __launch_bounds__(kBlock) void wos_bvc_start_kernel(const DevScene sc
   bool flip = false;
   for (int k = 0; k < DIM; k++) { x[k] = 0.0f; n[k] = 0.0f; }
   if (valid) {
-    for (int k = 0; k < DIM; k++) { x[k] = bpt[i * DIM + k]; n[k] = bnrm[i * DIM + k]; }
+    for (int k = 0; k < DIM; k++) { x[k] = bpt[i * DIM + k]; n[k] = bnrm ? bnrm[i * DIM + k] : 0.0f; }
     dd = bdd[i];
-    flip = sc.double_sided && aligned[i] != 0;
+    flip = on_neumann && sc.double_sided && aligned != nullptr && aligned[i] != 0;
     if (flip) for (int k = 0; k < DIM; k++) n[k] *= -1.0f;
   }
   const bool query = valid && dd > prm.epsilon_shell && prm.steps_before_maximal_spheres != 0;
@@ -120,7 +124,8 @@ __global__ __launch_bounds__(kBlock) void wos_bvc_start_kernel(const DevScene sc
     tk.tsrc[t] = 0.0f;
     tk.dd[t] = dd;
     tk.r0[t] = r0;
-    tk.sflags[t] = 1u;  // SampleType::OnNeumannBoundary
+    const bool shell = !(dd > prm.epsilon_shell);
+    tk.sflags[t] = (on_neumann ? 1u : 0u) | (shell && w > 0 ? 2u : 0u) | (tag << 8);
   }
   tk.pstate[i] = kPtEstimate;
   tk.perm[i] = (uint32_t)i;
@@ -143,6 +148,24 @@ __global__ __launch_bounds__(256) void wos_bvc_fold_kernel(const DevTasks tk, in
   }
   sol[i] = mean;
   if (nest) nest[i] = N;
+}
+
+// useFiniteDifferencesForBoundaryDerivatives (boundary_sampler.h:171-184): the normal derivative
+// of a Dirichlet sample is (g(x') - u) / |d| with x' its projection onto the Dirichlet boundary
+// (projectToDirichlet: the closest point, signed distance when double-sided) and u its estimate
+__global__ __launch_bounds__(256) void wos_bvc_fd_kernel(const DevScene sc, const float* __restrict__ pts,
+                                                         const float* __restrict__ sol, int64_t n,
+                                                         float* __restrict__ dn) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x[2] = {pts[2 * i], pts[2 * i + 1]};
+  float gv = sc.g_dirichlet, sd = 0.0f;
+  if (sc.n_dprims > 0) {
+    const Closest c = closest_lane<2>(sc.dprim, sc.n_dprims, x);
+    sd = sc.double_sided ? signed_dist<2>(sc.dpaux, c, x) : c.d;
+    gv = dirichlet_value<2>(sc, x);
+  }
+  dn[i] = (gv - sol[i]) / __builtin_fabsf(sd);
 }
 
 // ---- free-space Green's functions, 2D (distributions.h:85-119, 168-219) -------
@@ -237,7 +260,7 @@ __global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restr
   float x[2] = {0.0f, 0.0f}, dDist = 0.0f;
   if (valid) { x[0] = ept[2 * i]; x[1] = ept[2 * i + 1]; dDist = edd[i]; }
   // evaluation points closer than the cutoff to the Dirichlet boundary are not splatted
-  // (splatter.h:94); the scenes bvc accepts have no Dirichlet boundary
+  // (splatter.h:94): they take a pointwise estimate (estimatePointwiseNearDirichletBoundary)
   const bool splat = valid && !(dDist < cutoff);
   SplatStat st[3];
   for (int q = 0; q < 3; q++) { st[q].mean = 0.0f; st[q].g[0] = st[q].g[1] = 0.0f; st[q].n = 0; }
@@ -260,9 +283,10 @@ __global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restr
         gf.gradient(r, xy, K1, dG);
         const float dGNorm = __builtin_sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
         float est, ge[2];
+        const bool al = kind == kBvcAligned || kind == kBvcDirichletAligned;
         if (kind != kBvcDomain) {  // splatBoundaryData (splatter.h:214-264)
           const float nd = R[6];
-          const float s = kind == kBvcAligned ? -1.0f : 1.0f;
+          const float s = al ? -1.0f : 1.0f;
           const float n[2] = {R[2] * s, R[3] * s};
           float P = gf.poisson(r, xy, n, K1);
           float dP[2];
@@ -280,7 +304,7 @@ __global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restr
           est = (G * value) / pdf;
           for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
         }
-        st[kind].add(est, ge);
+        st[kind == kBvcDomain ? 2 : al ? 1 : 0].add(est, ge);
       }
     }
     __syncthreads();
@@ -319,11 +343,18 @@ hipError_t launch_bvc_point_info(const DevScene& sc, const float* pts, int64_t n
 size_t bvc_start_lds_bytes() { return (size_t)kWavesPerBlockHost * walk_scratch_bytes<2>(); }
 
 hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const float* bpt, const float* bnrm,
-                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, hipStream_t s) {
+                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, int on_neumann,
+                            uint32_t tag, hipStream_t s) {
   if (nb <= 0) return hipSuccess;
   const int grid = (int)((nb + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(wos_bvc_start_kernel<2>, dim3(grid), dim3(kBlock), bvc_start_lds_bytes(), s, sc, prm, bpt, bnrm,
-                     aligned, bdd, nb, tk);
+                     aligned, bdd, nb, tk, on_neumann, tag);
+  return hipGetLastError();
+}
+
+hipError_t launch_bvc_fd(const DevScene& sc, const float* pts, const float* sol, int64_t n, float* dn, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wos_bvc_fd_kernel, dim3((int)((n + 255) / 256)), dim3(256), 0, s, sc, pts, sol, n, dn);
   return hipGetLastError();
 }
 

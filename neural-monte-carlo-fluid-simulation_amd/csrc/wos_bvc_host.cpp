@@ -1,4 +1,4 @@
-// wos_bvc_host.cpp -- boundary value caching, host part: the boundary and domain
+// wos_bvc_host.cpp -- boundary value caching, host part: the boundary (Neumann and Dirichlet) and domain
 // samplers (boundary_value_caching/boundary_sampler.h, domain_sampler.h) and the
 // evaluation grid (demo/grid.h:352-368).  Float arithmetic in the reference's order
 // (built with -ffp-contract=off, like the kernels), so the samples equal the CPU
@@ -74,23 +74,66 @@ struct Seg {
   float pa[2], pb[2];
 };
 
-Seg segment(const float* v, const int32_t* ix, int p) {
-  Seg s;
-  for (int k = 0; k < 2; k++) {
-    s.pa[k] = v[2 * ix[2 * p] + k];
-    s.pb[k] = v[2 * ix[2 * p + 1] + k];
+// The sampler's boundary (boundary_sampler.h:87-412): the Neumann segments, then the Dirichlet
+// ones, whose vertices carry the sampler's own normals (computeNormals :193-236: unit segment
+// normals summed per vertex, normalised; per part -- a vertex shared with a Neumann segment
+// keeps its Dirichlet normal).
+struct Boundary {
+  const float *v, *dv;
+  const int32_t *ix, *dix;
+  int np = 0, ndp = 0;
+  std::vector<float> dn;  // [ndv][2]
+  int size() const { return np + ndp; }
+  bool dirichlet(int i) const { return i >= np; }
+  Seg raw(int i) const {
+    Seg s;
+    const float* V = i < np ? v : dv;
+    const int32_t* I = i < np ? ix : dix;
+    const int p = i < np ? i : i - np;
+    for (int k = 0; k < 2; k++) {
+      s.pa[k] = V[2 * I[2 * p] + k];
+      s.pb[k] = V[2 * I[2 * p + 1] + k];
+    }
+    return s;
   }
-  return s;
+  // Dirichlet ends displaced along the vertex normals (`pa += normalOffset*normals[index[0]]`)
+  Seg ends(int i, float offset) const {
+    Seg s = raw(i);
+    if (dirichlet(i)) {
+      const int p = i - np;
+      for (int k = 0; k < 2; k++) {
+        s.pa[k] += offset * dn[2 * dix[2 * p] + k];
+        s.pb[k] += offset * dn[2 * dix[2 * p + 1] + k];
+      }
+    }
+    return s;
+  }
+};
+
+void dirichlet_normals(Boundary& B, int ndv) {
+  B.dn.assign((size_t)2 * ndv, 0.0f);
+  for (int p = 0; p < B.ndp; p++) {
+    const Seg g = B.raw(B.np + p);
+    const float s0 = g.pb[0] - g.pa[0], s1 = g.pb[1] - g.pa[1];
+    float n[2] = {s1, -s0};
+    const float z = n[0] * n[0] + n[1] * n[1];
+    if (z > 0.0f) { const float r = std::sqrt(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+    for (int q = 0; q < 2; q++)
+      for (int k = 0; k < 2; k++) B.dn[2 * B.dix[2 * p + q] + k] += n[k];
+  }
+  for (int i = 0; i < ndv; i++) {
+    const float z = B.dn[2 * i] * B.dn[2 * i] + B.dn[2 * i + 1] * B.dn[2 * i + 1];
+    if (z > 0.0f) { const float r = std::sqrt(z); B.dn[2 * i] /= r; B.dn[2 * i + 1] /= r; }
+  }
 }
 
-// buildCDFTable (boundary_sampler.h:291-331) on an all-Neumann boundary: weight =
-// segment length when pMid + normalOffset * n lies in the bounding box (the solve
-// region of the boundary sampler, demo.cpp:299-301: !outsideBoundingDomain)
-float build_table(const float* v, const int32_t* ix, int np, const float* pmin, const float* pmax,
-                  float normal_offset, Cdf& cdf) {
-  std::vector<float> w(np, 0.0f);
-  for (int i = 0; i < np; i++) {
-    const Seg g = segment(v, ix, i);
+// buildCDFTable (boundary_sampler.h:291-331): weight = the (displaced) segment's length when
+// pMid + normalOffset * n lies in the bounding box (the solve region of the boundary sampler,
+// demo.cpp:299-301: !outsideBoundingDomain)
+float build_table(const Boundary& B, const float* pmin, const float* pmax, float normal_offset, Cdf& cdf) {
+  std::vector<float> w(B.size(), 0.0f);
+  for (int i = 0; i < B.size(); i++) {
+    const Seg g = B.raw(i);
     const float pMid[2] = {(g.pa[0] + g.pb[0]) / 2.0f, (g.pa[1] + g.pb[1]) / 2.0f};
     const float s0 = g.pb[0] - g.pa[0], s1 = g.pb[1] - g.pa[1];
     float n[2] = {s1, -s0};  // lineSegmentNormal(pa, pb, true): Eigen normalized()
@@ -98,14 +141,18 @@ float build_table(const float* v, const int32_t* ix, int np, const float* pmin, 
     if (z > 0.0f) { const float r = std::sqrt(z); n[0] = n[0] / r; n[1] = n[1] / r; }
     const float q[2] = {pMid[0] + normal_offset * n[0], pMid[1] + normal_offset * n[1]};
     const bool inside = q[0] >= pmin[0] && q[1] >= pmin[1] && q[0] <= pmax[0] && q[1] <= pmax[1];
-    if (inside) w[i] = std::sqrt(s1 * s1 + (-s0) * (-s0));  // lineSegmentSurfaceArea
+    if (inside) {
+      const Seg e = B.ends(i, normal_offset);
+      const float t0 = e.pb[0] - e.pa[0], t1 = e.pb[1] - e.pa[1];
+      w[i] = std::sqrt(t1 * t1 + (-t0) * (-t0));  // lineSegmentSurfaceArea
+    }
   }
   return cdf.build(w);
 }
 
 // generateSamples (boundary_sampler.h:333-402): n stratified draws into the table,
 // then per sampled segment one uniform draw (one sample) or a stratified set
-void gen_boundary(const float* v, const int32_t* ix, const Cdf& cdf, int n, float total, bool aligned, Pcg32& g,
+void gen_boundary(const Boundary& B, const Cdf& cdf, int n, float total, float normal_offset, bool aligned, Pcg32& g,
                   BvcSampling& out) {
   if (!(total > 0.0f) || n <= 0) return;
   std::vector<float> strat;
@@ -118,7 +165,7 @@ void gen_boundary(const float* v, const int32_t* ix, const Cdf& cdf, int n, floa
     if (c == 0) continue;
     if (c == 1) u.assign(1, g.nextf());
     else stratified(u, c, 1, g);
-    const Seg sg = segment(v, ix, f);
+    const Seg sg = B.ends(f, normal_offset);
     const float s0 = sg.pb[0] - sg.pa[0], s1 = sg.pb[1] - sg.pa[1];
     for (int i = 0; i < c; i++) {
       // sampleLineSegmentUniformly<2> (sampling.h:213-224)
@@ -132,38 +179,45 @@ void gen_boundary(const float* v, const int32_t* ix, const Cdf& cdf, int n, floa
       out.bnrm.push_back(nn[0]);
       out.bnrm.push_back(nn[1]);
       out.aligned.push_back(aligned ? 1 : 0);
+      out.dirichlet.push_back(B.dirichlet(f) ? 1 : 0);
     }
   }
 }
 
 }  // namespace
 
-bool bvc_generate_samples(const float* v, int nv, const int32_t* ix, int np, const float pmin[2],
-                          const float pmax[2], bool double_sided, int boundary_cache, int domain_cache,
-                          float normal_offset, bool ignore_source, uint64_t seed, BvcSampling& out,
-                          std::string& err) {
+bool bvc_generate_samples(const float* v, int nv, const int32_t* ix, int np, const float* dv, int ndv,
+                          const int32_t* dix, int ndp, const float pmin[2], const float pmax[2], bool double_sided,
+                          int boundary_cache, int domain_cache, float normal_offset, bool ignore_source,
+                          uint64_t seed, BvcSampling& out, std::string& err) {
   out = BvcSampling{};
   for (int i = 0; i < 2 * np; i++)
     if (ix[i] < 0 || ix[i] >= nv) { err = "bvc: segment index out of range"; return false; }
+  for (int i = 0; i < 2 * ndp; i++)
+    if (dix[i] < 0 || dix[i] >= ndv) { err = "bvc: Dirichlet segment index out of range"; return false; }
+  Boundary B;
+  B.v = v; B.ix = ix; B.np = np;
+  B.dv = dv; B.dix = dix; B.ndp = ndp;
+  dirichlet_normals(B, ndv);
   // ---- boundary samples (BoundarySampler::initialize + generateSamples)
   Pcg32 bs;
   bs.seed(seed32(seed, 0, 0, 4));
   Cdf t_main, t_aligned;
-  const float a_main = build_table(v, ix, np, pmin, pmax, -1.0f * normal_offset, t_main);
+  const float a_main = build_table(B, pmin, pmax, -1.0f * normal_offset, t_main);
   if (double_sided) {
-    const float a_al = build_table(v, ix, np, pmin, pmax, normal_offset, t_aligned);
+    const float a_al = build_table(B, pmin, pmax, normal_offset, t_aligned);
     const float total = a_main + a_al;
     const int n_main = (int)std::ceil((float)boundary_cache * a_main / total);
     const int n_al = (int)std::ceil((float)boundary_cache * a_al / total);
     out.pdf_main = 1.0f / a_main;
     out.pdf_aligned = 1.0f / a_al;
-    gen_boundary(v, ix, t_main, n_main, a_main, false, bs, out);
+    gen_boundary(B, t_main, n_main, a_main, -1.0f * normal_offset, false, bs, out);
     out.nb_main = (int)out.aligned.size();
-    gen_boundary(v, ix, t_aligned, n_al, a_al, true, bs, out);
+    gen_boundary(B, t_aligned, n_al, a_al, normal_offset, true, bs, out);
     out.nb_aligned = (int)out.aligned.size() - out.nb_main;
   } else {
     out.pdf_main = 1.0f / a_main;
-    gen_boundary(v, ix, t_main, boundary_cache, a_main, false, bs, out);
+    gen_boundary(B, t_main, boundary_cache, a_main, -1.0f * normal_offset, false, bs, out);
     out.nb_main = (int)out.aligned.size();
   }
   // ---- domain candidates (DomainSampler::generateSamples), inside test on the GPU
@@ -171,11 +225,16 @@ bool bvc_generate_samples(const float* v, int nv, const int32_t* ix, int np, con
   float vol;
   if (double_sided) {
     vol = ext[0] * ext[1];
-  } else {  // |signedVolume| of the boundary (LineSegment::signedVolume, line_segments.inl:38-44)
-    float sv = 0.0f;
-    for (int p = 0; p < np; p++) {
-      const Seg g = segment(v, ix, p);
-      sv += 0.5f * (g.pa[0] * g.pb[1] - g.pa[1] * g.pb[0]);
+  } else {  // getSolveRegionVolume (scene.h:92-100): |Dirichlet part's + Neumann part's signedVolume|
+    float sv = 0.0f;  // LineSegment::signedVolume, line_segments.inl:38-44
+    for (int part = 0; part < 2; part++) {
+      float sq = 0.0f;
+      const int n0 = part == 0 ? np : 0, n1 = part == 0 ? np + ndp : np;  // the Dirichlet part first
+      for (int i = n0; i < n1; i++) {
+        const Seg g = B.raw(i);
+        sq += 0.5f * (g.pa[0] * g.pb[1] - g.pa[1] * g.pb[0]);
+      }
+      sv += sq;
     }
     vol = std::fabs(sv);
   }
@@ -197,8 +256,7 @@ bool bvc_generate_samples(const float* v, int nv, const int32_t* ix, int np, con
   return true;
 }
 
-void bvc_evaluation_grid(int res, const float pmin[2], const float pmax[2], std::vector<float>& pts) {
-  const float ext[2] = {pmax[0] - pmin[0], pmax[1] - pmin[1]};
+void bvc_evaluation_grid(int res, const float pmin[2], const float ext[2], std::vector<float>& pts) {
   pts.resize((size_t)2 * res * res);
   for (int i = 0; i < res; i++)
     for (int j = 0; j < res; j++) {

@@ -747,6 +747,19 @@ wos::DevParams dev_params(const wos_solver_params* prm) {
   return dp;
 }
 
+// what a solve needs beyond wos_solve's arguments (BVC's Dirichlet samples): per point the
+// direction of the derivative [n][dim] and the derivative out [n] (device pointers), and
+// estimation at every point regardless of the inside test
+struct SolveExtra {
+  const float* ddir = nullptr;
+  float* deriv = nullptr;
+  bool force_estimate = false;
+};
+
+int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
+                 int64_t index_stride, float* p, float* grad, int32_t* n_est, int32_t* steps, wos_stats* stats,
+                 void* stream, uint32_t flags, const SolveExtra& ex);
+
 }  // namespace
 
 extern "C" {
@@ -763,19 +776,33 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   if (!(prm->epsilon_shell >= 0.0f) || !(prm->min_star_radius >= 0.0f) || !(prm->silhouette_precision >= 0.0f))
     return fail(WOS_E_INVALID, "wos_solve: negative tolerance");
   std::lock_guard<std::mutex> lock(s->mu);
+  HIP_TRY(hipSetDevice(s->device));
+  DevCtx& c = g_ctx[s->device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  return solve_locked(s, prm, pts, n, index_base, index_stride, p, grad, n_est, steps, stats, stream, flags,
+                      SolveExtra{});
+}
+
+}  // extern "C"
+
+namespace {
+
+// wos_solve with the scene's and the device context's locks held
+int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
+                 int64_t index_stride, float* p, float* grad, int32_t* n_est, int32_t* steps, wos_stats* stats,
+                 void* stream, uint32_t flags, const SolveExtra& ex) {
   Geom& geom = *s->geom;
   const wos::HostScene& host = geom.host;
   const int dim = host.dim;
-  HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
   DevCtx& c = g_ctx[s->device];
-  std::lock_guard<std::mutex> lk(c.mu);
   {
     int rc = ctx_ready(c, s->device);
     if (rc != WOS_OK) return rc;
   }
 
   wos::DevParams dp = dev_params(prm);
+  dp.force_estimate = ex.force_estimate ? 1 : 0;
   {
     // diagonal draws + shuffle draws of the stratified samples
     const int k_needed = 2 * (2 * dp.n_pairs) * (dim - 1);
@@ -881,6 +908,8 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
     hipEvent_t* ev = &q.bev[4 * k];
     const int64_t nb = std::min(chunk, n - b0);
     wos::DevTasks tk = task_view(c, dim, nb * wpp, (int32_t)wpp);
+    tk.ddir = ex.ddir ? ex.ddir + b0 * dim : nullptr;
+    tk.deriv = ex.deriv ? ex.deriv + b0 : nullptr;
     const int64_t bbase = index_base + b0 * index_stride;
     unsigned long long* qslot = c.d_counters + wos::kNumCounters;
     unsigned int* q_points = (unsigned int*)qslot;
@@ -934,6 +963,10 @@ int wos_solve(wos_scene* s, const wos_solver_params* prm, const float* pts, int6
   return WOS_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
 int wos_solve_stats(wos_scene* s, uint64_t ticket, wos_stats* stats) {
   if (!s || !stats) return fail(WOS_E_INVALID, "wos_solve_stats: null scene/stats");
   const auto unknown = [&] {
@@ -986,21 +1019,15 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (bp->n_walks_solution < 1) return fail(WOS_E_INVALID, "wos_bvc: nWalksForCachedSolutionEstimates must be >= 1");
   if (bp->boundary_cache_size < 0 || bp->domain_cache_size < 0) return fail(WOS_E_INVALID, "wos_bvc: negative cache size");
   if (prm->max_walk_length < 0) return fail(WOS_E_INVALID, "wos_bvc: maxWalkLength must be >= 0");
+  if (bp->grid_box[2] < 0.0f || bp->grid_box[3] < 0.0f) return fail(WOS_E_INVALID, "wos_bvc: negative grid_box extent");
   std::lock_guard<std::mutex> lock(s->mu);
   Geom& geom = *s->geom;
   const wos::HostScene& host = geom.host;
   if (host.dim != 2) return fail(WOS_E_INVALID, "wos_bvc: boundary value caching is 2D (the reference exports it from the 2D module only)");
-  if (host.n_dprims > 0)
-    return fail(WOS_E_INVALID, "wos_bvc: Dirichlet boundaries are not supported (the reference's scenes are all-Neumann, scene.h:39,68)");
-  if (host.n_prims <= 0) return fail(WOS_E_INVALID, "wos_bvc: scene has no boundary");
-  // no Dirichlet boundary: every evaluation point's Dirichlet distance is the bounding
-  // box's far-corner distance (>= half the diagonal), above the splat cutoff unless the
-  // box is degenerate -- pointwise estimation near the Dirichlet boundary never runs
-  {
-    const float hx = 0.5f * host.ext[0], hy = 0.5f * host.ext[1];
-    if (!(std::sqrt(hx * hx + hy * hy) >= bp->normal_offset))
-      return fail(WOS_E_INVALID, "wos_bvc: scene bounding box smaller than normalOffsetForCachedDirichletSamples");
-  }
+  if (host.n_prims + host.n_dprims <= 0) return fail(WOS_E_INVALID, "wos_bvc: scene has no boundary");
+  const bool has_dir = host.n_dprims > 0;
+  if (has_dir && bp->n_walks_gradient < 1)
+    return fail(WOS_E_INVALID, "wos_bvc: nWalksForCachedGradientEstimates must be >= 1");
   HIP_TRY(hipSetDevice(s->device));
   DevCtx& c = g_ctx[s->device];
   std::lock_guard<std::mutex> lk(c.mu);
@@ -1012,27 +1039,54 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(ctx_order(c, st));
   HIP_TRY(hipStreamSynchronize(st));
 
-  // ---- host: boundary samples, domain candidates, evaluation grid
+  // ---- host: boundary samples (Neumann then Dirichlet segments), domain candidates,
+  // evaluation grid (over grid_box, else the scene's bounding box)
   wos::BvcSampling smp;
   std::string err;
   const float pmin[2] = {host.pmin[0], host.pmin[1]}, pmax[2] = {host.pmax[0], host.pmax[1]};
   if (!wos::bvc_generate_samples(geom.v.data(), (int)(geom.v.size() / 2), geom.ix.data(), (int)(geom.ix.size() / 2),
-                                 pmin, pmax, geom.double_sided != 0, bp->boundary_cache_size, bp->domain_cache_size,
-                                 bp->normal_offset, prm->ignore_source != 0, prm->seed, smp, err))
+                                 geom.dv.data(), (int)(geom.dv.size() / 2), geom.dix.data(),
+                                 (int)(geom.dix.size() / 2), pmin, pmax, geom.double_sided != 0,
+                                 bp->boundary_cache_size, bp->domain_cache_size, bp->normal_offset,
+                                 prm->ignore_source != 0, prm->seed, smp, err))
     return fail(WOS_E_INVALID, "wos_bvc: " + err);
+  float gmin[2] = {pmin[0], pmin[1]}, gext[2] = {pmax[0] - pmin[0], pmax[1] - pmin[1]};
+  if (bp->grid_box[2] > 0.0f && bp->grid_box[3] > 0.0f) {
+    gmin[0] = bp->grid_box[0]; gmin[1] = bp->grid_box[1];
+    gext[0] = bp->grid_box[2]; gext[1] = bp->grid_box[3];
+  }
   std::vector<float> ept;
-  wos::bvc_evaluation_grid(bp->grid_res, pmin, pmax, ept);
+  wos::bvc_evaluation_grid(bp->grid_res, gmin, gext, ept);
   const int64_t nb = (int64_t)smp.aligned.size();
   const int64_t nd = (int64_t)(smp.dcand.size() / 2);
   const int64_t ne = (int64_t)bp->grid_res * bp->grid_res;
+  // runs of consecutive boundary samples of one type (the sampler emits a cache's Neumann
+  // samples before its Dirichlet ones): [begin, end), Dirichlet?
+  struct Run { int64_t b0, b1; bool dir; };
+  std::vector<Run> runs;
+  for (int64_t i = 0; i < nb; i++) {
+    const bool d = smp.dirichlet[i] != 0;
+    if (runs.empty() || runs.back().dir != d || runs.back().b1 != i) runs.push_back({i, i + 1, d});
+    else runs.back().b1 = i + 1;
+  }
+  // BoundarySampler::computeEstimates (boundary_sampler.h:154-166): a Dirichlet sample's
+  // derivative is along its normal, reversed for normal-aligned samples of double-sided scenes
+  std::vector<float> ddir_h(2 * nb, 0.0f);
+  for (int64_t i = 0; i < nb; i++) {
+    const float sg = (geom.double_sided && smp.aligned[i]) ? -1.0f : 1.0f;
+    ddir_h[2 * i] = smp.bnrm[2 * i] * sg;
+    ddir_h[2 * i + 1] = smp.bnrm[2 * i + 1] * sg;
+  }
 
   // ---- device buffers (freed on every exit)
   DevBufs B;
-  float *d_bpt, *d_bnrm, *d_bdd, *d_bsol, *d_dc, *d_dsrc, *d_ept, *d_edd, *d_end, *d_sol, *d_grad;
+  float *d_bpt, *d_bnrm, *d_bdd, *d_bsol, *d_bdn, *d_ddir, *d_dc, *d_dsrc, *d_ept, *d_edd, *d_end, *d_sol, *d_grad;
   int32_t *d_bnest, *d_din, *d_ein;
   uint8_t* d_al;
   HIP_TRY(B.get(&d_bpt, 2 * nb)); HIP_TRY(B.get(&d_bnrm, 2 * nb)); HIP_TRY(B.get(&d_bdd, nb));
-  HIP_TRY(B.get(&d_bsol, nb)); HIP_TRY(B.get(&d_bnest, nb)); HIP_TRY(B.get(&d_al, nb));
+  HIP_TRY(B.get(&d_bsol, nb)); HIP_TRY(B.get(&d_bdn, nb)); HIP_TRY(B.get(&d_ddir, 2 * nb));
+  float* d_dgrad;  // the Dirichlet samples' gradient (unused output of the solve)
+  HIP_TRY(B.get(&d_bnest, nb)); HIP_TRY(B.get(&d_al, nb)); HIP_TRY(B.get(&d_dgrad, 2 * nb));
   HIP_TRY(B.get(&d_dc, 2 * nd)); HIP_TRY(B.get(&d_din, nd)); HIP_TRY(B.get(&d_dsrc, nd));
   HIP_TRY(B.get(&d_ept, 2 * ne)); HIP_TRY(B.get(&d_edd, ne)); HIP_TRY(B.get(&d_end, ne)); HIP_TRY(B.get(&d_ein, ne));
   HIP_TRY(B.get(&d_sol, ne)); HIP_TRY(B.get(&d_grad, 2 * ne));
@@ -1040,9 +1094,39 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     HIP_TRY(hipMemcpy(d_bpt, smp.bpt.data(), 2 * nb * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_bnrm, smp.bnrm.data(), 2 * nb * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_al, smp.aligned.data(), nb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_ddir, ddir_h.data(), 2 * nb * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync(d_bdn, 0, nb * sizeof(float), st));
   }
   if (nd > 0) HIP_TRY(hipMemcpy(d_dc, smp.dcand.data(), 2 * nd * sizeof(float), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_ept, ept.data(), 2 * ne * sizeof(float), hipMemcpyHostToDevice));
+
+  // ---- Dirichlet samples: estimateSolutionAndGradient along the normal (nWalksForCachedGradient-
+  // Estimates, keyed by the sample index) on the solve pipeline; solution and derivative
+  // unmasked.  First, on its own stat slot (the solve resets the counters), then the rest.
+  wos_stats dstat{};
+  bool have_dstat = false;
+  if (has_dir && !bp->use_finite_differences) {
+    wos_solver_params gp = *prm;
+    gp.n_walks = bp->n_walks_gradient;
+    gp.boundary_distance_mask = 0.0f;
+    SolveExtra ex;
+    ex.force_estimate = true;
+    for (const Run& r : runs) {
+      if (!r.dir) continue;
+      ex.ddir = d_ddir + 2 * r.b0;
+      ex.deriv = d_bdn + r.b0;
+      wos_stats rs{};
+      int rc = solve_locked(s, &gp, d_bpt + 2 * r.b0, r.b1 - r.b0, r.b0, 1, d_bsol + r.b0, d_dgrad, d_bnest + r.b0,
+                            nullptr, &rs, st, WOS_PTRS_DEVICE, ex);
+      if (rc != WOS_OK) return rc;
+      dstat.walk_steps += rs.walk_steps; dstat.wasted_steps += rs.wasted_steps;
+      dstat.walks_recorded += rs.walks_recorded; dstat.walks_escaped += rs.walks_escaped;
+      dstat.walks_max_length += rs.walks_max_length; dstat.walks_rr += rs.walks_rr;
+      dstat.walks_dirichlet += rs.walks_dirichlet; dstat.rejection_iters += rs.rejection_iters;
+      dstat.kernel_ms += rs.kernel_ms;
+      have_dstat = true;
+    }
+  }
 
   const uint64_t ticket = c.next_ticket++;
   StatSlot& q = c.slot[ticket % kStatSlots];
@@ -1086,22 +1170,39 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     return fail(WOS_E_CAPACITY, "wos_bvc: samples buffer holds " + std::to_string(samples_capacity) + " of " +
                                     std::to_string(nb + nd_keep) + " samples (counts[3])");
   }
-
-  // ---- estimates at the boundary samples: estimateSolution walks (walk_on_stars.h:353-464)
-  wos_solver_params wp = *prm;
-  wp.n_walks = bp->n_walks_solution;
-  wp.disable_gradient_antithetic_variates = 1;  // one walk per task, no pairs
-  wos::DevParams dp = dev_params(&wp);
-  {
-    int rc = ensure_jump(c, 4096);
-    if (rc != WOS_OK) return rc;
-    dp.jump = c.d_jump;
-    dp.n_jump = c.n_jump;
-    dp.rej_tab = c.d_rejtab;
+  // evaluation points within normalOffset of the Dirichlet boundary (splatter.h:160-196)
+  std::vector<int64_t> near_idx;
+  std::vector<float> near_pt, edd_h;
+  if (has_dir) {
+    edd_h.resize(ne);
+    HIP_TRY(hipMemcpyAsync(edd_h.data(), d_edd, ne * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < ne; i++)
+      if (edd_h[i] < bp->normal_offset) {
+        near_idx.push_back(i);
+        near_pt.push_back(ept[2 * i]);
+        near_pt.push_back(ept[2 * i + 1]);
+      }
   }
+  const int64_t nn = (int64_t)near_idx.size();
+  float *d_npt = nullptr, *d_ndd = nullptr, *d_nsol = nullptr;
+  int32_t* d_nnest = nullptr;
+  HIP_TRY(B.get(&d_npt, 2 * nn)); HIP_TRY(B.get(&d_ndd, nn)); HIP_TRY(B.get(&d_nsol, nn)); HIP_TRY(B.get(&d_nnest, nn));
+  if (nn > 0) {
+    std::vector<float> ndd(nn);
+    for (int64_t k = 0; k < nn; k++) ndd[k] = edd_h[near_idx[k]];
+    HIP_TRY(hipMemcpy(d_npt, near_pt.data(), 2 * nn * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_ndd, ndd.data(), nn * sizeof(float), hipMemcpyHostToDevice));
+  }
+
+  // ---- estimateSolution walks (walk_on_stars.h:353-464) on the persistent walk kernel:
+  // Neumann boundary samples (nWalksForCachedSolutionEstimates, seed tag 6), finite-difference
+  // Dirichlet samples (nWalksForCachedGradientEstimates, tag 8), evaluation points near the
+  // Dirichlet boundary (nWalksForCachedSolutionEstimates, tag 7, keyed by their rank)
   WalkLayout wl;
+  wos_solver_params wp0 = *prm;
   {
-    int rc = walk_layout(s, &wp, wl);
+    int rc = walk_layout(s, &wp0, wl);
     if (rc != WOS_OK) return rc;
   }
   wos::DevScene dsc = wl.dsc;
@@ -1110,51 +1211,89 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     wl.geom_floats_walk = 0;
     wl.shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(2);
   }
-  const int64_t wpp = wp.n_walks;
-  if (nb * wpp > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: boundaryCacheSize x nWalks exceeds one task batch");
-  if (nb > 0) {
-    int rc = ensure_tasks(c, 2, nb * wpp, nb);
+  {
+    int rc = ensure_jump(c, 4096);
     if (rc != WOS_OK) return rc;
-    wos::DevTasks tk = task_view(c, 2, nb * wpp, (int32_t)wpp);
+  }
+  bool first_walk = true;
+  auto walks = [&](const float* pts_d, const float* nrm_d, const uint8_t* al_d, const float* dd_d, int64_t np_,
+                   int64_t base, int n_walks, int on_neumann, uint32_t tag, float* sol_d, int32_t* nest_d) -> int {
+    if (np_ <= 0) return WOS_OK;
+    wos_solver_params wp = *prm;
+    wp.n_walks = n_walks;
+    wp.disable_gradient_antithetic_variates = 1;  // one walk per task, no pairs
+    wos::DevParams dp = dev_params(&wp);
+    dp.jump = c.d_jump;
+    dp.n_jump = c.n_jump;
+    dp.rej_tab = c.d_rejtab;
+    const int64_t wpp = n_walks;
+    if (np_ * wpp > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
+    int rc = ensure_tasks(c, 2, np_ * wpp, np_);
+    if (rc != WOS_OK) return rc;
+    wos::DevTasks tk = task_view(c, 2, np_ * wpp, (int32_t)wpp);
     tk.n0 = tk.bdir;
     tk.r0 = tk.first;
     tk.sflags = reinterpret_cast<uint32_t*>(tk.sdir);
-    HIP_TRY(wos::launch_bvc_start(dsc, dp, d_bpt, d_bnrm, d_al, d_bdd, nb, tk, st));
-    HIP_TRY(hipEventRecord(q.bev[1], st));
+    // the walk queue's counters start at 0 for every launch
+    if (!first_walk) HIP_TRY(wos::launch_zero(c.d_counters + wos::kNumCounters, wos::kNumCounterSlots - wos::kNumCounters,
+                                              nullptr, 0, st));
+    first_walk = false;
+    HIP_TRY(wos::launch_bvc_start(dsc, dp, pts_d, nrm_d, al_d, dd_d, np_, tk, on_neumann, tag, st));
     int bpc = 0;
     HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc, dp.robust != 0));
     const int grid = (int)std::min<int64_t>((int64_t)std::max(1, bpc) * std::max(1, c.num_cus), (tk.T + 63) / 64);
     unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
-    HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, 0, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,
+    HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, base, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,
                                      wl.geom_floats_walk, st));
-    HIP_TRY(hipEventRecord(q.bev[2], st));
-    HIP_TRY(wos::launch_bvc_fold(tk, nb, d_bsol, d_bnest, st));
+    HIP_TRY(wos::launch_bvc_fold(tk, np_, sol_d, nest_d, st));
     q.bpc_walk = bpc;
-  } else {
-    HIP_TRY(hipEventRecord(q.bev[1], st));
-    HIP_TRY(hipEventRecord(q.bev[2], st));
+    return WOS_OK;
+  };
+  HIP_TRY(hipEventRecord(q.bev[1], st));
+  for (const Run& r : runs) {
+    const int64_t m = r.b1 - r.b0;
+    int rc = WOS_OK;
+    if (!r.dir)
+      rc = walks(d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_solution, 1, 6u,
+                 d_bsol + r.b0, d_bnest + r.b0);
+    else if (bp->use_finite_differences)
+      rc = walks(d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_gradient, 0, 8u,
+                 d_bsol + r.b0, d_bnest + r.b0);
+    if (rc != WOS_OK) return rc;
+    if (r.dir && bp->use_finite_differences)
+      HIP_TRY(wos::launch_bvc_fd(s->dev, d_bpt + 2 * r.b0, d_bsol + r.b0, m, d_bdn + r.b0, st));
   }
+  {
+    int rc = walks(d_npt, nullptr, nullptr, d_ndd, nn, 0, bp->n_walks_solution, 0, 7u, d_nsol, d_nnest);
+    if (rc != WOS_OK) return rc;
+  }
+  HIP_TRY(hipEventRecord(q.bev[2], st));
   q.walk_lds = (int32_t)wl.shmem_walk;
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
 
-  // ---- the cache: boundary samples (solution, Neumann value 0: pde.neumann, scene.h:176-181)
-  // then the domain samples inside the solve region (source)
-  std::vector<float> bsol(nb), dsrc(nd);
+  // ---- the cache: boundary samples (solution; the Neumann value 0: pde.neumann, scene.h:176-181;
+  // Dirichlet samples their normal derivative), then the domain samples inside the solve
+  // region (source)
+  std::vector<float> bsol(nb), bdn(nb), dsrc(nd), nsol(nn);
   std::vector<int32_t> din(nd);
-  if (nb > 0) HIP_TRY(hipMemcpyAsync(bsol.data(), d_bsol, nb * sizeof(float), hipMemcpyDeviceToHost, st));
+  if (nb > 0) {
+    HIP_TRY(hipMemcpyAsync(bsol.data(), d_bsol, nb * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(bdn.data(), d_bdn, nb * sizeof(float), hipMemcpyDeviceToHost, st));
+  }
   if (nd > 0) {
     HIP_TRY(hipMemcpyAsync(dsrc.data(), d_dsrc, nd * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(din.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   }
+  if (nn > 0) HIP_TRY(hipMemcpyAsync(nsol.data(), d_nsol, nn * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   std::vector<float> recs;
   recs.reserve((size_t)(nb + nd) * wos::kBvcRec);
   for (int64_t i = 0; i < nb; i++) {
-    const bool al = smp.aligned[i] != 0;
+    const bool al = smp.aligned[i] != 0, dir = smp.dirichlet[i] != 0;
+    const int kind = dir ? (al ? wos::kBvcDirichletAligned : wos::kBvcDirichlet) : (al ? wos::kBvcAligned : wos::kBvcBoundary);
     const float r[wos::kBvcRec] = {smp.bpt[2 * i], smp.bpt[2 * i + 1], smp.bnrm[2 * i], smp.bnrm[2 * i + 1],
-                                   al ? smp.pdf_aligned : smp.pdf_main, bsol[i], 0.0f,
-                                   (float)(al ? wos::kBvcAligned : wos::kBvcBoundary)};
+                                   al ? smp.pdf_aligned : smp.pdf_main, bsol[i], dir ? bdn[i] : 0.0f, (float)kind};
     recs.insert(recs.end(), r, r + wos::kBvcRec);
   }
   int64_t nd_kept = 0;
@@ -1179,14 +1318,36 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(hipMemcpyAsync(q.h_cnt, c.d_counters, wos::kNumCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(solution, d_sol, ne * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(grad, d_grad, 2 * ne * sizeof(float), hipMemcpyDeviceToHost, st));
+  std::vector<float> end_h(nn > 0 ? ne : 0);
+  std::vector<int32_t> ein_h(nn > 0 ? ne : 0);
+  if (nn > 0) {
+    HIP_TRY(hipMemcpyAsync(end_h.data(), d_end, ne * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ein_h.data(), d_ein, ne * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipEventRecord(q.done, st));
   HIP_TRY(hipStreamSynchronize(st));
   c.inflight = false;
+  // the pointwise estimates near the Dirichlet boundary replace the (unsplatted) points'
+  // statistics: solution = the estimate, gradient 0 (evalPt.reset, splatter.h:186-192),
+  // then saveEvaluationGrid's mask (grid.h:404-408)
+  for (int64_t k = 0; k < nn; k++) {
+    const int64_t i = near_idx[k];
+    const bool masked = (ein_h[i] == 0 && !geom.double_sided) ||
+                        std::min(std::fabs(edd_h[i]), std::fabs(end_h[i])) < prm->boundary_distance_mask;
+    solution[i] = masked ? 0.0f : nsol[k];
+  }
   if (counts) { counts[0] = smp.nb_main; counts[1] = smp.nb_aligned; counts[2] = nd_kept; counts[3] = nrec; }
   if (stats) {
     int rc = fill_stats(q, stats);
     if (rc != WOS_OK) return rc;
     stats->points_estimated = (uint64_t)nb;
+    if (have_dstat) {
+      stats->walk_steps += dstat.walk_steps; stats->wasted_steps += dstat.wasted_steps;
+      stats->walks_recorded += dstat.walks_recorded; stats->walks_escaped += dstat.walks_escaped;
+      stats->walks_max_length += dstat.walks_max_length; stats->walks_rr += dstat.walks_rr;
+      stats->walks_dirichlet += dstat.walks_dirichlet; stats->rejection_iters += dstat.rejection_iters;
+      stats->kernel_ms += dstat.kernel_ms;
+    }
   }
   if (samples && nrec > 0) {
     if (samples_capacity < nrec)

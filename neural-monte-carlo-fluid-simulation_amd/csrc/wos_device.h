@@ -2863,7 +2863,7 @@ template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
                                             bool active, int w, int64_t t0, bool yuk0, uint32_t* iters,
-                                            RejLDS* rejL, int lane, const float* pb) {
+                                            RejLDS* rejL, int lane, const float* pb, const float* dn) {
   constexpr int sd = DIM - 1;
   if (DIM == 2 && !active) return;
   if (!active) w = 0;
@@ -2983,14 +2983,15 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
         float ct = __builtin_fabsf(bd[DIM - 1]);
         float pdfc = DIM == 2 ? ct / 2.0f : (float)((double)ct / kPi);
         boundaryPdf = 0.5f * pdfc;
-        // transformCoordinates (sampling.h:176-203) with n = (1,0[,0])
+        // transformCoordinates (sampling.h:176-203) with n = directionForDerivative
+        // (dn: the point's own, e.g. a BVC Dirichlet sample's normal; else (1, 0[, 0]))
         if constexpr (DIM == 2) {
-          const float n0 = 1.0f, n1 = 0.0f;
+          const float n0 = dn ? dn[0] : 1.0f, n1 = dn ? dn[1] : 0.0f;
           float s0 = n1, s1 = -n0;
           float q0 = bd[0] * s0 + bd[1] * n0, q1 = bd[0] * s1 + bd[1] * n1;
           bd[0] = q0; bd[1] = q1;
         } else {
-          const float n[3] = {1.0f, 0.0f, 0.0f};
+          const float n[3] = {dn ? dn[0] : 1.0f, dn ? dn[1] : 0.0f, dn ? dn[2] : 0.0f};
           float sign = __builtin_copysignf(1.0f, n[2]);
           const float aa = -1.0f / (sign + n[2]);
           const float b = n[0] * n[1] * aa;
@@ -3143,7 +3144,7 @@ __device__ __forceinline__ int32_t point_state(const DevScene& sc, const DevPara
                                                float dDist, float dSigned, int* bucket_out, float* firstR) {
   const bool inside = !sc.watertight ? true
                       : (__builtin_fabsf(dSigned) < __builtin_fabsf(nSigned) ? dSigned < 0.0f : nSigned < 0.0f);
-  const bool estimate = inside || sc.double_sided;
+  const bool estimate = inside || sc.double_sided || prm.force_estimate;
   const float mask = prm.boundary_distance_mask;
   const bool maskP = __builtin_fabsf(nDist) < mask;
   const bool maskG = (!inside && !sc.double_sided) || __builtin_fabsf(nDist) < mask;
@@ -3327,7 +3328,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       const int w = w0 + lane;
       first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
                            (int64_t)pidx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane,
-                           pb);
+                           pb, tk.ddir ? tk.ddir + (int64_t)pidx * DIM : nullptr);
     }
     DIAG_ADD(D_FB_BALLS, t_fb2);
     DIAG_ADD(D_FB_TOTAL, t_fb0);
@@ -3374,9 +3375,10 @@ __device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& 
     // (walk_on_stars.h:437-439); walk w of sample pidx on its own stream
     for (int kk = 0; kk < DIM; kk++) { st.n[kk] = tk.n0[kk * tk.T + t]; st.prevDir[kk] = st.n[kk]; }
     st.prevDist = kFltMax;
-    st.onNeumann = (tk.sflags[t] & 1u) != 0u;
+    const uint32_t fl = tk.sflags[t];  // bit 0: starts on the Neumann boundary; bits 8..15: seed tag
+    st.onNeumann = (fl & 1u) != 0u;
     firstR = tk.r0[t];
-    ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 6));
+    ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, (fl >> 8) & 0xFFu));
     wsteps = 0;
   } else {
     ws.seed(seed32(prm.seed, (uint64_t)(base + (int64_t)pidx * stride), (uint64_t)w, 2));
@@ -3619,7 +3621,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         }
         if (t < 0 && rank < take) {
           t = (int64_t)v_t;
-          if (!v_ok) {  // point outside the domain: no walks
+          // BSTART: estimateSolution runs one walk only from inside the epsilon shell
+          // (walk_on_stars.h:383-386): the start kernel marks the others (sflags bit 1)
+          if (!v_ok || (BSTART && (tk.sflags[t] & 2u))) {  // point outside the domain: no walks
             tk.code[t] = 0u;
             t = -1;
           } else {
@@ -3715,9 +3719,14 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   const bool estimate = (ps & kPtEstimate) != 0;
   float mean[DIM + 1];
   for (int k = 0; k <= DIM; k++) mean[k] = 0.0f;
-  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
+  float sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f, sDeriv = 0.0f;
   int sN = 0;
   uint32_t steps = 0;
+  // directionForDerivative (walk_on_stars.h:603-607): the point's own or (1, 0[, 0])
+  float dn[DIM];
+  for (int k = 0; k < DIM; k++) dn[k] = k == 0 ? 1.0f : 0.0f;
+  if (tk.deriv && tk.ddir && tid < nb)
+    for (int k = 0; k < DIM; k++) dn[k] = tk.ddir[i * DIM + k];
   for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
     const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
     // kFoldUnroll<DIM> staging slots in flight per thread: all their loads are issued
@@ -3768,12 +3777,16 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
           const float delta = total - mean[0];
           mean[0] += delta / fN;
         }
+        float deriv = 0.0f;
         for (int k = 0; k < DIM; k++) {
           const float be = (total - first - cvb) * lds[3 + k][tid][j];
           const float se = (first - cvs) * lds[3 + DIM + k][tid][j];
           const float delta = (be + se) - mean[k + 1];
           mean[k + 1] += delta / fN;
+          deriv += be * dn[k];
+          deriv += se * dn[k];
         }
+        sDeriv += deriv;  // addDerivativeContribution
         sFirst += first;
       }
     }
@@ -3785,6 +3798,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   for (int k = 0; k < DIM; k++) g_out[i * DIM + k] = maskG ? 0.0f : mean[k + 1];
   if (nest_out) nest_out[i] = sN;
   if (steps_out) steps_out[i] = (int32_t)steps;
+  if (tk.deriv) tk.deriv[i] = sDeriv / (float)(sN > 1 ? sN : 1);  // getEstimatedDerivative (unmasked)
 }
 
 }  // namespace wos

@@ -43,7 +43,9 @@ hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t
 hipError_t launch_bvc_point_info(const DevScene& sc, const float* pts, int64_t n, float* dd, float* nd,
                                  int32_t* inside, float* src, hipStream_t s);
 hipError_t launch_bvc_start(const DevScene& sc, const DevParams& prm, const float* bpt, const float* bnrm,
-                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, hipStream_t s);
+                            const uint8_t* aligned, const float* bdd, int64_t nb, const DevTasks& tk, int on_neumann,
+                            uint32_t tag, hipStream_t s);
+hipError_t launch_bvc_fd(const DevScene& sc, const float* pts, const float* sol, int64_t n, float* dn, hipStream_t s);
 hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const DevTasks& tk, int64_t base,
                                int64_t stride, unsigned long long* counters, unsigned int* tqueue, int grid,
                                size_t shmem, int geom_floats, hipStream_t s);

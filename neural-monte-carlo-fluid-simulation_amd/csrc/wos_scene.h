@@ -115,6 +115,8 @@ struct DevParams {
   int32_t ignore_source;
   int32_t robust;           // wos_solver_params.robust_float (Gfn::scaled)
   int32_t neumann_inert;    // 1: no ball can reach the float-overflow regime (walk kernel without the Neumann term)
+  int32_t force_estimate;   // 1: estimate every point, inside the domain or not (BVC's Dirichlet samples:
+                            // BoundarySampler::computeEstimates solves at every sample, boundary_sampler.h:125-166)
   uint64_t seed;
   // PCG32 jump-ahead table: jump[2k], jump[2k+1] = (A_k, C_k) with
   // state_k = A_k * state_0 + C_k (mod 2^64); lets the lanes of a wave draw the
@@ -165,6 +167,11 @@ struct DevTasks {
   // reference-semantics first-ball kernel; nullptr: the first-ball kernel evaluates them
   float* pball;
   int64_t pball_stride;
+  // per point [n][DIM] SampleEstimationData::directionForDerivative (nullptr: (1, 0[, 0]),
+  // walk_on_stars.h:665-666) and the estimated directional derivative out [n]
+  // (getEstimatedDerivative, :843-846; nullptr: not computed) -- BVC's Dirichlet samples
+  const float* ddir;
+  float* deriv;
 };
 
 // floats per task: start state pt[DIM] thr tsrc dd, record first bdir[DIM] sdir[DIM] total code

@@ -74,7 +74,7 @@ class BvcParams(C.Structure):
                 ("boundary_cache_size", C.c_int32), ("domain_cache_size", C.c_int32),
                 ("grid_res", C.c_int32), ("use_finite_differences", C.c_int32),
                 ("normal_offset", C.c_float), ("radius_clamp", C.c_float),
-                ("kernel_regularization", C.c_float)]
+                ("kernel_regularization", C.c_float), ("grid_box", C.c_float * 4)]
 
 
 class Stats(C.Structure):

@@ -69,9 +69,10 @@ def solver_params(solver=None, output=None, seed=None, schedule=0):
     return p
 
 
-def bvc_params(solver=None, output=None):
+def bvc_params(solver=None, output=None, grid_box=None):
     """The boundary-value-caching keys runBoundaryValueCaching reads (demo.cpp:269-290):
-    same names and defaults; output.gridRes is required."""
+    same names and defaults; output.gridRes is required.  grid_box = (x0, y0, ex, ey): the
+    rectangle of the evaluation grid (None: the scene's bounding box, demo.cpp:311)."""
     s = dict(solver or {})
     o = dict(output or {})
     if "gridRes" not in o:
@@ -88,6 +89,9 @@ def bvc_params(solver=None, output=None):
     b.normal_offset = _get_opt(s, "normalOffsetForCachedDirichletSamples", 5.0 * eps, float)
     b.radius_clamp = _get_opt(s, "radiusClampForKernels", 1e-3, float)
     b.kernel_regularization = _get_opt(s, "regularizationForKernels", 0.0, float)
+    if grid_box is not None:
+        for k in range(4):
+            b.grid_box[k] = float(grid_box[k])
     return b
 
 
@@ -277,10 +281,10 @@ class WosScene:
 
     def bvc(self, params=None, bvc=None, samples=True):
         """Boundary value caching (wos_bvc; the reference's bvc, demo.cpp:265-363) on this
-        2D all-Neumann scene.  Returns (solution [g, g], grad [g, g, 2], info) on the
-        evaluation grid (index [i, j] = point (i/g, j/g) of the bounding box, masked as
+        2D scene (Neumann and Dirichlet boundaries).  Returns (solution [g, g], grad [g, g, 2],
+        info) on the evaluation grid (index [i, j] = point (i/g, j/g) of the grid box, masked as
         saveEvaluationGrid masks); info holds the sample counts, the cached samples
-        ([k, 8]: x y nx ny pdf value normalDerivative kind) and the stats."""
+        ([k, 8]: x y nx ny pdf value normalDerivative kind, include/wos.h) and the stats."""
         L = _lib.load()
         params = params if params is not None else solver_params()
         if bvc is None:

@@ -1635,7 +1635,7 @@ typedef struct {
 } pcount_t;
 
 static void estimate_point(const scene_t *sc, const oracle_params *prm, const float *x, uint64_t gidx,
-                           float dDist, float nDist, stats_t *S, pcount_t *pc)
+                           float dDist, float nDist, stats_t *S, pcount_t *pc, const float *ddir)
 {
     const int dim = sc->dim;
     int nWalks = prm->n_walks, nAnti = 1;
@@ -1651,7 +1651,9 @@ static void estimate_point(const scene_t *sc, const oracle_params *prm, const fl
         pcg_t ps; pcg_seed(&ps, oracle_seed32(prm->seed, gidx, 0, 0), 1u);
         gen_stratified(strat, 2 * nWalks, sd, &ps);
     }
-    const float dirForDeriv[3] = {1.0f, 0.0f, 0.0f};
+    /* SampleEstimationData::directionForDerivative: (1, 0[, 0]) by default (walk_on_stars.h:
+     * 665-666); BVC's Dirichlet samples pass their normal (boundary_sampler.h:154-166) */
+    const float dirForDeriv[3] = {ddir ? ddir[0] : 1.0f, ddir ? ddir[1] : 0.0f, ddir && dim == 3 ? ddir[2] : 0.0f};
     int yuk0 = sc->absorption > 0.0f && prm->steps_before_tikhonov == 0;
     for (int w = 0; w < nWalks; w++) {
         float boundaryPdf = 0.0f, sourcePdf = 0.0f, boundaryPt[3] = {0, 0, 0}, sourcePt[3] = {0, 0, 0};
@@ -1705,7 +1707,7 @@ static void estimate_point(const scene_t *sc, const oracle_params *prm, const fl
                     float ct = fabsf(bd[dim - 1]);
                     float pdfc = dim == 2 ? ct / 2.0f : (float)((double)ct / PI_D);
                     boundaryPdf = 0.5f * pdfc;
-                    /* transformCoordinates (sampling.h:176-203) with n = (1,0[,0]) */
+                    /* transformCoordinates (sampling.h:176-203) with n = directionForDerivative */
                     const float *n = dirForDeriv;
                     if (dim == 2) {
                         float s0 = n[1], s1 = -n[0];
@@ -1801,7 +1803,7 @@ static void solve_one(job_t *J, int64_t i, pcount_t *pc, uint64_t *nest)
     int estimated = 0;
     pcount_t before = *pc;
     if (inside || sc->double_sided) {
-        estimate_point(sc, J->prm, x, (uint64_t)(J->base + i * J->stride), dDist, nDist, &S, pc);
+        estimate_point(sc, J->prm, x, (uint64_t)(J->base + i * J->stride), dDist, nDist, &S, pc, NULL);
         estimated = 1; (*nest)++;
     }
     float mask = J->prm->boundary_distance_mask;
@@ -1926,7 +1928,7 @@ double oracle_math(int which, double x, int math_mode)
 /* ========================================================================= */
 /* Boundary value caching: runBoundaryValueCaching (demo.cpp:265-363) over    */
 /* boundary_value_caching/{boundary_sampler,domain_sampler,splatter}.h, 2D,   */
-/* all-Neumann scenes (scene.h:39,68).                                        */
+/* Neumann and Dirichlet boundaries.                                          */
 /* RNG (documented deviation): boundary sampler stream seed32(key,0,0,4),     */
 /* domain sampler seed32(key,0,0,5), walk w of boundary sample i             */
 /* seed32(key,i,w,6); sampled segments visited in ascending order (the        */
@@ -1956,22 +1958,79 @@ static int cdf_sample(const float *table, int size, float u)
     return sclampi(first - 1, 0, size - 2);
 }
 
-/* buildCDFTable (boundary_sampler.h:291-331), every segment on the Neumann boundary */
-static float bvc_table(const geom_t *g, const scene_t *sc, float offset, float *table)
+/* The BoundarySampler's boundary (boundary_sampler.h:87-412): every segment of the scene, here the
+ * Neumann segments then the Dirichlet ones (the reference: the OBJ's order, typed by
+ * onNeumannBoundary at the midpoint, demo.cpp:300-313); Dirichlet vertices carry the sampler's
+ * own vertex normals (computeNormals :193-236: unit segment normals summed, normalised), per
+ * part (a vertex shared by a Neumann and a Dirichlet segment keeps its Dirichlet normal). */
+typedef struct {
+    int ns, nn;                 /* segments, of which the first nn are Neumann */
+    const float *(*a), *(*b);   /* endpoints */
+    const float *(*na), *(*nb); /* Dirichlet vertex normals (NULL for Neumann segments) */
+    float (*dn)[3];             /* storage of the Dirichlet vertex normals */
+} bseg_t;
+
+static void bseg_build(const scene_t *sc, bseg_t *B)
 {
-    float *w = calloc((size_t)g->np + 1, sizeof(float));
-    for (int i = 0; i < g->np; i++) {
-        const float *pa = g->v[g->ix[i][0]], *pb = g->v[g->ix[i][1]];
-        float pm[2] = {(pa[0] + pb[0]) / 2.0f, (pa[1] + pb[1]) / 2.0f};
+    const geom_t *N = &sc->neu, *D = &sc->dir;
+    B->nn = N->np; B->ns = N->np + D->np;
+    B->a = calloc((size_t)B->ns + 1, sizeof(float *)); B->b = calloc((size_t)B->ns + 1, sizeof(float *));
+    B->na = calloc((size_t)B->ns + 1, sizeof(float *)); B->nb = calloc((size_t)B->ns + 1, sizeof(float *));
+    B->dn = calloc((size_t)D->nv + 1, sizeof(float[3]));
+    for (int p = 0; p < D->np; p++) {
+        const float *pa = D->v[D->ix[p][0]], *pb = D->v[D->ix[p][1]];
         float s0 = pb[0] - pa[0], s1 = pb[1] - pa[1];
+        float n[2] = {s1, -s0};
+        float z = n[0] * n[0] + n[1] * n[1];
+        if (z > 0.0f) { float r = sqrtf(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+        for (int q = 0; q < 2; q++) { float *v = B->dn[D->ix[p][q]]; v[0] += n[0]; v[1] += n[1]; }
+    }
+    for (int i = 0; i < D->nv; i++) {
+        float z = B->dn[i][0] * B->dn[i][0] + B->dn[i][1] * B->dn[i][1];
+        if (z > 0.0f) { float r = sqrtf(z); B->dn[i][0] /= r; B->dn[i][1] /= r; }
+    }
+    for (int i = 0; i < N->np; i++) { B->a[i] = N->v[N->ix[i][0]]; B->b[i] = N->v[N->ix[i][1]]; }
+    for (int p = 0; p < D->np; p++) {
+        int i = N->np + p;
+        B->a[i] = D->v[D->ix[p][0]]; B->b[i] = D->v[D->ix[p][1]];
+        B->na[i] = B->dn[D->ix[p][0]]; B->nb[i] = B->dn[D->ix[p][1]];
+    }
+}
+
+static void bseg_free(bseg_t *B) { free(B->a); free(B->b); free(B->na); free(B->nb); free(B->dn); }
+
+/* segment i's endpoints, a Dirichlet segment's displaced along its vertex normals by `offset`
+ * (`pa += normalOffset*normals[index[0]]`, boundary_sampler.h:307-310,367-370) */
+static void bseg_ends(const bseg_t *B, int i, float offset, float *pa, float *pb)
+{
+    pa[0] = B->a[i][0]; pa[1] = B->a[i][1]; pb[0] = B->b[i][0]; pb[1] = B->b[i][1];
+    if (i >= B->nn) {
+        pa[0] += offset * B->na[i][0]; pa[1] += offset * B->na[i][1];
+        pb[0] += offset * B->nb[i][0]; pb[1] += offset * B->nb[i][1];
+    }
+}
+
+/* buildCDFTable (boundary_sampler.h:291-331) */
+static float bvc_table(const bseg_t *B, const scene_t *sc, float offset, float *table)
+{
+    float *w = calloc((size_t)B->ns + 1, sizeof(float));
+    for (int i = 0; i < B->ns; i++) {
+        const float *pa0 = B->a[i], *pb0 = B->b[i];
+        float pm[2] = {(pa0[0] + pb0[0]) / 2.0f, (pa0[1] + pb0[1]) / 2.0f};
+        float s0 = pb0[0] - pa0[0], s1 = pb0[1] - pa0[1];
         float n[2] = {s1, -s0};
         float z = n[0] * n[0] + n[1] * n[1];
         if (z > 0.0f) { float r = sqrtf(z); n[0] = n[0] / r; n[1] = n[1] / r; }
         float q[2] = {pm[0] + offset * n[0], pm[1] + offset * n[1]};
         int in = q[0] >= sc->pmin[0] && q[1] >= sc->pmin[1] && q[0] <= sc->pmax[0] && q[1] <= sc->pmax[1];
-        if (in) w[i] = sqrtf(s1 * s1 + (-s0) * (-s0));
+        if (in) {
+            float pa[2], pb[2];
+            bseg_ends(B, i, offset, pa, pb);
+            float t0 = pb[0] - pa[0], t1 = pb[1] - pa[1];
+            w[i] = sqrtf(t1 * t1 + (-t0) * (-t0));
+        }
     }
-    float total = cdf_build(table, w, g->np);
+    float total = cdf_build(table, w, B->ns);
     free(w);
     return total;
 }
@@ -1983,27 +2042,31 @@ static void rec_push(recbuf_t *b, const float *r)
     memcpy(b->rec + 8 * (size_t)b->n, r, sizeof(float) * 8); b->n++;
 }
 
+/* sample kinds of the cache records [x y nx ny pdf value dn/dn kind] */
+enum { KB_NEUMANN = 0, KB_NEUMANN_ALIGNED = 1, KB_DOMAIN = 2, KB_DIRICHLET = 3, KB_DIRICHLET_ALIGNED = 4 };
+
 /* generateSamples (boundary_sampler.h:333-402) */
-static void bvc_gen_boundary(const geom_t *g, const float *table, int n, float total, int aligned, pcg_t *rng,
-                             recbuf_t *out, float pdf)
+static void bvc_gen_boundary(const bseg_t *B, const float *table, int n, float total, float offset, int aligned,
+                             pcg_t *rng, recbuf_t *out, float pdf)
 {
     if (!(total > 0.0f) || n <= 0) return;
     float *strat = malloc(sizeof(float) * (size_t)n);
     gen_stratified(strat, n, 1, rng);
-    int *count = calloc((size_t)g->np, sizeof(int));
-    for (int i = 0; i < n; i++) count[cdf_sample(table, g->np + 1, strat[i])]++;
-    for (int f = 0; f < g->np; f++) {
+    int *count = calloc((size_t)B->ns, sizeof(int));
+    for (int i = 0; i < n; i++) count[cdf_sample(table, B->ns + 1, strat[i])]++;
+    for (int f = 0; f < B->ns; f++) {
         int c = count[f];
         if (!c) continue;
         float *u = malloc(sizeof(float) * (size_t)c);
         if (c == 1) u[0] = pcg_float(rng); else gen_stratified(u, c, 1, rng);
-        const float *pa = g->v[g->ix[f][0]], *pb = g->v[g->ix[f][1]];
+        float pa[2], pb[2];
+        bseg_ends(B, f, offset, pa, pb);
         float s0 = pb[0] - pa[0], s1 = pb[1] - pa[1];
+        float kind = f >= B->nn ? (aligned ? KB_DIRICHLET_ALIGNED : KB_DIRICHLET) : (aligned ? KB_NEUMANN_ALIGNED : KB_NEUMANN);
         for (int i = 0; i < c; i++) {
             float nn[2] = {s1, -s0};
             float norm = sqrtf(nn[0] * nn[0] + nn[1] * nn[1]);
-            float r[8] = {pa[0] + u[i] * s0, pa[1] + u[i] * s1, nn[0] / norm, nn[1] / norm, pdf, 0.0f, 0.0f,
-                          aligned ? 1.0f : 0.0f};
+            float r[8] = {pa[0] + u[i] * s0, pa[1] + u[i] * s1, nn[0] / norm, nn[1] / norm, pdf, 0.0f, 0.0f, kind};
             rec_push(out, r);
         }
         free(u);
@@ -2011,16 +2074,19 @@ static void bvc_gen_boundary(const geom_t *g, const float *table, int n, float t
     free(count); free(strat);
 }
 
-/* estimateSolution (walk_on_stars.h:353-464) at a boundary sample */
+/* estimateSolution (walk_on_stars.h:353-464) at a sample point: on the Neumann boundary (a
+ * boundary sample) or in the domain (an evaluation point near the Dirichlet boundary,
+ * splatter.h:160-196, or a finite-difference Dirichlet sample); walk w seeded
+ * seed32(key, sidx, w, tag) */
 static float bvc_estimate(const scene_t *sc, const oracle_params *prm, const float *pt, const float *nrm, int aligned,
-                          int nWalks, uint64_t sidx, pcount_t *pc)
+                          int on_neumann, int nWalks, uint64_t sidx, uint32_t tag, pcount_t *pc)
 {
     float x[3] = {pt[0], pt[1], 0.0f};
     float dDist = dist_dirichlet(sc, x, 0);
     if (dDist <= prm->epsilon_shell) nWalks = 1;
     float cn[3] = {nrm[0], nrm[1], 0.0f};
     int flip = 0;
-    if (sc->double_sided && aligned) { cn[0] *= -1.0f; cn[1] *= -1.0f; flip = 1; }
+    if (sc->double_sided && on_neumann && aligned) { cn[0] *= -1.0f; cn[1] *= -1.0f; flip = 1; }
     float firstR;
     if (dDist > prm->epsilon_shell && prm->steps_before_maximal_spheres != 0) {
         firstR = star_radius(&sc->neu, x, prm->min_star_radius, dDist, prm->silhouette_precision, flip);
@@ -2034,13 +2100,13 @@ static float bvc_estimate(const scene_t *sc, const oracle_params *prm, const flo
         gfn_t g; gfn_init(&g, 2, yuk0, sc->absorption);
         wstate_t st; memset(&st, 0, sizeof(st));
         memcpy(st.pt, x, 12); memcpy(st.n, cn, 12); memcpy(st.prevDir, cn, 12);
-        st.prevDist = FLT_MAX; st.throughput = 1.0f; st.onNeumann = 1;
-        pcg_t ws; pcg_seed(&ws, oracle_seed32(prm->seed, sidx, (uint64_t)w, 6), 1u);
+        st.prevDist = FLT_MAX; st.throughput = 1.0f; st.onNeumann = on_neumann;
+        pcg_t ws; pcg_seed(&ws, oracle_seed32(prm->seed, sidx, (uint64_t)w, tag), 1u);
         wcount_t wc = {0, 0};
         int code = walk(sc, prm, dDist, firstR, &ws, &g, &st, &wc);
         pc->iters += wc.iters;
         if (code == WC_DIRICHLET || code == WC_RR) {
-            float term = (code == WC_DIRICHLET && !prm->ignore_dirichlet) ? sc->g_dirichlet : 0.0f;
+            float term = (code == WC_DIRICHLET && !prm->ignore_dirichlet) ? dirichlet_value(sc, st.pt) : 0.0f;
             float total = st.throughput * term + st.totalNeumann + st.totalSource;
             N += 1;
             float delta = total - mean;
@@ -2083,6 +2149,7 @@ static void bvc_splat_point(const fs2_t *gf, const float *x, const recbuf_t *rb,
     for (int j = 0; j < rb->n; j++) {
         const float *R = rb->rec + 8 * (size_t)j;
         int kind = (int)R[7];
+        int slot = kind == KB_DOMAIN ? 2 : (kind == KB_NEUMANN_ALIGNED || kind == KB_DIRICHLET_ALIGNED) ? 1 : 0;
         float pdf = R[4], value = R[5];
         float yx[2] = {R[0] - x[0], R[1] - x[1]}, xy[2] = {x[0] - R[0], x[1] - R[1]};
         float r = smaxf(radius_clamp, sqrtf(yx[0] * yx[0] + yx[1] * yx[1]));
@@ -2101,8 +2168,8 @@ static void bvc_splat_point(const fs2_t *gf, const float *x, const recbuf_t *rb,
         }
         float dGNorm = sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
         float est, ge[2];
-        if (kind != 2) {
-            float sg = kind == 1 ? -1.0f : 1.0f;
+        if (kind != KB_DOMAIN) {
+            float sg = slot == 1 ? -1.0f : 1.0f;
             float n[2] = {R[2] * sg, R[3] * sg};
             float nd = n[0] * xy[0] + n[1] * xy[1];
             float P, dP[2];
@@ -2132,7 +2199,7 @@ static void bvc_splat_point(const fs2_t *gf, const float *x, const recbuf_t *rb,
             est = (G * value) / pdf;
             for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
         }
-        sstat_add(&st[kind], est, ge);
+        sstat_add(&st[slot], est, ge);
     }
     float v = st[0].mean; v += st[1].mean; v += st[2].mean;
     *sol = v;
@@ -2144,39 +2211,69 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
                oracle_stats *stats)
 {
     if (!scene || !prm || !bp || !solution || !grad) return -1;
-    if (scene->dim != 2 || scene->n_dprims > 0 || scene->n_prims <= 0 || bp->grid_res < 1 ||
-        bp->n_walks_solution < 1) return -2;
+    if (scene->dim != 2 || scene->n_prims + scene->n_dprims <= 0 || bp->grid_res < 1 || bp->n_walks_solution < 1 ||
+        (scene->n_dprims > 0 && bp->n_walks_gradient < 1)) return -2;
     scene_t sc;
     g_libm = prm->math_mode == 1;
     g_robust = prm->robust_float != 0;
     if (scene_build(&sc, scene)) { scene_free(&sc); return -3; }
     const geom_t *g = &sc.neu;
+    bseg_t B; bseg_build(&sc, &B);
     recbuf_t rb = {0};
-    /* ---- boundary samples */
+    /* ---- boundary samples (BoundarySampler::initialize + generateSamples, demo.cpp:316-318) */
     pcg_t bs; pcg_seed(&bs, oracle_seed32(prm->seed, 0, 0, 4), 1u);
-    float *t_main = malloc(sizeof(float) * ((size_t)g->np + 1)), *t_al = malloc(sizeof(float) * ((size_t)g->np + 1));
-    float a_main = bvc_table(g, &sc, -1.0f * bp->normal_offset, t_main);
+    float *t_main = malloc(sizeof(float) * ((size_t)B.ns + 1)), *t_al = malloc(sizeof(float) * ((size_t)B.ns + 1));
+    float a_main = bvc_table(&B, &sc, -1.0f * bp->normal_offset, t_main);
     int nb_main, nb_al = 0;
     if (sc.double_sided) {
-        float a_al = bvc_table(g, &sc, bp->normal_offset, t_al);
+        float a_al = bvc_table(&B, &sc, bp->normal_offset, t_al);
         float total = a_main + a_al;
         int n_main = (int)ceilf((float)bp->boundary_cache_size * a_main / total);
         int n_al = (int)ceilf((float)bp->boundary_cache_size * a_al / total);
-        bvc_gen_boundary(g, t_main, n_main, a_main, 0, &bs, &rb, 1.0f / a_main);
+        bvc_gen_boundary(&B, t_main, n_main, a_main, -1.0f * bp->normal_offset, 0, &bs, &rb, 1.0f / a_main);
         nb_main = rb.n;
-        bvc_gen_boundary(g, t_al, n_al, a_al, 1, &bs, &rb, 1.0f / a_al);
+        bvc_gen_boundary(&B, t_al, n_al, a_al, bp->normal_offset, 1, &bs, &rb, 1.0f / a_al);
         nb_al = rb.n - nb_main;
     } else {
-        bvc_gen_boundary(g, t_main, bp->boundary_cache_size, a_main, 0, &bs, &rb, 1.0f / a_main);
+        bvc_gen_boundary(&B, t_main, bp->boundary_cache_size, a_main, -1.0f * bp->normal_offset, 0, &bs, &rb,
+                         1.0f / a_main);
         nb_main = rb.n;
     }
     free(t_main); free(t_al);
-    /* ---- estimates at the boundary samples (BoundarySampler::computeEstimates) */
+    /* ---- estimates at the boundary samples (BoundarySampler::computeEstimates :121-190):
+     * Neumann samples estimateSolution (nWalksForCachedSolutionEstimates, walks tag 6);
+     * Dirichlet samples estimateSolutionAndGradient along their normal (nWalksForCachedGradient-
+     * Estimates, keyed by the sample index) -> solution and normal derivative, or with
+     * useFiniteDifferences estimateSolution in the domain (tag 8) and (g(proj) - u)/|d| */
     pcount_t pc; memset(&pc, 0, sizeof(pc));
     for (int i = 0; i < rb.n; i++) {
         float *R = rb.rec + 8 * (size_t)i;
-        R[5] = bvc_estimate(&sc, prm, R, R + 2, R[7] == 1.0f, bp->n_walks_solution, (uint64_t)i, &pc);
-        R[6] = 0.0f;  /* pde.neumann == 0 (scene.h:176-181) */
+        int kind = (int)R[7], al = kind == KB_NEUMANN_ALIGNED || kind == KB_DIRICHLET_ALIGNED;
+        if (kind == KB_NEUMANN || kind == KB_NEUMANN_ALIGNED) {
+            R[5] = bvc_estimate(&sc, prm, R, R + 2, al, 1, bp->n_walks_solution, (uint64_t)i, 6u, &pc);
+            R[6] = 0.0f;  /* pde.neumann == 0 (scene.h:176-181) */
+            continue;
+        }
+        float x[3] = {R[0], R[1], 0.0f};
+        if (bp->use_finite_differences) {
+            R[5] = bvc_estimate(&sc, prm, R, R + 2, al, 0, bp->n_walks_gradient, (uint64_t)i, 8u, &pc);
+            cp_t c;
+            float gv = sc.g_dirichlet, sd = 0.0f;
+            if (closest_point(&sc.dir, x, &c, sc.double_sided) >= 0) {
+                gv = dirichlet_value(&sc, x);
+                sd = sc.double_sided ? signed_distance(&c, x) : c.d;
+            }
+            R[6] = (gv - R[5]) / fabsf(sd);
+            continue;
+        }
+        float dir[3] = {R[2], R[3], 0.0f};
+        if (sc.double_sided && al) { dir[0] *= -1.0f; dir[1] *= -1.0f; }
+        stats_t S;
+        oracle_params wp = *prm;
+        wp.n_walks = bp->n_walks_gradient;
+        estimate_point(&sc, &wp, x, (uint64_t)i, dist_dirichlet(&sc, x, 0), dist_neumann(&sc, x, 0), &S, &pc, dir);
+        R[5] = S.solMean;
+        R[6] = S.totalDeriv / (float)(S.nSol > 1 ? S.nSol : 1);
     }
     /* ---- domain samples (DomainSampler::generateSamples) */
     int nd_kept = 0;
@@ -2185,10 +2282,16 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
         float vol;
         if (sc.double_sided) vol = ext[0] * ext[1];
         else {
+            /* getSolveRegionVolume (scene.h:92-100): |signed area of the Dirichlet part + the Neumann part| */
             float sv = 0.0f;
-            for (int p = 0; p < g->np; p++) {
-                const float *pa = g->v[g->ix[p][0]], *pb = g->v[g->ix[p][1]];
-                sv += 0.5f * (pa[0] * pb[1] - pa[1] * pb[0]);
+            const geom_t *parts[2] = {&sc.dir, g};
+            for (int q = 0; q < 2; q++) {
+                float sq = 0.0f;
+                for (int p = 0; p < parts[q]->np; p++) {
+                    const float *pa = parts[q]->v[parts[q]->ix[p][0]], *pb = parts[q]->v[parts[q]->ix[p][1]];
+                    sq += 0.5f * (pa[0] * pb[1] - pa[1] * pb[0]);
+                }
+                sv += sq;
             }
             vol = fabsf(sv);
         }
@@ -2210,16 +2313,28 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
             free(strat);
         }
     }
-    /* ---- splat onto the evaluation grid (createEvaluationGrid grid.h:352-368, saveEvaluationGrid 370-414) */
+    /* ---- splat onto the evaluation grid (createEvaluationGrid grid.h:352-368, saveEvaluationGrid 370-414)
+     * over bp->grid_box (x0, y0, ex, ey; extent 0: the scene's box); points closer to the Dirichlet
+     * boundary than normalOffset take a pointwise estimateSolution instead (splatter.h:160-196,
+     * nWalksForCachedSolutionEstimates, walks seed32(key, rank, w, 7)) with a zero gradient */
     fs2_t gf = {sc.absorption > 0.0f, sc.absorption, sqrtf(sc.absorption)};
     const int res = bp->grid_res;
+    float gmin[2] = {sc.pmin[0], sc.pmin[1]};
     float ext[2] = {sc.pmax[0] - sc.pmin[0], sc.pmax[1] - sc.pmin[1]};
+    if (bp->grid_box[2] > 0.0f && bp->grid_box[3] > 0.0f) {
+        gmin[0] = bp->grid_box[0]; gmin[1] = bp->grid_box[1]; ext[0] = bp->grid_box[2]; ext[1] = bp->grid_box[3];
+    }
+    uint64_t n_near = 0;  /* rank of an evaluation point among those near the Dirichlet boundary: its walks' key */
     for (int i = 0; i < res; i++) for (int j = 0; j < res; j++) {
         size_t q = (size_t)i * res + j;
-        float x[3] = {((float)i / (float)res) * ext[0] + sc.pmin[0], ((float)j / (float)res) * ext[1] + sc.pmin[1], 0.0f};
+        float x[3] = {((float)i / (float)res) * ext[0] + gmin[0], ((float)j / (float)res) * ext[1] + gmin[1], 0.0f};
         float dDist = dist_dirichlet(&sc, x, 0), nDist = dist_neumann(&sc, x, 0);
         float v = 0.0f, gv[2] = {0.0f, 0.0f};
         if (!(dDist < bp->normal_offset)) bvc_splat_point(&gf, x, &rb, bp->radius_clamp, bp->kernel_regularization, &v, gv);
+        else if (sc.dir.np > 0) {
+            static const float zero[2] = {0.0f, 0.0f};
+            v = bvc_estimate(&sc, prm, x, zero, 0, 0, bp->n_walks_solution, n_near++, 7u, &pc);
+        }
         int in = inside_domain(&sc, x);
         int masked = (!in && !sc.double_sided) || sminf(fabsf(dDist), fabsf(nDist)) < prm->boundary_distance_mask;
         solution[q] = masked ? 0.0f : v;
@@ -2240,6 +2355,7 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
         stats->rejection_iters = pc.iters;
     }
     free(rb.rec);
+    bseg_free(&B);
     scene_free(&sc);
     return rc;
 }

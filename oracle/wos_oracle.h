@@ -102,11 +102,13 @@ int oracle_solve_m2(const oracle_scene_desc *scene, const oracle_params *prm,
                     oracle_stats *stats);
 
 /* Boundary value caching: runBoundaryValueCaching (bindings/zombie/demo/demo.cpp:
- * 265-363), 2D all-Neumann scenes.  Outputs as wos_bvc (include/wos.h). */
+ * 265-363), 2D scenes with Neumann and Dirichlet boundaries.  Outputs as wos_bvc
+ * (include/wos.h). */
 typedef struct oracle_bvc_params {
     int32_t n_walks_solution, n_walks_gradient, boundary_cache_size, domain_cache_size, grid_res;
     int32_t use_finite_differences;
     float normal_offset, radius_clamp, kernel_regularization;
+    float grid_box[4];        /* evaluation grid x0, y0, ex, ey (extent 0: the scene's bounding box) */
 } oracle_bvc_params;
 
 int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const oracle_bvc_params *bvc,

@@ -49,7 +49,7 @@ class BvcParams(C.Structure):
                 ("boundary_cache_size", C.c_int32), ("domain_cache_size", C.c_int32),
                 ("grid_res", C.c_int32), ("use_finite_differences", C.c_int32),
                 ("normal_offset", C.c_float), ("radius_clamp", C.c_float),
-                ("kernel_regularization", C.c_float)]
+                ("kernel_regularization", C.c_float), ("grid_box", C.c_float * 4)]
 
 
 class Stats(C.Structure):
@@ -259,8 +259,9 @@ def seed32(key, idx, pair, tag):
     return int(lib().oracle_seed32(key, idx, pair, tag))
 
 
-def bvc_params(solver=None, output=None):
-    """Oracle copy of the BVC keys (demo.cpp:269-290), same defaults as the product's."""
+def bvc_params(solver=None, output=None, grid_box=None):
+    """Oracle copy of the BVC keys (demo.cpp:269-290), same defaults as the product's;
+    grid_box = (x0, y0, ex, ey) of the evaluation grid (None: the scene's bounding box)."""
     s = dict(solver or {})
     o = dict(output or {})
     b = BvcParams()
@@ -274,6 +275,8 @@ def bvc_params(solver=None, output=None):
     b.normal_offset = float(s.get("normalOffsetForCachedDirichletSamples", 5.0 * eps))
     b.radius_clamp = float(s.get("radiusClampForKernels", 1e-3))
     b.kernel_regularization = float(s.get("regularizationForKernels", 0.0))
+    for k in range(4):
+        b.grid_box[k] = 0.0 if grid_box is None else float(grid_box[k])
     return b
 
 

@@ -135,27 +135,36 @@ def test_bvc_dirichlet_disk_kat_gpu(gpu):
 
 def test_bvc_values_match_reference_bvc_pfm(gpu):
     """The engine demo's own solutions/bvc.pfm (bvc.json: 6144 boundary samples, 96 / 960 walks)
-    against the HIP BVC: the zero pattern exactly; per unmasked pixel z = (p_ref - mean)/sigma
-    over K = 16 independent keys (sigma^2 = s^2 (1 + 1/K), s the spread of one run) -- the
-    splatted cache's error is correlated across pixels, so the bar is on chi^2/N (< 1.5) and
-    the share of |z| > 4 (<= 1 %), not on the mean."""
+    against the HIP BVC over K = 64 independent keys: the zero pattern exactly, and per unmasked
+    pixel z = (p_ref - mean)/(s sqrt(1 + 1/K)), s the per-pixel spread of one run.  A splatted
+    cache's error is correlated across the whole image, so chi^2/N of ONE image is itself widely
+    spread; its calibration is the leave-one-out chi^2/N of each of our own runs against the
+    other K - 1.  Pass: the reference's chi^2/N within that distribution (<= its 95th percentile)
+    and at most 1 % of |z| > 4 -- the reference's image behaves like one more run of this
+    estimator."""
     U, sc, _ = _engine_scenes(None)
     solver, output = _engine_bvc(small=False)
-    K = 16
+    K = 64
     runs = [sc.bvc(solver_params(solver, output, seed=0x5EED5000 + s),
                    bvc_params(solver, output, grid_box=U["box"]), samples=False)[0].ravel() for s in range(K)]
     sc.close()
     R = np.asarray(runs, np.float64)
     ref = U["bvc_values"]
     zero = ref == 0
-    assert ((R[0] == 0) == zero).all()
+    assert all(((r == 0) == zero).all() for r in R)
     m, sd = R.mean(0), R.std(0, ddof=1)
     ok = ~zero & (sd > 0)
     z = (ref[ok] - m[ok]) / (sd[ok] * np.sqrt(1.0 + 1.0 / K))
-    stats = {"n": int(ok.sum()), "mean_z": float(z.mean()), "chi2_n": float((z * z).mean()),
+    calib = []
+    for k in range(K):
+        o = np.delete(R, k, 0)
+        zz = (R[k][ok] - o.mean(0)[ok]) / (o.std(0, ddof=1)[ok] * np.sqrt(1.0 + 1.0 / (K - 1)))
+        calib.append(float((zz * zz).mean()))
+    stats = {"n": int(ok.sum()), "chi2_n": float((z * z).mean()), "mean_z": float(z.mean()),
              "frac_z4": float((np.abs(z) > 4).mean()), "mean_diff": float((ref[ok] - m[ok]).mean()),
-             "rms_diff": float(np.sqrt(((ref[ok] - m[ok]) ** 2).mean())), "mean_sd": float(sd[ok].mean())}
+             "rms_diff": float(np.sqrt(((ref[ok] - m[ok]) ** 2).mean())), "mean_sd": float(sd[ok].mean()),
+             "calib_chi2_n_pct5_50_95": [float(v) for v in np.percentile(calib, [5, 50, 95])]}
     print("HIP BVC vs bvc.pfm", stats)
     assert stats["n"] == 65536 - 36665
-    assert stats["chi2_n"] < 1.5, stats
+    assert stats["chi2_n"] <= np.percentile(calib, 95), stats
     assert stats["frac_z4"] <= 0.01, stats

@@ -9,7 +9,11 @@ is the vector-instruction issue rate.  valu_issue_frac = SQ_INSTS_VALU x 4 cycle
 2.4 GHz x 256 CUs x 4 SIMDs), the kernel time from the same pass's dispatch
 timestamps; the SQ_WAIT_* split says how much of a wave's life is spent parked on
 memory / LDS waits (s_waitcnt) versus stalled at issue.
-    python3 tools/collect_sq.py [tag] [config]
+    python3 tools/collect_sq.py [tag] [config] [set]
+
+set "issue" (default) is the pass above; "mix" and "mix2" are the instruction-mix passes
+(VALU by type: F64 add/mul/fma/transcendental, F32, INT32/64, conversions; SALU and
+scalar-pipe active cycles, branches, scalar loads), written to <tag>_<set>_walk_sq.json.
 """
 import csv
 import glob
@@ -24,9 +28,18 @@ from bench import lib_sha16  # noqa: E402
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 CONFIG = sys.argv[2] if len(sys.argv) > 2 else "B"
-OUT = os.path.join(REPO, "gpurun_out", f"{TAG}_sq")
-COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
-            "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
+SET = sys.argv[3] if len(sys.argv) > 3 else "issue"
+SETS = {
+    "issue": ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+              "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"],
+    "mix": ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
+            "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"],
+    "mix2": ["SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_ACTIVE_INST_VALU",
+             "SQ_ACTIVE_INST_SCA", "SQ_INST_CYCLES_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_SMEM"],
+}
+COUNTERS = SETS[SET]
+PFX = TAG if SET == "issue" else f"{TAG}_{SET}"
+OUT = os.path.join(REPO, "gpurun_out", f"{PFX}_sq")
 CLOCK_HZ, SIMDS = 2.4e9, 256 * 4
 
 
@@ -51,8 +64,12 @@ def main():
         n = len(ds)
         mean = {c: sum(per[d].get(c, 0.0) for d in ds) / n for c in COUNTERS}
         t = sum(dur[d] for d in ds) / n
-        return {"kernel": name, "config": CONFIG, "lib_sha16": lib_sha16(), "dispatches": n, "kernel_s": t,
-                "counters": mean,
+        res = {"kernel": name, "config": CONFIG, "lib_sha16": lib_sha16(), "dispatches": n, "kernel_s": t,
+               "counters": mean,
+               "source": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass), bench.py --steps 2 --warmup 1"}
+        if SET != "issue":
+            return res
+        return {**res,
                 "valu_issue_frac": mean["SQ_INSTS_VALU"] * 4 / (t * CLOCK_HZ * SIMDS),
                 "wait_any_frac": mean["SQ_WAIT_ANY"] / max(mean["SQ_WAVE_CYCLES"], 1.0),
                 "wait_inst_frac": mean["SQ_WAIT_INST_ANY"] / max(mean["SQ_WAVE_CYCLES"], 1.0),
@@ -64,11 +81,11 @@ def main():
         raise SystemExit(f"no wos_walk_kernel records under {OUT}")
     # every kernel of the projection (the first-ball and setup kernels too)
     allk = {k: summary(k) for k in sorted(set(kname.values()))}
-    json.dump(allk, open(os.path.join(REPO, "gpurun_out", f"{TAG}_all_sq.json"), "w"), indent=1)
+    json.dump(allk, open(os.path.join(REPO, "gpurun_out", f"{PFX}_all_sq.json"), "w"), indent=1)
     for k, v in allk.items():
-        print(k, json.dumps({x: v[x] for x in ("kernel_s", "valu_issue_frac", "wait_any_frac", "active_frac")}))
+        print(k, json.dumps({x: v[x] for x in ("kernel_s", "valu_issue_frac", "wait_any_frac", "active_frac") if x in v}))
     res = allk["wos_walk_kernel"]
-    path = os.path.join(REPO, "gpurun_out", f"{TAG}_walk_sq.json")
+    path = os.path.join(REPO, "gpurun_out", f"{PFX}_walk_sq.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res))
 

@@ -47,6 +47,11 @@ def test_gpu_vs_glibc_reference_math_config_b(gpu, oracle):
     rep = {"config": "B karman 128 walks, points[::16]", "points": int(pts.shape[0]), "flipped_points": flips,
            "points_with_any_bit_difference": differ, "grad_l2_abs": l2, "grad_mc_standard_error_rms": se,
            "grad_l2_over_mc_se": l2 / se, "p_l2_abs": l2_p, "north_star_gate": 1e-4}
+    try:
+        from bench import lib_sha16  # the library the figures were measured on
+        rep["lib_sha16"] = lib_sha16()
+    except ImportError:
+        pass
     print(json.dumps(rep))
     if os.path.isdir("gpurun_out"):
         with open(os.path.join("gpurun_out", "tolerance_B.json"), "w") as f:

@@ -14,30 +14,55 @@ import sys
 
 PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "neural-monte-carlo-fluid-simulation_amd", "csrc")
-FN = re.compile(r"^(?:template\s*<[^>]*>\s*)?(?:__device__|__global__|WOS_HD|static __device__)[^;{]*?\b(\w+)\s*\(")
+FN = re.compile(r"^(?:template\s*<[^>]*>\s*)?(?:__device__|__global__|WOS_HD|static __device__)")
+NOT_NAMES = {"__launch_bounds__", "__attribute__", "amdgpu_waves_per_eu", "amdgpu_flat_work_group_size"}
+
+
+def fn_name(line):
+    """the declared function's name: the first `name(` that is not an attribute"""
+    for m in re.finditer(r"\b(\w+)\s*\(", line):
+        if m.group(1) not in NOT_NAMES:
+            return m.group(1)
+    return None
 
 
 def spans(path):
-    """[(first line, name)] of the functions (and lambdas named by their variable) in a header."""
+    """[(first line, last line, name)] of the functions and named lambdas of a header: from the
+    declaration to the brace that closes its body (comments and strings are not parsed; the
+    headers keep braces out of them)."""
+    text = open(path).read().split("\n")
     out = []
-    for i, line in enumerate(open(path), 1):
-        m = FN.match(line)
-        if m:
-            out.append((i, m.group(1)))
+    for i, line in enumerate(text):
+        lam = re.match(r"\s+auto (\w+) = \[", line)
+        name = lam.group(1) if lam else (fn_name(line) if FN.match(line) else None)
+        if not name:
             continue
-        m = re.match(r"\s+auto (\w+) = \[", line)
-        if m:
-            out.append((i, m.group(1)))
+        depth, opened, j = 0, False, i
+        while j < len(text):
+            code = text[j].split("//")[0]
+            if not opened and ";" in code and "{" not in code and j > i + 6:
+                break  # a declaration without a body
+            for ch in code:
+                if ch == "{":
+                    depth += 1
+                    opened = True
+                elif ch == "}":
+                    depth -= 1
+            if opened and depth <= 0:
+                break
+            j += 1
+        if opened:
+            out.append((i + 1, j + 1, name))
     return out
 
 
 def owner(tab, line):
-    name = "?"
-    for first, nm in tab:
-        if first > line:
-            break
-        name = nm
-    return name
+    """the innermost function / lambda whose span holds the line"""
+    best, width = "?", None
+    for first, last, nm in tab:
+        if first <= line <= last and (width is None or last - first < width):
+            best, width = nm, last - first
+    return best
 
 
 def salu_kind(op, line):

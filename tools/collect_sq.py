@@ -13,7 +13,9 @@ memory / LDS waits (s_waitcnt) versus stalled at issue.
 
 set "issue" (default) is the pass above; "mix" and "mix2" are the instruction-mix passes
 (VALU by type: F64 add/mul/fma/transcendental, F32, INT32/64, conversions; SALU and
-scalar-pipe active cycles, branches, scalar loads), written to <tag>_<set>_walk_sq.json.
+scalar-pipe active cycles, branches, scalar loads); "icache" the instruction cache (requests,
+hits, misses) with LDS bank conflicts and LDS issue waits; "dcache" the scalar data cache and
+the LDS load / store / atomic split.  Written to <tag>_<set>_walk_sq.json.
 """
 import csv
 import glob
@@ -36,6 +38,10 @@ SETS = {
             "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"],
     "mix2": ["SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_ACTIVE_INST_VALU",
              "SQ_ACTIVE_INST_SCA", "SQ_INST_CYCLES_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_SMEM"],
+    "icache": ["SQC_ICACHE_REQ", "SQC_ICACHE_HITS", "SQC_ICACHE_MISSES", "SQC_ICACHE_MISSES_DUPLICATE", "SQ_IFETCH",
+               "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "SQ_LDS_IDX_ACTIVE"],
+    "dcache": ["SQC_DCACHE_REQ", "SQC_DCACHE_HITS", "SQC_DCACHE_MISSES", "SQC_DCACHE_MISSES_DUPLICATE",
+               "SQ_INSTS_LDS_LOAD", "SQ_INSTS_LDS_STORE", "SQ_INSTS_LDS_ATOMIC", "SQ_INSTS_SMEM"],
 }
 COUNTERS = SETS[SET]
 PFX = TAG if SET == "issue" else f"{TAG}_{SET}"
@@ -49,7 +55,7 @@ def main():
            sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline",
            "--no-projection-wall", "--no-strong"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
-                   stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=300)
+                   stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=150)
     per, dur, kname = {}, {}, {}
     for f in glob.glob(os.path.join(OUT, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):

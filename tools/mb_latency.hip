@@ -44,6 +44,14 @@ __global__ void k_gmem_chain(unsigned long long* out, const int* __restrict__ g,
   uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = idx; }
 }
+// dependent scalar loads (s_load_dword through the scalar cache; the table stays in it)
+__global__ void k_smem_chain(unsigned long long* out, const int* __restrict__ g, int n, int seed) {
+  int idx = __builtin_amdgcn_readfirstlane(seed & 1023);
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < n; i++) idx = __builtin_amdgcn_readfirstlane(g[idx] & 1023);
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = idx; }
+}
 __global__ void k_bperm_chain(unsigned long long* out, int n, int seed) {
   int v = threadIdx.x + seed;
   uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -92,6 +100,7 @@ int main1() {
     hipLaunchKernelGGL(k_dvalu_chain, 1, 64, 0, 0, d, N * 10, 1.0); rep("valu f64 fma chain", N * 10);
     hipLaunchKernelGGL(k_gmem_chain, 1, 64, 0, 0, d, g, 200, 5); rep("global dep chain 4MB", 200);
     hipLaunchKernelGGL(k_bperm_chain, 1, 64, 0, 0, d, N, 1); rep("shfl dep chain", N);
+    hipLaunchKernelGGL(k_smem_chain, 1, 64, 0, 0, d, g, N, 7); rep("scalar-load dep chain", N);
     hipLaunchKernelGGL(k_ldsatomic, 1, 64, 0, 0, d, N, 1); rep("lds atomicMin64 same", N);
   }
   return 0;

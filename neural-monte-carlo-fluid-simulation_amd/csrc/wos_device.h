@@ -392,6 +392,49 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
+// Wave minima through DPP lane moves (VALU, a few cycles each) instead of six ds_bpermute
+// round trips (~80 cycles each, tools/mb_latency.hip): within each row of 16 lanes by
+// quad swaps and row mirrors, then across rows with row_bcast:15 / row_bcast:31, the
+// result in lane 63.  A source lane outside the row mask keeps the destination's own
+// value, which leaves a minimum unchanged.  Needs every lane active (the solo query
+// forms are convergent); otherwise the ds_bpermute butterfly above.
+#ifndef WOS_DPP_MIN
+#define WOS_DPP_MIN 1
+#endif
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ void dpp_min_step(uint32_t& hi, uint32_t& lo) {
+  const uint32_t nh = dpp_u32<CTRL, ROWS>(hi), nl = dpp_u32<CTRL, ROWS>(lo);
+  const bool take = (((unsigned long long)nh << 32) | nl) < (((unsigned long long)hi << 32) | lo);
+  hi = take ? nh : hi;
+  lo = take ? nl : lo;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64_solo(unsigned long long v) {
+  if (!WOS_DPP_MIN || __builtin_amdgcn_read_exec() != ~0ull) return wave_min_u64(v);
+  uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  dpp_min_step<0xB1>(hi, lo);        // quad_perm [1, 0, 3, 2]
+  dpp_min_step<0x4E>(hi, lo);        // quad_perm [2, 3, 0, 1]
+  dpp_min_step<0x141>(hi, lo);       // row_half_mirror
+  dpp_min_step<0x140>(hi, lo);       // row_mirror: every lane holds its row's minimum
+  dpp_min_step<0x142, 0xA>(hi, lo);  // row_bcast:15 into rows 1 and 3
+  dpp_min_step<0x143, 0xC>(hi, lo);  // row_bcast:31 into rows 2 and 3
+  return ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+}
+__device__ __forceinline__ uint32_t wave_min_u32_solo(uint32_t v) {
+  if (!WOS_DPP_MIN || __builtin_amdgcn_read_exec() != ~0ull) return wave_min_u32(v);
+  v = min(v, dpp_u32<0xB1>(v));
+  v = min(v, dpp_u32<0x4E>(v));
+  v = min(v, dpp_u32<0x141>(v));
+  v = min(v, dpp_u32<0x140>(v));
+  v = min(v, dpp_u32<0x142, 0xA>(v));
+  v = min(v, dpp_u32<0x143, 0xC>(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // a lane's float value, wave-uniform
 __device__ __forceinline__ float lane_bcast(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -492,6 +535,57 @@ __device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
     if (d2 <= sr2) { sr2 = d2; best = d; }
   }
   return best;
+}
+
+// computeDistToDirichlet for ONE querying lane of the wave (a lone walk), wave-cooperative:
+// the group with the smallest box bound is evaluated first (kGroup lanes) for a running
+// bound, then the primitives of every group whose bound does not exceed it, kGroup lanes
+// per group; (fl(d*d), larger index on ties) minima by wave reductions, and the winner's
+// distance from the same cp_prim -- dirichlet_dist_culled's value (a primitive with
+// d^2 <= the bound lies in a group whose bound is <= d^2: never skipped).  Convergent.
+#ifndef WOS_DIR_SOLO
+#define WOS_DIR_SOLO 1
+#endif
+template <int DIM>
+__device__ __forceinline__ float dirichlet_dist_solo(const DevScene& sc, const float* dprim, const float* dgroup,
+                                                     const float* xo, int lane) {
+  constexpr int PS = Layout<DIM>::prim;
+  const int ng = sc.n_dgroups, np = sc.n_dprims;
+  unsigned long long gk = ~0ull;
+  for (int g = lane; g < ng; g += kWave) {
+    const unsigned long long k =
+        ((unsigned long long)__float_as_uint(box_dist2<DIM>(dgroup + g * kGroupStride, xo)) << 32) | (uint32_t)g;
+    gk = k < gk ? k : gk;
+  }
+  const int g0 = (int)(uint32_t)wave_min_u64_solo(gk);
+  unsigned long long best = ~0ull;
+  auto eval = [&](int p) {
+    float pt[DIM], t0, t1;
+    const float d = cp_prim<DIM>(dprim + p * PS, xo, pt, &t0, &t1);
+    const unsigned long long k = ((unsigned long long)__float_as_uint(d * d) << 32) | (0xFFFFFFFFu - (uint32_t)p);
+    best = k < best ? k : best;
+  };
+  if (lane < kGroup && g0 * kGroup + lane < np) eval(g0 * kGroup + lane);
+  best = wave_min_u64_solo(best);
+  const float sr2 = __uint_as_float((uint32_t)(best >> 32));
+  for (int w0 = 0; w0 < ng; w0 += kWave) {
+    const int g = w0 + lane;
+    uint64_t pm = __ballot(g < ng && g != g0 && !(box_dist2<DIM>(dgroup + g * kGroupStride, xo) > sr2));
+    while (pm != 0) {
+      // lanes [kGroup q, kGroup (q + 1)) take the q-th group of the mask
+      uint64_t mm = pm;
+      for (int q = lane / kGroup; q > 0 && mm != 0; q--) mm &= mm - 1;
+      for (int q = 0; q < kWave / kGroup && pm != 0; q++) pm &= pm - 1;
+      if (mm != 0) {
+        const int p = (w0 + __builtin_ctzll(mm)) * kGroup + (lane & (kGroup - 1));
+        if (p < np) eval(p);
+      }
+    }
+  }
+  best = wave_min_u64_solo(best);
+  const int pw = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+  float pt[DIM], t0, t1;
+  return cp_prim<DIM>(dprim + pw * PS, xo, pt, &t0, &t1);
 }
 
 struct Hit { float p[3], n[3], d; };
@@ -2173,8 +2267,26 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
   st.walkLength++;
   if (st.walkLength > prm.max_walk_length) return WC_MAXLEN;
   if (sc.absorption > 0.0f && prm.steps_before_tikhonov == st.walkLength) g.init(true, sc.absorption);
-  dirichletDist = dirichlet_dist_culled<DIM>(sc, G.dprim, G.dgroup, st.pt);
+  // the next Dirichlet distance: walk_iteration (dirichlet_dist_step), a lone walk's wave-cooperatively
+  (void)dirichletDist;
   return -1;
+}
+
+// the Dirichlet distance at the new position of every continuing walk (walk_on_stars.h:324):
+// per lane, or wave-cooperatively when only one walk of the wave continues.  Convergent.
+template <int DIM>
+__device__ __forceinline__ void dirichlet_dist_step(const DevScene& sc, const LGeom& G, bool want, const float* x,
+                                                    float& dirichletDist, int lane) {
+  const uint64_t m = __ballot(want && sc.n_dprims > 0);
+  if (WOS_DIR_SOLO && m != 0 && (m & (m - 1)) == 0) {
+    const int ol = __builtin_ctzll(m);
+    float xo[DIM];
+    for (int k = 0; k < DIM; k++) xo[k] = lane_bcast(x[k], ol);
+    const float d = dirichlet_dist_solo<DIM>(sc, G.dprim, G.dgroup, xo, lane);
+    if (want) dirichletDist = d;
+    return;
+  }
+  if (want) dirichletDist = dirichlet_dist_culled<DIM>(sc, G.dprim, G.dgroup, x);
 }
 
 // ---------------------------------------------------------------------------
@@ -2278,7 +2390,7 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
         }
       }
     }
-    best = wave_min_u64(best);
+    best = wave_min_u64_solo(best);
     bool found = false;
     if (need && best != ~0ull) {
       const int p = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
@@ -2531,8 +2643,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
         }
       }
     }
-    best = wave_min_u64(best);
-    brk = wave_min_u32(brk);
+    best = wave_min_u64_solo(best);
+    brk = wave_min_u32_solo(brk);
     if (need) {
       int sw = -1;
       if (brk != 0xFFFFFFFFu) sw = (int)brk;
@@ -3422,6 +3534,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   DIAG_ADD_LONE(D_SAMPLE, D_L_SAMPLE, t_smp, lone);
   DIAG_T0(t_tail);
   if (live) code = walk_step_tail<DIM>(sc, G, prm, ddist, ws, g, st, dir, hit, ip, sp);
+  dirichlet_dist_step<DIM>(sc, G, live && code < 0, st.pt, ddist, lane);
   if (BSTART) firstR = 0.0f;  // firstStep = false (walk_on_stars.h:325)
   DIAG_ADD_LONE(D_TAIL, D_L_TAIL, t_tail, lone);
   DIAG_ADD_LONE(D_STEP, D_L_STEP, t_step, lone);

@@ -142,6 +142,7 @@ typedef struct wos_solver_params {
 #define WOS_SCHED_GEOM_GLOBAL   0x1u  /* read the geometry records through L2 even when they fit LDS */
 #define WOS_SCHED_FULL_NEUMANN  0x2u  /* keep the walk kernel's Neumann term even when it is provably +0 */
 #define WOS_SCHED_NO_STAR_GRID  0x4u  /* no star-radius cell grid: the cooperative group scan alone */
+#define WOS_SCHED_NO_DIR_GRID   0x8u  /* no Dirichlet-distance cell grid (2D): the culled scans alone */
 
 void wos_default_params(wos_solver_params *p);
 
@@ -165,7 +166,7 @@ typedef struct wos_stats {
     int32_t walk_lds_bytes;     /* dynamic LDS per walk-kernel workgroup */
     int32_t star_grid;          /* 1: the star-radius cell grid was used */
     int32_t geom_global;        /* 1: geometry read from global memory (too large for LDS) */
-    int32_t reserved;
+    int32_t dir_grid;                       /* the walk kernel used the Dirichlet-distance cell grid (2D) */
     uint64_t ticket;            /* id of this solve on its device (for wos_solve_stats) */
 } wos_stats;
 

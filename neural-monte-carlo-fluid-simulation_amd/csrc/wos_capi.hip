@@ -65,7 +65,7 @@ struct StatSlot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   std::vector<hipEvent_t> bev;          // per-chunk kernel boundary events (4 per chunk), grow-only
   int64_t n_batches = 0;
-  int32_t bpc_fb = 0, bpc_walk = 0, walk_lds = 0, star_grid = 0, geom_global = 0;
+  int32_t bpc_fb = 0, bpc_walk = 0, walk_lds = 0, star_grid = 0, geom_global = 0, dir_grid = 0;
 };
 constexpr int kStatSlots = 16;
 
@@ -185,6 +185,10 @@ struct Geom {
     uint32_t* d = nullptr;
   };
   std::list<Grid> grids;  // stable addresses (a solve keeps a pointer)
+  // the Dirichlet-distance cell grid (geometry only: built once, on first use)
+  bool dgrid_built = false, dgrid_ok = false;
+  wos::DirGrid dgrid;
+  uint32_t* d_dgrid = nullptr;
   ~Geom() {
     hipSetDevice(device);
     hipFree(d_prim); hipFree(d_paux); hipFree(d_sil); hipFree(d_dprim); hipFree(d_dpaux);
@@ -192,6 +196,7 @@ struct Geom {
     hipFree(d_ptree); hipFree(d_stree); hipFree(d_dtree);
     hipFree(d_nbox); hipFree(d_nchild); hipFree(d_nref);
     for (Grid& g : grids) hipFree(g.d);
+    hipFree(d_dgrid);
   }
 };
 
@@ -282,6 +287,21 @@ int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
   }
   g.grids.push_back(std::move(x));
   *out = &g.grids.back();
+  return WOS_OK;
+}
+
+int dir_grid(Geom& g, bool* ok) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (!g.dgrid_built) {
+    g.dgrid_built = true;
+    g.dgrid_ok = wos::build_dirichlet_grid(g.host, g.dgrid);
+    if (g.dgrid_ok) {
+      HIP_TRY(hipMalloc((void**)&g.d_dgrid, g.dgrid.words.size() * sizeof(uint32_t)));
+      HIP_TRY(hipMemcpy(g.d_dgrid, g.dgrid.words.data(), g.dgrid.words.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+    }
+  }
+  *ok = g.dgrid_ok;
   return WOS_OK;
 }
 
@@ -652,6 +672,7 @@ int fill_stats(const StatSlot& q, wos_stats* stats) {
   stats->walk_lds_bytes = q.walk_lds;
   stats->star_grid = q.star_grid;
   stats->geom_global = q.geom_global;
+  stats->dir_grid = q.dir_grid;
   stats->ticket = q.ticket;
   return WOS_OK;
 }
@@ -691,6 +712,22 @@ int walk_layout(wos_scene* s, const wos_solver_params* prm, WalkLayout& L) {
         dsc.sgrid_n[k] = gr->grid.n[k];
         dsc.sgrid_min[k] = gr->grid.gmin[k];
         dsc.sgrid_inv[k] = gr->grid.inv[k];
+      }
+    }
+  }
+  // the Dirichlet-distance cell grid (global memory)
+  dsc.dgrid = nullptr;
+  if (!(prm->schedule & WOS_SCHED_NO_DIR_GRID) && host.dim == 2 && host.n_dprims > 0) {
+    bool ok = false;
+    int rc = dir_grid(geom, &ok);
+    if (rc != WOS_OK) return rc;
+    if (ok) {
+      dsc.dgrid = geom.d_dgrid;
+      dsc.dgrid_off_words = geom.dgrid.off_words;
+      for (int k = 0; k < 2; k++) {
+        dsc.dgrid_n[k] = geom.dgrid.n[k];
+        dsc.dgrid_min[k] = geom.dgrid.gmin[k];
+        dsc.dgrid_inv[k] = geom.dgrid.inv[k];
       }
     }
   }
@@ -901,6 +938,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   q.walk_lds = (int32_t)shmem_walk;
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
+  q.dir_grid = dsc.dgrid != nullptr;
   HIP_TRY(hipEventRecord(q.ev0, st));
   if (n_chunks == 0) HIP_TRY(wos::launch_zero(c.d_counters, wos::kNumCounterSlots, nullptr, 0, st));
   for (int64_t k = 0; k < n_chunks; k++) {
@@ -1271,6 +1309,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   q.walk_lds = (int32_t)wl.shmem_walk;
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
+  q.dir_grid = dsc.dgrid != nullptr;
 
   // ---- the cache: boundary samples (solution; the Neumann value 0: pde.neumann, scene.h:176-181;
   // Dirichlet samples their normal derivative), then the domain samples inside the solve
@@ -1327,6 +1366,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(hipEventRecord(q.done, st));
   HIP_TRY(hipStreamSynchronize(st));
   c.inflight = false;
+  wos::diag_dump("bvc");  // DIAG builds only
   // the pointwise estimates near the Dirichlet boundary replace the (unsplatted) points'
   // statistics: solution = the estimate, gradient 0 (evalPt.reset, splatter.h:186-192),
   // then saveEvaluationGrid's mask (grid.h:404-408)

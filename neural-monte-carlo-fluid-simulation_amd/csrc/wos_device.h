@@ -537,6 +537,38 @@ __device__ float dirichlet_dist_lane(const DevScene& sc, const float* x) {
   return best;
 }
 
+// computeDistToDirichlet through the Dirichlet cell grid (2D, DevScene::dgrid): the
+// segments of x's cell list in index order with the full scan's `<=` rule -- the full
+// scan's distance (wos_host_scene.h DirGrid).  Returns a negative value when x lies
+// outside the grid (the caller scans).
+template <int DIM>
+__device__ __forceinline__ float dirichlet_dist_grid(const DevScene& sc, const float* dprim, const float* x) {
+  if constexpr (DIM != 2) {
+    return -1.0f;
+  } else {
+    int c = 0;
+    for (int k = 1; k >= 0; k--) {
+      const int nk = sc.dgrid_n[k];
+      const float v = (x[k] - sc.dgrid_min[k]) * sc.dgrid_inv[k];
+      if (!(v >= 0.0f && v < (float)nk)) return -1.0f;
+      int i = (int)v;
+      if (i > nk - 1) i = nk - 1;
+      c = c * nk + i;
+    }
+    const uint32_t b = sc.dgrid[c], e = sc.dgrid[c + 1];
+    const uint16_t* lst = reinterpret_cast<const uint16_t*>(sc.dgrid + sc.dgrid_off_words);
+    float sr2 = kFltMax, best = kFltMax;
+    for (uint32_t i = b; i < e; i++) {
+      const int p = (int)lst[i];
+      float pt[2], t0, t1;
+      const float d = cp_prim<2>(dprim + p * kPrimStride2, x, pt, &t0, &t1);
+      const float d2 = d * d;
+      if (d2 <= sr2) { sr2 = d2; best = d; }
+    }
+    return best;
+  }
+}
+
 // computeDistToDirichlet for ONE querying lane of the wave (a lone walk), wave-cooperative:
 // the group with the smallest box bound is evaluated first (kGroup lanes) for a running
 // bound, then the primitives of every group whose bound does not exceed it, kGroup lanes
@@ -2277,6 +2309,14 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
 template <int DIM>
 __device__ __forceinline__ void dirichlet_dist_step(const DevScene& sc, const LGeom& G, bool want, const float* x,
                                                     float& dirichletDist, int lane) {
+  if (DIM == 2 && sc.dgrid != nullptr) {
+    // the cell grid: a short list per lane (outside the grid: the culled scan)
+    if (want) {
+      const float d = dirichlet_dist_grid<DIM>(sc, G.dprim, x);
+      dirichletDist = d >= 0.0f ? d : dirichlet_dist_culled<DIM>(sc, G.dprim, G.dgroup, x);
+    }
+    return;
+  }
   const uint64_t m = __ballot(want && sc.n_dprims > 0);
   if (WOS_DIR_SOLO && m != 0 && (m & (m - 1)) == 0) {
     const int ol = __builtin_ctzll(m);

@@ -392,6 +392,36 @@ double box_point_dist(const double* lo, const double* hi, const double* p, int d
 
 }  // namespace
 
+// Distance between an axis-aligned box [lo, hi] and the segment a-b (2D, double): 0 when
+// they meet, else the smallest of the endpoints' box distances and the corners' segment
+// distances (two disjoint convex polygons are closest at a vertex of one of them).
+double box_seg_dist2d(const double* lo, const double* hi, const double* a, const double* b) {
+  // Liang-Barsky clip of a + t (b - a), t in [0, 1], against the box
+  double t0 = 0.0, t1 = 1.0;
+  bool meets = true;
+  for (int k = 0; k < 2 && meets; k++) {
+    const double d = b[k] - a[k];
+    if (d == 0.0) {
+      if (a[k] < lo[k] || a[k] > hi[k]) meets = false;
+    } else {
+      double u = (lo[k] - a[k]) / d, v = (hi[k] - a[k]) / d;
+      if (u > v) std::swap(u, v);
+      t0 = std::max(t0, u);
+      t1 = std::min(t1, v);
+      if (t0 > t1) meets = false;
+    }
+  }
+  if (meets) return 0.0;
+  SilGeo g;
+  for (int k = 0; k < 2; k++) { g.a[k] = a[k]; g.b[k] = b[k]; }
+  double m = std::min(box_point_dist(lo, hi, a, 2), box_point_dist(lo, hi, b, 2));
+  for (int q = 0; q < 4; q++) {
+    const double c[3] = {(q & 1) ? hi[0] : lo[0], (q & 2) ? hi[1] : lo[1], 0.0};
+    m = std::min(m, seg_point_dist(g, c, 2));
+  }
+  return m;
+}
+
 // For a cell box C (enlarged beyond the kernel's cell-index rounding) and a
 // candidate s with adjacent normals n0, n1:
 //   * f_i(x) = (x - a).n_i is linear in x, so its range over C is spanned by the
@@ -665,6 +695,81 @@ bool load_obj(const std::string& path, int dim, bool flip, bool normalize_domain
     }
     for (int i = 0; i < nv; i++) for (int k = 0; k < dim; k++) verts[i * dim + k] /= radius;
   }
+  return true;
+}
+
+
+bool build_dirichlet_grid(const HostScene& hs, DirGrid& out) {
+  out = DirGrid();
+  const int nd = hs.n_dprims;
+  if (hs.dim != 2 || nd <= 0 || nd > 65535) return false;
+  // segments a, b = a + v as the kernels' records hold them
+  std::vector<double> sa(2 * (size_t)nd), sb(2 * (size_t)nd);
+  for (int p = 0; p < nd; p++) {
+    const float* P = &hs.dprim[(size_t)p * kPrimStride2];
+    for (int k = 0; k < 2; k++) {
+      sa[2 * p + k] = P[k];
+      sb[2 * p + k] = (double)P[k] + (double)P[2 + k];
+    }
+  }
+  double span = std::max((double)hs.ext[0], (double)hs.ext[1]);
+  if (!(span > 0.0)) return false;
+  const double gpad = 1e-3 * span + 1e-6;
+  double glo[2], gext[2];
+  for (int k = 0; k < 2; k++) {
+    glo[k] = (double)hs.pmin[k] - gpad;
+    gext[k] = ((double)hs.pmax[k] + gpad) - glo[k];
+  }
+  const double vol = gext[0] * gext[1];
+  const double slack = 1e-5 * span;
+  // the finest grid up to 128 x 128 cells whose lists stay short (the cost scales with ncell x nd)
+  const int target = nd <= 512 ? 16384 : (nd <= 4096 ? 4096 : 1024);
+  const double h = std::sqrt(vol / target);
+  for (int k = 0; k < 2; k++) {
+    out.n[k] = std::max(1, (int)std::ceil(gext[k] / h));
+    out.gmin[k] = (float)glo[k];
+    out.inv[k] = (float)((double)out.n[k] / gext[k]);
+  }
+  out.ncell = out.n[0] * out.n[1];
+  std::vector<uint32_t> off((size_t)out.ncell + 1, 0u);
+  std::vector<uint16_t> lst;
+  std::vector<double> mind(nd);
+  for (int c = 0; c < out.ncell; c++) {
+    const int ic[2] = {c % out.n[0], c / out.n[0]};
+    double lo[2], hi[2];
+    for (int k = 0; k < 2; k++) {
+      const double w = 1.0 / (double)out.inv[k];
+      const double delta = 1e-3 * w + 1e-5 * span;
+      lo[k] = (double)out.gmin[k] + ic[k] * w - delta;
+      hi[k] = (double)out.gmin[k] + (ic[k] + 1) * w + delta;
+    }
+    double U = HUGE_VAL;
+    for (int p = 0; p < nd; p++) {
+      const double* a = &sa[2 * p];
+      const double* b = &sb[2 * p];
+      SilGeo g;
+      for (int k = 0; k < 2; k++) { g.a[k] = a[k]; g.b[k] = b[k]; }
+      double dmax = 0.0;
+      for (int q = 0; q < 4; q++) {
+        const double cq[3] = {(q & 1) ? hi[0] : lo[0], (q & 2) ? hi[1] : lo[1], 0.0};
+        dmax = std::max(dmax, seg_point_dist(g, cq, 2));
+      }
+      U = std::min(U, dmax);
+      mind[p] = box_seg_dist2d(lo, hi, a, b);
+    }
+    const double thr = U * (1.0 + 1e-4) + slack;
+    for (int p = 0; p < nd; p++)
+      if (!(mind[p] > thr)) lst.push_back((uint16_t)p);
+    off[(size_t)c + 1] = (uint32_t)lst.size();
+    out.max_list = std::max(out.max_list, (int)(off[(size_t)c + 1] - off[c]));
+  }
+  out.list_len = lst.size();
+  // worth it only while the lists are short against the culled scan
+  if (out.max_list > 256 || out.list_len > (size_t)out.ncell * 16) return false;
+  out.off_words = out.ncell + 1;
+  out.words.assign((size_t)out.off_words + (lst.size() + 1) / 2, 0u);
+  std::memcpy(out.words.data(), off.data(), off.size() * sizeof(uint32_t));
+  if (!lst.empty()) std::memcpy(out.words.data() + out.off_words, lst.data(), lst.size() * sizeof(uint16_t));
   return true;
 }
 

@@ -81,6 +81,27 @@ struct StarGrid {
 // does not fit budget_bytes at a useful resolution (the kernel then scans groups)
 bool build_star_grid(const HostScene& hs, float prec, float min_r, size_t budget_bytes, StarGrid& out);
 
+// Dirichlet-distance cell grid (2D): a uniform grid over the padded bounding box; cell c
+// holds the ascending list of the Dirichlet segments that can be the closest one
+// (computeDistToDirichlet, fcpw_scene_loader.h:299-315) to a point of the (slightly
+// enlarged) cell: segment s is left out only when its distance from every point of the
+// cell is certainly above the distance from that point to another segment -- its
+// box distance exceeds, with margin, the smallest corner-maximum distance U of the
+// cell's segments.  A scan of the list in index order with the full scan's `<=` rule
+// returns the full scan's distance bit for bit (the float argmin is within ~1e-6 of the
+// true minimum, far inside the margin).
+struct DirGrid {
+  int n[2] = {1, 1};
+  float gmin[2] = {0.0f, 0.0f}, inv[2] = {0.0f, 0.0f};
+  int ncell = 0;
+  int off_words = 0;             // u32 offsets (ncell + 1 entries)
+  std::vector<uint32_t> words;   // [u32 offsets | u16 segment indices, packed]
+  size_t list_len = 0;
+  int max_list = 0;
+};
+// false for 3D scenes, no / too many Dirichlet segments, or lists too long to pay off
+bool build_dirichlet_grid(const HostScene& hs, DirGrid& out);
+
 // Upper bounds for the Yukawa rejection test (wos_kernel.hip rej_quick_bound): the
 // accept threshold of rejectionSampleGreensFn at radius r = x R is
 // T = R * x * Q_s(x) / (norm * bound) with s = mu R and

@@ -94,6 +94,12 @@ struct DevScene {
   int32_t sgrid_words, sgrid_off_words;
   int32_t sgrid_n[3];
   float sgrid_min[3], sgrid_inv[3];
+  // Dirichlet-distance cell grid (2D; wos_host_scene.h DirGrid; nullptr: none), global
+  // memory: u32 cell offsets then u16 segment indices
+  const uint32_t* dgrid;
+  int32_t dgrid_off_words;
+  int32_t dgrid_n[2];
+  float dgrid_min[2], dgrid_inv[2];
 };
 
 struct DevParams {

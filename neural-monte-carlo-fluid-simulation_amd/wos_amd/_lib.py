@@ -67,6 +67,7 @@ class SolverParams(C.Structure):
 SCHED_GEOM_GLOBAL = 0x1
 SCHED_FULL_NEUMANN = 0x2
 SCHED_NO_STAR_GRID = 0x4
+SCHED_NO_DIR_GRID = 0x8
 
 
 class BvcParams(C.Structure):
@@ -83,7 +84,7 @@ class Stats(C.Structure):
         "walks_rr", "walks_dirichlet", "points_estimated", "rejection_iters")] + [
         (n, C.c_double) for n in ("kernel_ms", "first_ball_ms", "walk_ms", "fold_ms")] + [("walk_launches", C.c_uint64)] + [
         (n, C.c_int32) for n in ("first_ball_blocks_per_cu", "walk_blocks_per_cu", "walk_lds_bytes", "star_grid",
-                                 "geom_global", "reserved")] + [("ticket", C.c_uint64)]
+                                 "geom_global", "dir_grid")] + [("ticket", C.c_uint64)]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_double else int(getattr(self, n))) for n, t in self._fields_}

@@ -162,6 +162,64 @@ extern "C" int hs_star_grid_check(int dim, const float* v, int nv, const int* ix
   return mismatches;
 }
 
+// ---- Dirichlet-distance grid soundness: for every point inside the grid, every segment
+// whose true (double) distance is within a relative 1e-6 (+ 1e-7 of the span) of the
+// nearest one -- every segment the float scan could pick -- is on the point's cell list
+// (cell index exactly as the kernel computes it, dirichlet_dist_grid).
+extern "C" int hs_dir_grid_check(const float* v, int nv, const int* ix, int np, const float* dv, int ndv,
+                                 const int* dix, int nd, const float* pts, int npts, int* info) {
+  wos::HostSceneInput in;
+  in.dim = 2;
+  in.vertices = v; in.n_vertices = nv;
+  in.prims = ix; in.n_prims = np;
+  in.dvertices = dv; in.n_dvertices = ndv;
+  in.dprims = dix; in.n_dprims = nd;
+  wos::HostScene hs;
+  std::string err;
+  if (!wos::prepare_scene(in, hs, err)) return -1;
+  wos::DirGrid g;
+  const bool ok = wos::build_dirichlet_grid(hs, g);
+  for (int k = 0; k < 8; k++) info[k] = 0;
+  info[0] = ok;
+  info[1] = g.ncell; info[2] = (int)g.list_len; info[3] = g.max_list; info[4] = g.n[0]; info[5] = g.n[1];
+  if (!ok) return 0;
+  const uint32_t* off = g.words.data();
+  const uint16_t* lst = reinterpret_cast<const uint16_t*>(g.words.data() + g.off_words);
+  const double span = std::max(hs.ext[0], hs.ext[1]);
+  int bad = 0;
+  for (int i = 0; i < npts; i++) {
+    const float* x = pts + (size_t)i * 2;
+    int c = 0;
+    bool inside = true;
+    for (int k = 1; k >= 0; k--) {
+      const float vv = (x[k] - g.gmin[k]) * g.inv[k];
+      if (!(vv >= 0.0f && vv < (float)g.n[k])) { inside = false; break; }
+      int ii = (int)vv;
+      if (ii > g.n[k] - 1) ii = g.n[k] - 1;
+      c = c * g.n[k] + ii;
+    }
+    if (!inside) continue;
+    info[6]++;
+    std::vector<double> d(hs.n_dprims);
+    double m = HUGE_VAL;
+    for (int p = 0; p < hs.n_dprims; p++) {
+      const float* P = &hs.dprim[(size_t)p * wos::kPrimStride2];
+      const double a[2] = {P[0], P[1]}, u[2] = {P[2], P[3]};
+      const double uu = u[0] * u[0] + u[1] * u[1];
+      const double t = uu > 0.0 ? std::min(1.0, std::max(0.0, (u[0] * (x[0] - a[0]) + u[1] * (x[1] - a[1])) / uu)) : 0.0;
+      const double w0 = x[0] - (a[0] + t * u[0]), w1 = x[1] - (a[1] + t * u[1]);
+      d[p] = std::sqrt(w0 * w0 + w1 * w1);
+      m = std::min(m, d[p]);
+    }
+    const double thr = m * (1.0 + 1e-6) + 1e-7 * span;
+    for (int p = 0; p < hs.n_dprims; p++) {
+      if (d[p] > thr) continue;
+      if (!std::binary_search(lst + off[c], lst + off[c + 1], (uint16_t)p)) bad++;
+    }
+  }
+  return bad;
+}
+
 // the rejection bound table of the kernels' certain-reject screen (wos_host_scene.h)
 
 extern "C" int hs_rej_table(int dim, float* out) {

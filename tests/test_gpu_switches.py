@@ -7,8 +7,10 @@ wos_solver_params.schedule (include/wos.h WOS_SCHED_*) selects, per solve:
                          term is provably +0 (the "Neumann-inert" instantiation is the
                          default for such scenes);
 * WOS_SCHED_NO_STAR_GRID the cooperative silhouette-group scan alone, without the
-                         star-radius cell grid.
-One process solves the same points under all 8 combinations of the bits and compares p, grad p,
+                         star-radius cell grid;
+* WOS_SCHED_NO_DIR_GRID  the culled Dirichlet-distance scans alone, without the
+                         Dirichlet cell grid (2D scenes with Dirichlet segments).
+One process solves the same points under all 16 combinations of the bits and compares p, grad p,
 the per-point walk counts and step counts bit for bit with the default (schedule 0), which
 itself is compared with the CPU oracle.
 Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance), the
@@ -18,12 +20,12 @@ import pytest
 
 import objparse
 from wos_amd import WosScene, solver_params, workloads
-from wos_amd._lib import SCHED_FULL_NEUMANN, SCHED_GEOM_GLOBAL, SCHED_NO_STAR_GRID
+from wos_amd._lib import SCHED_FULL_NEUMANN, SCHED_GEOM_GLOBAL, SCHED_NO_DIR_GRID, SCHED_NO_STAR_GRID
 
 pytestmark = pytest.mark.gpu
 
-SETTINGS = list(range(8))  # every combination of the three bits
-assert SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID == 7
+SETTINGS = list(range(16))  # every combination of the four bits
+assert SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID | SCHED_NO_DIR_GRID == 15
 
 
 def _scenes():
@@ -55,6 +57,8 @@ def test_switches_are_bit_identical(gpu, oracle, name, cfg, make, pts, make_orac
         assert st["geom_global"] == (1 if sched & SCHED_GEOM_GLOBAL else 0)
         if sched & SCHED_NO_STAR_GRID:
             assert st["star_grid"] == 0
+        if name == "dirichlet":
+            assert st["dir_grid"] == (0 if sched & SCHED_NO_DIR_GRID else 1)
         out = [np.asarray(p).view(np.uint32), np.asarray(g).view(np.uint32), np.asarray(n_est), np.asarray(steps)]
         if ref is None:
             ref = out

@@ -310,3 +310,40 @@ def test_group_tree_contains_and_traverses(shim, ngroups):
                 assert g0 <= g < limit
                 got.append(g)
         assert got == want, trial
+
+
+@pytest.mark.parametrize("case", ["dirichlet_obstacle", "engine"])
+def test_dirichlet_grid_lists_hold_the_nearest_segments(shim, case):
+    """The Dirichlet-distance cell grid (wos_host_scene.cpp build_dirichlet_grid): at random
+    points and points on and next to the Dirichlet segments, every segment the float scan
+    could pick (true distance within 1e-6 relative of the nearest) is on the point's cell
+    list, so the kernel's list scan returns the full scan's distance."""
+    rng = np.random.default_rng(7)
+    if case == "engine":
+        import engine_pin as ep
+        U = ep.upstream_scene()
+        (nv, nix), (dv, dix) = U["neumann"], U["dirichlet"]
+    else:
+        c = workloads.dirichlet_obstacle_config(n_walks=4, res=8)
+        nv, nix, dv, dix = c["vertices"], c["prims"], c["dvertices"], c["dprims"]
+    nv, dv = np.ascontiguousarray(nv, np.float32), np.ascontiguousarray(dv, np.float32)
+    nix, dix = np.ascontiguousarray(nix, np.int32), np.ascontiguousarray(dix, np.int32)
+    allv = np.concatenate([nv, dv])
+    lo, hi = allv.min(0), allv.max(0)
+    pts = [rng.uniform(lo, hi, (20000, 2))]
+    a, b = dv[dix[:, 0]], dv[dix[:, 1]]
+    t = rng.uniform(0, 1, (len(dix), 8, 1))
+    on = a[:, None, :] + t * (b - a)[:, None, :]
+    pts.append(on.reshape(-1, 2))
+    pts.append((on + rng.normal(0, 1e-3 * float((hi - lo).max()), on.shape)).reshape(-1, 2))
+    pts.append(np.concatenate([a, b]))
+    pts = np.ascontiguousarray(np.concatenate(pts), np.float32)
+    info = np.zeros(8, np.int32)
+    f, i = C.POINTER(C.c_float), C.POINTER(C.c_int)
+    bad = shim.hs_dir_grid_check(nv.ctypes.data_as(f), nv.shape[0], nix.ctypes.data_as(i), nix.shape[0],
+                                 dv.ctypes.data_as(f), dv.shape[0], dix.ctypes.data_as(i), dix.shape[0],
+                                 pts.ctypes.data_as(f), pts.shape[0], info.ctypes.data_as(i))
+    assert info[0] == 1, info  # the grid is built
+    assert info[6] > 0.9 * pts.shape[0], info
+    assert bad == 0, (bad, info)
+    assert info[3] <= 256 and info[2] <= 16 * info[1], info  # short lists

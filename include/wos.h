@@ -218,7 +218,10 @@ void wos_default_bvc_params(wos_bvc_params *p);
  * Boundary samples cover the Neumann and the Dirichlet segments (boundary_sampler.h:87-412);
  * evaluation points within normalOffset of the Dirichlet boundary take a pointwise
  * estimateSolution (splatter.h:160-196).  3D scenes return WOS_E_INVALID (zombie3d exports no
- * bvc). */
+ * bvc).  The three walk sets (Dirichlet samples, Neumann samples, near-boundary points) run
+ * on three streams at once; stats: kernel_ms the whole call, first_ball_ms the point
+ * queries, walk_ms until the cache is complete, fold_ms the splat and the near-boundary
+ * walks still running beside it. */
 int wos_bvc(wos_scene *scene, const wos_solver_params *params, const wos_bvc_params *bvc,
             float *solution, float *grad, float *samples, int64_t samples_capacity, int64_t *counts,
             wos_stats *stats);

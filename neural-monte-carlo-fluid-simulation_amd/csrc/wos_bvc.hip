@@ -225,33 +225,73 @@ struct FreeSpace2 {
 
 __device__ __forceinline__ bool finite_f(float v) { return __builtin_isfinite(v); }
 
-struct SplatStat {
-  float mean, g[2];
-  int n;
-  __device__ __forceinline__ void add(float est, const float* ge) {
-    n += 1;
-    const float fN = (float)n;
-    mean += (est - mean) / fN;
-    for (int k = 0; k < 2; k++) g[k] += (ge[k] - g[k]) / fN;
+// One (evaluation point, cached sample) term of Splatter::splat: the estimate and its
+// gradient, and the statistics class it folds into (0 boundary, 1 normal-aligned,
+// 2 domain; 3: skipped, a non-finite kernel value -- the reference's `continue`).
+__device__ __forceinline__ int splat_term(const FreeSpace2& gf, const float* R, const float* x, float radius_clamp,
+                                          float reg, float* est, float* ge) {
+  const int kind = (int)R[7];
+  const float pdf = R[4], value = R[5];
+  const float yx[2] = {R[0] - x[0], R[1] - x[1]};
+  const float xy[2] = {x[0] - R[0], x[1] - R[1]};
+  float r = smax(radius_clamp, __builtin_sqrtf(yx[0] * yx[0] + yx[1] * yx[1]));
+  float K0 = 0.0f, K1 = 0.0f, K2 = 0.0f;
+  if (gf.yukawa) gf.bessel_k(r * gf.sqrtLambda, &K0, &K1, kind == kBvcDomain ? nullptr : &K2);
+  float G = gf.evaluate(r, K0);
+  float dG[2];
+  gf.gradient(r, xy, K1, dG);
+  const float dGNorm = __builtin_sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
+  const bool al = kind == kBvcAligned || kind == kBvcDirichletAligned;
+  if (kind != kBvcDomain) {  // splatBoundaryData (splatter.h:214-264)
+    const float nd = R[6];
+    const float s = al ? -1.0f : 1.0f;
+    const float n[2] = {R[2] * s, R[3] * s};
+    float P = gf.poisson(r, xy, n, K1);
+    float dP[2];
+    gf.poisson_gradient(r, xy, n, K0, K1, K2, dP);
+    const float dPNorm = __builtin_sqrtf(dP[0] * dP[0] + dP[1] * dP[1]);
+    if (!(finite_f(G) && finite_f(P) && finite_f(dGNorm) && finite_f(dPNorm))) return 3;
+    if (reg > 0.0f) {
+      r /= reg;
+      P *= 1.0f - fexp(-r * r);  // computePoissonKernelRegularization<2> (splatter.h:28-32)
+    }
+    *est = (G * nd - P * value) / pdf;
+    for (int k = 0; k < 2; k++) ge[k] = (dG[k] * nd - dP[k] * value) / pdf;
+    return al ? 1 : 0;
   }
-};
+  // splatSourceData (splatter.h:267-301)
+  if (!(finite_f(G) && finite_f(dGNorm))) return 3;
+  *est = (G * value) / pdf;
+  for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
+  return 2;
+}
 
-constexpr int kSplatTile = 256;
+// The splat runs in two phases per tile of kSplatT cached samples, for kSplatPts
+// evaluation points (one per lane) per workgroup of 4 waves:
+//   terms  every wave evaluates a quarter of the tile's (point, sample) terms into LDS
+//          -- the arithmetic, 4 waves per point set instead of one;
+//   fold   waves 0, 1, 2 each run one component (solution, gradient x, gradient y) of
+//          the point's three Welford statistics (SampleStatistics, splatter.h:315-334)
+//          over the tile's terms in cache order -- the same division chain per
+//          component as one lane running all three, so the result is unchanged; wave 3
+//          stages the next tile's records.
+constexpr int kSplatPts = 64, kSplatT = 32, kSplatWaves = 4;
 
-// Splatter::splat over every evaluation point (one lane each) and every cached sample
-// (boundary, normal-aligned, domain in cache order), then EvaluationPoint::
-// getEstimatedSolution / getEstimatedGradient (splatter.h:315-334) and the output mask
-// of saveEvaluationGrid (grid.h:393-409).
-__global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restrict__ recs, int nrec,
-                                                            const float* __restrict__ ept,
-                                                            const float* __restrict__ edd,
-                                                            const float* __restrict__ end_,
-                                                            const int32_t* __restrict__ ein, int64_t ne,
-                                                            float absorption, float radius_clamp, float reg,
-                                                            float cutoff, float mask, int double_sided,
-                                                            float* __restrict__ sol_out, float* __restrict__ grad_out) {
-  __shared__ float tile[kSplatTile * kBvcRec];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Splatter::splat over every evaluation point and every cached sample (boundary,
+// normal-aligned, domain in cache order), then EvaluationPoint::getEstimatedSolution /
+// getEstimatedGradient (splatter.h:315-334) and the output mask of saveEvaluationGrid
+// (grid.h:393-409).
+__global__ __launch_bounds__(kSplatPts * kSplatWaves) void wos_bvc_splat_kernel(
+    const float* __restrict__ recs, int nrec, const float* __restrict__ ept, const float* __restrict__ edd,
+    const float* __restrict__ end_, const int32_t* __restrict__ ein, int64_t ne, float absorption,
+    float radius_clamp, float reg, float cutoff, float mask, int double_sided, float* __restrict__ sol_out,
+    float* __restrict__ grad_out) {
+  __shared__ float rtile[2][kSplatT * kBvcRec];
+  __shared__ float term[3][kSplatT][kSplatPts];
+  __shared__ uint8_t tcls[kSplatT][kSplatPts];
+  const int lane = threadIdx.x & (kSplatPts - 1);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kSplatPts));
+  const int64_t i = (int64_t)blockIdx.x * kSplatPts + lane;
   const bool valid = i < ne;
   FreeSpace2 gf;
   gf.yukawa = absorption > 0.0f;
@@ -262,68 +302,56 @@ __global__ __launch_bounds__(256) void wos_bvc_splat_kernel(const float* __restr
   // evaluation points closer than the cutoff to the Dirichlet boundary are not splatted
   // (splatter.h:94): they take a pointwise estimate (estimatePointwiseNearDirichletBoundary)
   const bool splat = valid && !(dDist < cutoff);
-  SplatStat st[3];
-  for (int q = 0; q < 3; q++) { st[q].mean = 0.0f; st[q].g[0] = st[q].g[1] = 0.0f; st[q].n = 0; }
-  for (int t0 = 0; t0 < nrec; t0 += kSplatTile) {
-    const int cnt = nrec - t0 < kSplatTile ? nrec - t0 : kSplatTile;
-    for (int e = threadIdx.x; e < cnt * kBvcRec; e += blockDim.x) tile[e] = recs[(size_t)t0 * kBvcRec + e];
-    __syncthreads();
-    if (splat) {
-      for (int j = 0; j < cnt; j++) {
-        const float* R = tile + j * kBvcRec;
-        const int kind = (int)R[7];
-        const float pdf = R[4], value = R[5];
-        const float yx[2] = {R[0] - x[0], R[1] - x[1]};
-        const float xy[2] = {x[0] - R[0], x[1] - R[1]};
-        float r = smax(radius_clamp, __builtin_sqrtf(yx[0] * yx[0] + yx[1] * yx[1]));
-        float K0 = 0.0f, K1 = 0.0f, K2 = 0.0f;
-        if (gf.yukawa) gf.bessel_k(r * gf.sqrtLambda, &K0, &K1, kind == kBvcDomain ? nullptr : &K2);
-        float G = gf.evaluate(r, K0);
-        float dG[2];
-        gf.gradient(r, xy, K1, dG);
-        const float dGNorm = __builtin_sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
-        float est, ge[2];
-        const bool al = kind == kBvcAligned || kind == kBvcDirichletAligned;
-        if (kind != kBvcDomain) {  // splatBoundaryData (splatter.h:214-264)
-          const float nd = R[6];
-          const float s = al ? -1.0f : 1.0f;
-          const float n[2] = {R[2] * s, R[3] * s};
-          float P = gf.poisson(r, xy, n, K1);
-          float dP[2];
-          gf.poisson_gradient(r, xy, n, K0, K1, K2, dP);
-          const float dPNorm = __builtin_sqrtf(dP[0] * dP[0] + dP[1] * dP[1]);
-          if (!(finite_f(G) && finite_f(P) && finite_f(dGNorm) && finite_f(dPNorm))) continue;
-          if (reg > 0.0f) {
-            r /= reg;
-            P *= 1.0f - fexp(-r * r);  // computePoissonKernelRegularization<2> (splatter.h:28-32)
-          }
-          est = (G * nd - P * value) / pdf;
-          for (int k = 0; k < 2; k++) ge[k] = (dG[k] * nd - dP[k] * value) / pdf;
-        } else {  // splatSourceData (splatter.h:267-301)
-          if (!(finite_f(G) && finite_f(dGNorm))) continue;
-          est = (G * value) / pdf;
-          for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
-        }
-        st[kind == kBvcDomain ? 2 : al ? 1 : 0].add(est, ge);
-      }
+  // this wave's component of the three classes' statistics and their counts
+  float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
+  int n0 = 0, n1 = 0, n2 = 0;
+  for (int e = threadIdx.x; e < kSplatT * kBvcRec; e += kSplatPts * kSplatWaves)
+    if (e < nrec * kBvcRec) rtile[0][e] = recs[e];
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = 0; t0 < nrec; t0 += kSplatT) {
+    const int cnt = nrec - t0 < kSplatT ? nrec - t0 : kSplatT;
+    // terms: samples wave, wave + 4, ... of the tile
+    for (int j = wave; j < cnt; j += kSplatWaves) {
+      float est = 0.0f, ge[2] = {0.0f, 0.0f};
+      int c = 3;
+      if (splat) c = splat_term(gf, &rtile[buf][j * kBvcRec], x, radius_clamp, reg, &est, ge);
+      term[0][j][lane] = est;
+      term[1][j][lane] = ge[0];
+      term[2][j][lane] = ge[1];
+      tcls[j][lane] = (uint8_t)c;
     }
     __syncthreads();
+    if (wave < 3) {
+      if (splat) {
+        for (int j = 0; j < cnt; j++) {
+          const int c = tcls[j][lane];
+          if (c == 3) continue;
+          const float v = term[wave][j][lane];
+          int n = c == 0 ? n0 : c == 1 ? n1 : n2;
+          float m = c == 0 ? m0 : c == 1 ? m1 : m2;
+          n += 1;
+          m += (v - m) / (float)n;
+          if (c == 0) { m0 = m; n0 = n; } else if (c == 1) { m1 = m; n1 = n; } else { m2 = m; n2 = n; }
+        }
+      }
+    } else {
+      const int nx = t0 + kSplatT;
+      for (int e = lane; e < kSplatT * kBvcRec; e += kSplatPts)
+        if ((int64_t)nx * kBvcRec + e < (int64_t)nrec * kBvcRec) rtile[buf ^ 1][e] = recs[(size_t)nx * kBvcRec + e];
+    }
+    __syncthreads();
+    buf ^= 1;
   }
-  if (!valid) return;
-  float sol = st[0].mean;
-  sol += st[1].mean;
-  sol += st[2].mean;
-  float g[2];
-  for (int k = 0; k < 2; k++) {
-    g[k] = st[0].g[k];
-    g[k] += st[1].g[k];
-    g[k] += st[2].g[k];
-  }
+  if (!valid || wave >= 3) return;
+  float v = m0;
+  v += m1;
+  v += m2;
   const bool in = ein[i] != 0;
   const float ad = __builtin_fabsf(dDist), an = __builtin_fabsf(end_[i]);
   const bool masked = (!in && !double_sided) || smin(ad, an) < mask;
-  sol_out[i] = masked ? 0.0f : sol;
-  for (int k = 0; k < 2; k++) grad_out[2 * i + k] = masked ? 0.0f : g[k];
+  if (wave == 0) sol_out[i] = masked ? 0.0f : v;
+  else grad_out[2 * i + (wave - 1)] = masked ? 0.0f : v;
 }
 
 template __global__ void wos_walk_kernel<2, false, true>(const DevScene, const DevParams, const DevTasks, int64_t,
@@ -388,8 +416,9 @@ hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const
                             const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
                             float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s) {
   if (ne <= 0) return hipSuccess;
-  hipLaunchKernelGGL(wos_bvc_splat_kernel, dim3((int)((ne + 255) / 256)), dim3(256), 0, s, recs, nrec, ept, edd, end_,
-                     ein, ne, absorption, radius_clamp, reg, cutoff, mask, double_sided, sol, grad);
+  hipLaunchKernelGGL(wos_bvc_splat_kernel, dim3((int)((ne + kSplatPts - 1) / kSplatPts)), dim3(kSplatPts * kSplatWaves),
+                     0, s, recs, nrec, ept, edd, end_, ein, ne, absorption, radius_clamp, reg, cutoff, mask,
+                     double_sided, sol, grad);
   return hipGetLastError();
 }
 

@@ -69,6 +69,21 @@ struct StatSlot {
 };
 constexpr int kStatSlots = 16;
 
+// A walk-task workspace with its own counters and non-blocking stream: boundary value
+// caching runs its independent walk sets (the boundary samples' walks, the walks of the
+// evaluation points near the Dirichlet boundary) beside the Dirichlet samples' solve on
+// the call's stream, so one set's long tail overlaps the others' bulk.
+struct TaskWs {
+  float* tasks = nullptr;
+  int64_t task_cap = 0;
+  int32_t* pstate = nullptr;
+  int64_t pstate_cap = 0;
+  unsigned long long* counters = nullptr;  // kNumCounterSlots
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+};
+constexpr int kSideWs = 2;
+
 struct DevCtx {
   std::mutex mu;  // one solve at a time per device (the workspace is shared)
   bool ready = false;
@@ -94,6 +109,7 @@ struct DevCtx {
   float* d_rejtab = nullptr;   // rejection bound table, 2D then 3D (DevParams::rej_tab)
   int stat_waiters = 0;        // wos_solve_stats calls waiting on a slot's event without the lock
   std::condition_variable no_waiters;
+  TaskWs side[kSideWs];        // boundary value caching's side-stream workspaces (lazy)
 };
 
 constexpr int kMaxDevices = 64;
@@ -112,6 +128,12 @@ void ctx_free(DevCtx& c) {
     q = StatSlot{};
   }
   if (c.done) hipEventDestroy(c.done);
+  for (TaskWs& w : c.side) {
+    hipFree(w.tasks); hipFree(w.pstate); hipFree(w.counters);
+    if (w.done) hipEventDestroy(w.done);
+    if (w.stream) hipStreamDestroy(w.stream);
+    w = TaskWs{};
+  }
   c.d_pts = c.d_p = c.d_g = nullptr;
   c.d_nest = c.d_steps = nullptr;
   c.ws_points = 0;
@@ -580,28 +602,33 @@ int ensure_workspace(DevCtx& c, int dim, size_t npts) {
 // walk tasks per batch: 2^24 tasks = 0.8 GB (2D) / 1.0 GB (3D) of workspace
 constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
 
-int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
+int ensure_tasks_in(float*& d_tasks, int64_t& task_cap, int32_t*& d_pstate, int64_t& pstate_cap, int dim,
+                    int64_t tasks, int64_t points) {
   // sized for 3D records so either dimension fits
   const int tf = std::max(wos::task_floats(dim), wos::task_floats(3));
-  if (tasks > c.task_cap) {
-    hipFree(c.d_tasks);
-    c.d_tasks = nullptr; c.task_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c.d_tasks, (size_t)tasks * tf * sizeof(float)));
-    c.task_cap = tasks;
+  if (tasks > task_cap) {
+    hipFree(d_tasks);
+    d_tasks = nullptr; task_cap = 0;
+    HIP_TRY(hipMalloc((void**)&d_tasks, (size_t)tasks * tf * sizeof(float)));
+    task_cap = tasks;
   }
-  if (points > c.pstate_cap) {
-    hipFree(c.d_pstate);
-    c.d_pstate = nullptr; c.pstate_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c.d_pstate, ((size_t)7 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
-    c.pstate_cap = points;
+  if (points > pstate_cap) {
+    hipFree(d_pstate);
+    d_pstate = nullptr; pstate_cap = 0;
+    HIP_TRY(hipMalloc((void**)&d_pstate, ((size_t)7 * points + 2 * wos::kCostBuckets) * sizeof(int32_t)));
+    pstate_cap = points;
   }
   return WOS_OK;
 }
 
-// SoA views into the task workspace for a chunk of T tasks
-wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
+int ensure_tasks(DevCtx& c, int dim, int64_t tasks, int64_t points) {
+  return ensure_tasks_in(c.d_tasks, c.task_cap, c.d_pstate, c.pstate_cap, dim, tasks, points);
+}
+
+// SoA views into a task workspace for a chunk of T tasks
+wos::DevTasks task_view_in(float* d_tasks, int32_t* d_pstate, int64_t pstate_cap, int dim, int64_t T, int32_t wpp) {
   wos::DevTasks tk{};
-  float* f = c.d_tasks;
+  float* f = d_tasks;
   tk.pt = f; f += dim * T;
   tk.thr = f; f += T;
   tk.tsrc = f; f += T;
@@ -611,15 +638,27 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   tk.sdir = f; f += dim * T;
   tk.total = f; f += T;
   tk.code = (uint32_t*)f;
-  tk.pstate = c.d_pstate;
-  tk.perm = (uint32_t*)(c.d_pstate + c.pstate_cap);
-  tk.prad = (float*)(c.d_pstate + 2 * c.pstate_cap);
-  tk.hist = (uint32_t*)(c.d_pstate + 3 * c.pstate_cap);
-  tk.pball = (float*)(c.d_pstate + 3 * c.pstate_cap + 2 * wos::kCostBuckets);
-  tk.pball_stride = c.pstate_cap;
+  tk.pstate = d_pstate;
+  tk.perm = (uint32_t*)(d_pstate + pstate_cap);
+  tk.prad = (float*)(d_pstate + 2 * pstate_cap);
+  tk.hist = (uint32_t*)(d_pstate + 3 * pstate_cap);
+  tk.pball = (float*)(d_pstate + 3 * pstate_cap + 2 * wos::kCostBuckets);
+  tk.pball_stride = pstate_cap;
   tk.T = T;
   tk.wpp = wpp;
   return tk;
+}
+
+wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
+  return task_view_in(c.d_tasks, c.d_pstate, c.pstate_cap, dim, T, wpp);
+}
+
+// a side workspace's stream, event and counters (created on first use)
+int side_ready(TaskWs& w) {
+  if (!w.stream) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+  if (!w.done) HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+  if (!w.counters) HIP_TRY(hipMalloc((void**)&w.counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
+  return WOS_OK;
 }
 
 // state_k = A_k * state_0 + C_k for the PCG32 LCG (multiplier kPcgMult, increment kPcgInc)
@@ -1138,34 +1177,6 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (nd > 0) HIP_TRY(hipMemcpy(d_dc, smp.dcand.data(), 2 * nd * sizeof(float), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_ept, ept.data(), 2 * ne * sizeof(float), hipMemcpyHostToDevice));
 
-  // ---- Dirichlet samples: estimateSolutionAndGradient along the normal (nWalksForCachedGradient-
-  // Estimates, keyed by the sample index) on the solve pipeline; solution and derivative
-  // unmasked.  First, on its own stat slot (the solve resets the counters), then the rest.
-  wos_stats dstat{};
-  bool have_dstat = false;
-  if (has_dir && !bp->use_finite_differences) {
-    wos_solver_params gp = *prm;
-    gp.n_walks = bp->n_walks_gradient;
-    gp.boundary_distance_mask = 0.0f;
-    SolveExtra ex;
-    ex.force_estimate = true;
-    for (const Run& r : runs) {
-      if (!r.dir) continue;
-      ex.ddir = d_ddir + 2 * r.b0;
-      ex.deriv = d_bdn + r.b0;
-      wos_stats rs{};
-      int rc = solve_locked(s, &gp, d_bpt + 2 * r.b0, r.b1 - r.b0, r.b0, 1, d_bsol + r.b0, d_dgrad, d_bnest + r.b0,
-                            nullptr, &rs, st, WOS_PTRS_DEVICE, ex);
-      if (rc != WOS_OK) return rc;
-      dstat.walk_steps += rs.walk_steps; dstat.wasted_steps += rs.wasted_steps;
-      dstat.walks_recorded += rs.walks_recorded; dstat.walks_escaped += rs.walks_escaped;
-      dstat.walks_max_length += rs.walks_max_length; dstat.walks_rr += rs.walks_rr;
-      dstat.walks_dirichlet += rs.walks_dirichlet; dstat.rejection_iters += rs.rejection_iters;
-      dstat.kernel_ms += rs.kernel_ms;
-      have_dstat = true;
-    }
-  }
-
   const uint64_t ticket = c.next_ticket++;
   StatSlot& q = c.slot[ticket % kStatSlots];
   while (q.bev.size() < 4) {
@@ -1177,7 +1188,6 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   q.n_batches = 1;
   q.bpc_fb = 0;
   q.bpc_walk = 0;
-  HIP_TRY(hipMemsetAsync(c.d_counters, 0, wos::kNumCounterSlots * sizeof(unsigned long long), st));
   HIP_TRY(hipEventRecord(q.ev0, st));
   HIP_TRY(hipEventRecord(q.bev[0], st));
   const wos::DevScene& sc0 = s->dev;
@@ -1233,10 +1243,18 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     HIP_TRY(hipMemcpy(d_ndd, ndd.data(), nn * sizeof(float), hipMemcpyHostToDevice));
   }
 
-  // ---- estimateSolution walks (walk_on_stars.h:353-464) on the persistent walk kernel:
-  // Neumann boundary samples (nWalksForCachedSolutionEstimates, seed tag 6), finite-difference
-  // Dirichlet samples (nWalksForCachedGradientEstimates, tag 8), evaluation points near the
-  // Dirichlet boundary (nWalksForCachedSolutionEstimates, tag 7, keyed by their rank)
+  // ---- Three independent walk sets, on three streams (their tails overlap the others' bulk):
+  //   the call's stream  the Dirichlet samples' estimateSolutionAndGradient along the normal
+  //                      (nWalksForCachedGradientEstimates, keyed by the sample index) on the
+  //                      solve pipeline, solution and derivative unmasked;
+  //   side[0]            estimateSolution walks (walk_on_stars.h:353-464) of the Neumann
+  //                      boundary samples (nWalksForCachedSolutionEstimates, seed tag 6) and
+  //                      the finite-difference Dirichlet samples (nWalksForCachedGradient-
+  //                      Estimates, tag 8);
+  //   side[1]            estimateSolution walks of the evaluation points near the Dirichlet
+  //                      boundary (nWalksForCachedSolutionEstimates, tag 7, keyed by rank).
+  // Every allocation (layout grids, jump table, workspaces) happens before the first launch:
+  // hipFree / hipMalloc would serialise the streams.
   WalkLayout wl;
   wos_solver_params wp0 = *prm;
   {
@@ -1249,14 +1267,67 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     wl.geom_floats_walk = 0;
     wl.shmem_walk = wos::kWavesPerBlockHost * wos::walk_wave_lds_bytes(2);
   }
+  const bool dir_solve = has_dir && !bp->use_finite_differences;
+  wos_solver_params gp = *prm;
+  gp.n_walks = bp->n_walks_gradient;
+  gp.boundary_distance_mask = 0.0f;
   {
-    int rc = ensure_jump(c, 4096);
+    // the Dirichlet solves' stratified-sample draws (solve_locked) bound the table from above
+    int rc = ensure_jump(c, std::max(4096, 4 * std::max(1, bp->n_walks_gradient)));
     if (rc != WOS_OK) return rc;
   }
-  bool first_walk = true;
-  auto walks = [&](const float* pts_d, const float* nrm_d, const uint8_t* al_d, const float* dd_d, int64_t np_,
+  int64_t side_tasks[kSideWs] = {0, 0}, side_points[kSideWs] = {0, 0};
+  for (const Run& r : runs) {
+    const int64_t m = r.b1 - r.b0;
+    if (!r.dir || bp->use_finite_differences) {
+      const int64_t w = r.dir ? bp->n_walks_gradient : bp->n_walks_solution;
+      if (m * w > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
+      side_tasks[0] = std::max(side_tasks[0], m * w);
+      side_points[0] = std::max(side_points[0], m);
+    } else if (dir_solve) {
+      const int64_t wpp = gp.disable_gradient_antithetic_variates ? gp.n_walks : 2 * std::max(1, gp.n_walks / 2);
+      const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(m, kMaxBatchTasks / wpp));
+      int rc = ensure_tasks(c, 2, chunk * wpp, chunk);
+      if (rc != WOS_OK) return rc;
+    }
+  }
+  if (nn * bp->n_walks_solution > kMaxBatchTasks)
+    return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
+  side_tasks[1] = nn * bp->n_walks_solution;
+  side_points[1] = nn;
+  for (int k = 0; k < kSideWs; k++) {
+    TaskWs& w = c.side[k];
+    int rc = side_ready(w);
+    if (rc == WOS_OK) rc = ensure_tasks_in(w.tasks, w.task_cap, w.pstate, w.pstate_cap, 2, side_tasks[k], side_points[k]);
+    if (rc != WOS_OK) return rc;
+  }
+  HIP_TRY(hipEventRecord(q.bev[1], st));
+  for (TaskWs& w : c.side) {
+    HIP_TRY(hipStreamWaitEvent(w.stream, q.bev[1], 0));
+    HIP_TRY(wos::launch_zero(w.counters, wos::kNumCounterSlots, nullptr, 0, w.stream));
+  }
+
+  std::vector<uint64_t> dtickets;
+  if (dir_solve) {
+    SolveExtra ex;
+    ex.force_estimate = true;
+    for (const Run& r : runs) {
+      if (!r.dir) continue;
+      ex.ddir = d_ddir + 2 * r.b0;
+      ex.deriv = d_bdn + r.b0;
+      wos_stats rs{};
+      int rc = solve_locked(s, &gp, d_bpt + 2 * r.b0, r.b1 - r.b0, r.b0, 1, d_bsol + r.b0, d_dgrad, d_bnest + r.b0,
+                            nullptr, &rs, st, WOS_PTRS_DEVICE | WOS_ASYNC, ex);
+      if (rc != WOS_OK) return rc;
+      dtickets.push_back(rs.ticket);
+    }
+  }
+
+  bool first_walk[kSideWs] = {true, true};
+  auto walks = [&](int k, const float* pts_d, const float* nrm_d, const uint8_t* al_d, const float* dd_d, int64_t np_,
                    int64_t base, int n_walks, int on_neumann, uint32_t tag, float* sol_d, int32_t* nest_d) -> int {
     if (np_ <= 0) return WOS_OK;
+    TaskWs& w = c.side[k];
     wos_solver_params wp = *prm;
     wp.n_walks = n_walks;
     wp.disable_gradient_antithetic_variates = 1;  // one walk per task, no pairs
@@ -1265,55 +1336,54 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     dp.n_jump = c.n_jump;
     dp.rej_tab = c.d_rejtab;
     const int64_t wpp = n_walks;
-    if (np_ * wpp > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
-    int rc = ensure_tasks(c, 2, np_ * wpp, np_);
-    if (rc != WOS_OK) return rc;
-    wos::DevTasks tk = task_view(c, 2, np_ * wpp, (int32_t)wpp);
+    wos::DevTasks tk = task_view_in(w.tasks, w.pstate, w.pstate_cap, 2, np_ * wpp, (int32_t)wpp);
     tk.n0 = tk.bdir;
     tk.r0 = tk.first;
     tk.sflags = reinterpret_cast<uint32_t*>(tk.sdir);
     // the walk queue's counters start at 0 for every launch
-    if (!first_walk) HIP_TRY(wos::launch_zero(c.d_counters + wos::kNumCounters, wos::kNumCounterSlots - wos::kNumCounters,
-                                              nullptr, 0, st));
-    first_walk = false;
-    HIP_TRY(wos::launch_bvc_start(dsc, dp, pts_d, nrm_d, al_d, dd_d, np_, tk, on_neumann, tag, st));
+    if (!first_walk[k])
+      HIP_TRY(wos::launch_zero(w.counters + wos::kNumCounters, wos::kNumCounterSlots - wos::kNumCounters, nullptr, 0,
+                               w.stream));
+    first_walk[k] = false;
+    HIP_TRY(wos::launch_bvc_start(dsc, dp, pts_d, nrm_d, al_d, dd_d, np_, tk, on_neumann, tag, w.stream));
     int bpc = 0;
     HIP_TRY(wos::occupancy_walk_bstart(dsc.geom_global != 0, wl.shmem_walk, &bpc, dp.robust != 0));
     const int grid = (int)std::min<int64_t>((int64_t)std::max(1, bpc) * std::max(1, c.num_cus), (tk.T + 63) / 64);
-    unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
-    HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, base, 1, c.d_counters, q_tasks, grid, wl.shmem_walk,
-                                     wl.geom_floats_walk, st));
-    HIP_TRY(wos::launch_bvc_fold(tk, np_, sol_d, nest_d, st));
+    unsigned int* q_tasks = (unsigned int*)(w.counters + wos::kTaskQueueSlot0);
+    HIP_TRY(wos::launch_walks_bstart(dsc, dp, tk, base, 1, w.counters, q_tasks, grid, wl.shmem_walk,
+                                     wl.geom_floats_walk, w.stream));
+    HIP_TRY(wos::launch_bvc_fold(tk, np_, sol_d, nest_d, w.stream));
     q.bpc_walk = bpc;
     return WOS_OK;
   };
-  HIP_TRY(hipEventRecord(q.bev[1], st));
   for (const Run& r : runs) {
     const int64_t m = r.b1 - r.b0;
     int rc = WOS_OK;
     if (!r.dir)
-      rc = walks(d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_solution, 1, 6u,
-                 d_bsol + r.b0, d_bnest + r.b0);
+      rc = walks(0, d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_solution, 1,
+                 6u, d_bsol + r.b0, d_bnest + r.b0);
     else if (bp->use_finite_differences)
-      rc = walks(d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_gradient, 0, 8u,
-                 d_bsol + r.b0, d_bnest + r.b0);
+      rc = walks(0, d_bpt + 2 * r.b0, d_bnrm + 2 * r.b0, d_al + r.b0, d_bdd + r.b0, m, r.b0, bp->n_walks_gradient, 0,
+                 8u, d_bsol + r.b0, d_bnest + r.b0);
     if (rc != WOS_OK) return rc;
     if (r.dir && bp->use_finite_differences)
-      HIP_TRY(wos::launch_bvc_fd(s->dev, d_bpt + 2 * r.b0, d_bsol + r.b0, m, d_bdn + r.b0, st));
+      HIP_TRY(wos::launch_bvc_fd(s->dev, d_bpt + 2 * r.b0, d_bsol + r.b0, m, d_bdn + r.b0, c.side[0].stream));
   }
   {
-    int rc = walks(d_npt, nullptr, nullptr, d_ndd, nn, 0, bp->n_walks_solution, 0, 7u, d_nsol, d_nnest);
+    int rc = walks(1, d_npt, nullptr, nullptr, d_ndd, nn, 0, bp->n_walks_solution, 0, 7u, d_nsol, d_nnest);
     if (rc != WOS_OK) return rc;
   }
-  HIP_TRY(hipEventRecord(q.bev[2], st));
+  for (TaskWs& w : c.side) HIP_TRY(hipEventRecord(w.done, w.stream));
   q.walk_lds = (int32_t)wl.shmem_walk;
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
   q.dir_grid = dsc.dgrid != nullptr;
 
-  // ---- the cache: boundary samples (solution; the Neumann value 0: pde.neumann, scene.h:176-181;
-  // Dirichlet samples their normal derivative), then the domain samples inside the solve
-  // region (source)
+  // ---- the cache, once the boundary samples' estimates are in (the Dirichlet solves on this
+  // stream, side[0]): boundary samples (solution; the Neumann value 0: pde.neumann,
+  // scene.h:176-181; Dirichlet samples their normal derivative), then the domain samples
+  // inside the solve region (source).  The near-boundary walks keep running on side[1].
+  HIP_TRY(hipStreamWaitEvent(st, c.side[0].done, 0));
   std::vector<float> bsol(nb), bdn(nb), dsrc(nd), nsol(nn);
   std::vector<int32_t> din(nd);
   if (nb > 0) {
@@ -1324,7 +1394,6 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     HIP_TRY(hipMemcpyAsync(dsrc.data(), d_dsrc, nd * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(din.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   }
-  if (nn > 0) HIP_TRY(hipMemcpyAsync(nsol.data(), d_nsol, nn * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   std::vector<float> recs;
   recs.reserve((size_t)(nb + nd) * wos::kBvcRec);
@@ -1348,13 +1417,23 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   const int64_t nrec = nb + nd_kept;
   float* d_recs = nullptr;
   HIP_TRY(B.get(&d_recs, (size_t)nrec * wos::kBvcRec));
-  if (nrec > 0) HIP_TRY(hipMemcpy(d_recs, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (nrec > 0)
+    HIP_TRY(hipMemcpyAsync(d_recs, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(q.bev[2], st));
   HIP_TRY(wos::launch_bvc_splat(d_recs, (int)nrec, d_ept, d_edd, d_end, d_ein, ne, s->dev.absorption,
                                 bp->radius_clamp, bp->kernel_regularization, bp->normal_offset,
                                 prm->boundary_distance_mask, geom.double_sided, d_sol, d_grad, st));
+  HIP_TRY(hipStreamWaitEvent(st, c.side[1].done, 0));
   HIP_TRY(hipEventRecord(q.bev[3], st));
   HIP_TRY(hipEventRecord(q.ev1, st));
-  HIP_TRY(hipMemcpyAsync(q.h_cnt, c.d_counters, wos::kNumCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  // the walk counters of both side workspaces (summed below); the Dirichlet solves' own
+  // counters are in their stat slots
+  std::vector<unsigned long long> cnt1(wos::kNumCounters);
+  HIP_TRY(hipMemcpyAsync(q.h_cnt, c.side[0].counters, wos::kNumCounters * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(cnt1.data(), c.side[1].counters, wos::kNumCounters * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
+  if (nn > 0) HIP_TRY(hipMemcpyAsync(nsol.data(), d_nsol, nn * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(solution, d_sol, ne * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(grad, d_grad, 2 * ne * sizeof(float), hipMemcpyDeviceToHost, st));
   std::vector<float> end_h(nn > 0 ? ne : 0);
@@ -1366,6 +1445,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(hipEventRecord(q.done, st));
   HIP_TRY(hipStreamSynchronize(st));
   c.inflight = false;
+  for (int k = 0; k < wos::kNumCounters; k++) q.h_cnt[k] += cnt1[k];
   wos::diag_dump("bvc");  // DIAG builds only
   // the pointwise estimates near the Dirichlet boundary replace the (unsplatted) points'
   // statistics: solution = the estimate, gradient 0 (evalPt.reset, splatter.h:186-192),
@@ -1381,12 +1461,17 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     int rc = fill_stats(q, stats);
     if (rc != WOS_OK) return rc;
     stats->points_estimated = (uint64_t)nb;
-    if (have_dstat) {
-      stats->walk_steps += dstat.walk_steps; stats->wasted_steps += dstat.wasted_steps;
-      stats->walks_recorded += dstat.walks_recorded; stats->walks_escaped += dstat.walks_escaped;
-      stats->walks_max_length += dstat.walks_max_length; stats->walks_rr += dstat.walks_rr;
-      stats->walks_dirichlet += dstat.walks_dirichlet; stats->rejection_iters += dstat.rejection_iters;
-      stats->kernel_ms += dstat.kernel_ms;
+    // the Dirichlet solves ran inside this call's span: their counters, not their times
+    for (uint64_t t : dtickets) {
+      const StatSlot& dq = c.slot[t % kStatSlots];
+      if (dq.ticket != t) continue;
+      wos_stats rs{};
+      rc = fill_stats(dq, &rs);
+      if (rc != WOS_OK) return rc;
+      stats->walk_steps += rs.walk_steps; stats->wasted_steps += rs.wasted_steps;
+      stats->walks_recorded += rs.walks_recorded; stats->walks_escaped += rs.walks_escaped;
+      stats->walks_max_length += rs.walks_max_length; stats->walks_rr += rs.walks_rr;
+      stats->walks_dirichlet += rs.walks_dirichlet; stats->rejection_iters += rs.rejection_iters;
     }
   }
   if (samples && nrec > 0) {

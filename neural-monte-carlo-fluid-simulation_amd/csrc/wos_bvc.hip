@@ -240,7 +240,9 @@ __device__ __forceinline__ int splat_term(const FreeSpace2& gf, const float* R, 
   float G = gf.evaluate(r, K0);
   float dG[2];
   gf.gradient(r, xy, K1, dG);
-  const float dGNorm = __builtin_sqrtf(dG[0] * dG[0] + dG[1] * dG[1]);
+  // the kernel norms |dG|, |dP| only gate on finiteness (splatter.h:224-228, 273-275): the
+  // square root of a sum of squares is finite exactly when the sum is
+  const float dGNorm2 = dG[0] * dG[0] + dG[1] * dG[1];
   const bool al = kind == kBvcAligned || kind == kBvcDirichletAligned;
   if (kind != kBvcDomain) {  // splatBoundaryData (splatter.h:214-264)
     const float nd = R[6];
@@ -249,8 +251,8 @@ __device__ __forceinline__ int splat_term(const FreeSpace2& gf, const float* R, 
     float P = gf.poisson(r, xy, n, K1);
     float dP[2];
     gf.poisson_gradient(r, xy, n, K0, K1, K2, dP);
-    const float dPNorm = __builtin_sqrtf(dP[0] * dP[0] + dP[1] * dP[1]);
-    if (!(finite_f(G) && finite_f(P) && finite_f(dGNorm) && finite_f(dPNorm))) return 3;
+    const float dPNorm2 = dP[0] * dP[0] + dP[1] * dP[1];
+    if (!(finite_f(G) && finite_f(P) && finite_f(dGNorm2) && finite_f(dPNorm2))) return 3;
     if (reg > 0.0f) {
       r /= reg;
       P *= 1.0f - fexp(-r * r);  // computePoissonKernelRegularization<2> (splatter.h:28-32)
@@ -260,7 +262,7 @@ __device__ __forceinline__ int splat_term(const FreeSpace2& gf, const float* R, 
     return al ? 1 : 0;
   }
   // splatSourceData (splatter.h:267-301)
-  if (!(finite_f(G) && finite_f(dGNorm))) return 3;
+  if (!(finite_f(G) && finite_f(dGNorm2))) return 3;
   *est = (G * value) / pdf;
   for (int k = 0; k < 2; k++) ge[k] = (dG[k] * value) / pdf;
   return 2;

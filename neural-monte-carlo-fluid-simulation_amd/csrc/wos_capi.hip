@@ -905,6 +905,14 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   // scenes beyond the LDS budget (or WOS_SCHED_GEOM_GLOBAL): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
+  // the first-ball kernel's walk-start Dirichlet distances read the cell grid too (global memory)
+  dfb.dgrid = dsc.dgrid;
+  dfb.dgrid_off_words = dsc.dgrid_off_words;
+  for (int k = 0; k < 2; k++) {
+    dfb.dgrid_n[k] = dsc.dgrid_n[k];
+    dfb.dgrid_min[k] = dsc.dgrid_min[k];
+    dfb.dgrid_inv[k] = dsc.dgrid_inv[k];
+  }
   // (only the walk kernel stages geometry, so only its LDS decides)
   if ((prm->schedule & WOS_SCHED_GEOM_GLOBAL) || shmem_walk > kLdsDynamicMax) {
     dfb.geom_global = 1;

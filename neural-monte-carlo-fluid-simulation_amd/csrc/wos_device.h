@@ -3183,7 +3183,12 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
     tk.tsrc[t] = totalSource;
     // without Dirichlet geometry the distance is the bbox far corner of the walk start,
     // recomputed by the walk kernel from the same floats instead of stored and reloaded
-    if (sc.n_dprims > 0) tk.dd[t] = dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
+    if (sc.n_dprims > 0) {
+      // the Dirichlet cell grid where it covers the point (2D), else the culled scan
+      float d = -1.0f;
+      if (DIM == 2 && sc.dgrid) d = dirichlet_dist_grid<DIM>(sc, sc.dprim, g.ySurf);
+      tk.dd[t] = d >= 0.0f ? d : dirichlet_dist_culled<DIM>(sc, sc.dprim, sc.dgroup, g.ySurf);
+    }
     DIAG_ADD(D_FB_ST, t_st);
   }
 }

@@ -277,38 +277,80 @@ __device__ __forceinline__ int splat_term(const FreeSpace2& gf, const float* R, 
 //          over the tile's terms in cache order -- the same division chain per
 //          component as one lane running all three, so the result is unchanged; wave 3
 //          stages the next tile's records.
+// A launch folds the records [r0, r1) of the cache: the statistics start from zero
+// (first) or from `state`, and end in the outputs (last) or in `state` -- so the splat
+// of the Neumann samples can run while the Dirichlet samples are still being estimated,
+// and the rest continues the same division chains exactly.  state: per point, per
+// component, the three classes' means then their counts ([3][6][ne] words).
 constexpr int kSplatPts = 64, kSplatT = 32, kSplatWaves = 4;
 
-// Splatter::splat over every evaluation point and every cached sample (boundary,
+// The evaluation points the splat visits, packed (wave-ordered runs; the order only groups
+// points into waves): not masked by saveEvaluationGrid (grid.h:393-409) -- their output is 0
+// whatever their statistics -- and not within the cutoff of the Dirichlet boundary
+// (splatter.h:94: a pointwise estimate, estimatePointwiseNearDirichletBoundary, replaces
+// them).  Every other point's output is 0 (the outputs are cleared before the splat).
+__global__ __launch_bounds__(256) void wos_bvc_splat_list_kernel(const float* __restrict__ edd,
+                                                                 const float* __restrict__ end_,
+                                                                 const int32_t* __restrict__ ein, int64_t ne,
+                                                                 float cutoff, float mask, int double_sided,
+                                                                 uint32_t* __restrict__ list,
+                                                                 uint32_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool keep = false;
+  if (i < ne) {
+    const float dDist = edd[i];
+    const bool in = ein[i] != 0;
+    const float ad = __builtin_fabsf(dDist), an = __builtin_fabsf(end_[i]);
+    const bool masked = (!in && !double_sided) || smin(ad, an) < mask;
+    keep = !masked && !(dDist < cutoff);
+  }
+  const uint64_t b = __ballot(keep);
+  if (b == 0) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(count, (uint32_t)__popcll(b));
+  base = (uint32_t)__shfl((int)base, 0);
+  if (keep) list[base + rank] = (uint32_t)i;
+}
+
+// Splatter::splat over every listed evaluation point and every cached sample (boundary,
 // normal-aligned, domain in cache order), then EvaluationPoint::getEstimatedSolution /
-// getEstimatedGradient (splatter.h:315-334) and the output mask of saveEvaluationGrid
-// (grid.h:393-409).
+// getEstimatedGradient (splatter.h:315-334).
 __global__ __launch_bounds__(kSplatPts * kSplatWaves) void wos_bvc_splat_kernel(
-    const float* __restrict__ recs, int nrec, const float* __restrict__ ept, const float* __restrict__ edd,
-    const float* __restrict__ end_, const int32_t* __restrict__ ein, int64_t ne, float absorption,
-    float radius_clamp, float reg, float cutoff, float mask, int double_sided, float* __restrict__ sol_out,
+    const float* __restrict__ recs, int r0, int r1, int first, int last, float* __restrict__ state,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, const float* __restrict__ ept,
+    int64_t ne, float absorption, float radius_clamp, float reg, float* __restrict__ sol_out,
     float* __restrict__ grad_out) {
   __shared__ float rtile[2][kSplatT * kBvcRec];
   __shared__ float term[3][kSplatT][kSplatPts];
   __shared__ uint8_t tcls[kSplatT][kSplatPts];
+  const int64_t nl = (int64_t)*count;
+  if ((int64_t)blockIdx.x * kSplatPts >= nl) return;  // block-uniform
   const int lane = threadIdx.x & (kSplatPts - 1);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kSplatPts));
-  const int64_t i = (int64_t)blockIdx.x * kSplatPts + lane;
-  const bool valid = i < ne;
+  const int64_t j = (int64_t)blockIdx.x * kSplatPts + lane;  // list slot
+  const bool valid = j < nl;
+  const int64_t i = valid ? (int64_t)list[j] : 0;
   FreeSpace2 gf;
   gf.yukawa = absorption > 0.0f;
   gf.lambda = absorption;
   gf.sqrtLambda = __builtin_sqrtf(absorption);
-  float x[2] = {0.0f, 0.0f}, dDist = 0.0f;
-  if (valid) { x[0] = ept[2 * i]; x[1] = ept[2 * i + 1]; dDist = edd[i]; }
-  // evaluation points closer than the cutoff to the Dirichlet boundary are not splatted
-  // (splatter.h:94): they take a pointwise estimate (estimatePointwiseNearDirichletBoundary)
-  const bool splat = valid && !(dDist < cutoff);
+  float x[2] = {0.0f, 0.0f};
+  if (valid) { x[0] = ept[2 * i]; x[1] = ept[2 * i + 1]; }
+  const bool splat = valid;
   // this wave's component of the three classes' statistics and their counts
   float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
   int n0 = 0, n1 = 0, n2 = 0;
+  float* sw = state + (size_t)(wave < 3 ? wave : 0) * 6 * ne + j;  // this wave's component, by slot
+  if (!first && valid && wave < 3) {
+    m0 = sw[0]; m1 = sw[ne]; m2 = sw[2 * ne];
+    n0 = __float_as_int(sw[3 * ne]); n1 = __float_as_int(sw[4 * ne]); n2 = __float_as_int(sw[5 * ne]);
+  }
+  const float* rr = recs + (size_t)r0 * kBvcRec;
+  const int nrec = r1 - r0;
   for (int e = threadIdx.x; e < kSplatT * kBvcRec; e += kSplatPts * kSplatWaves)
-    if (e < nrec * kBvcRec) rtile[0][e] = recs[e];
+    if (e < nrec * kBvcRec) rtile[0][e] = rr[e];
   __syncthreads();
   int buf = 0;
   for (int t0 = 0; t0 < nrec; t0 += kSplatT) {
@@ -340,20 +382,22 @@ __global__ __launch_bounds__(kSplatPts * kSplatWaves) void wos_bvc_splat_kernel(
     } else {
       const int nx = t0 + kSplatT;
       for (int e = lane; e < kSplatT * kBvcRec; e += kSplatPts)
-        if ((int64_t)nx * kBvcRec + e < (int64_t)nrec * kBvcRec) rtile[buf ^ 1][e] = recs[(size_t)nx * kBvcRec + e];
+        if ((int64_t)nx * kBvcRec + e < (int64_t)nrec * kBvcRec) rtile[buf ^ 1][e] = rr[(size_t)nx * kBvcRec + e];
     }
     __syncthreads();
     buf ^= 1;
   }
   if (!valid || wave >= 3) return;
+  if (!last) {
+    sw[0] = m0; sw[ne] = m1; sw[2 * ne] = m2;
+    sw[3 * ne] = __int_as_float(n0); sw[4 * ne] = __int_as_float(n1); sw[5 * ne] = __int_as_float(n2);
+    return;
+  }
   float v = m0;
   v += m1;
   v += m2;
-  const bool in = ein[i] != 0;
-  const float ad = __builtin_fabsf(dDist), an = __builtin_fabsf(end_[i]);
-  const bool masked = (!in && !double_sided) || smin(ad, an) < mask;
-  if (wave == 0) sol_out[i] = masked ? 0.0f : v;
-  else grad_out[2 * i + (wave - 1)] = masked ? 0.0f : v;
+  if (wave == 0) sol_out[i] = v;
+  else grad_out[2 * i + (wave - 1)] = v;
 }
 
 template __global__ void wos_walk_kernel<2, false, true>(const DevScene, const DevParams, const DevTasks, int64_t,
@@ -414,13 +458,39 @@ hipError_t launch_bvc_fold(const DevTasks& tk, int64_t nb, float* sol, int32_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const float* edd, const float* end_,
-                            const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
-                            float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s) {
+hipError_t launch_bvc_splat_list(const float* edd, const float* end_, const int32_t* ein, int64_t ne, float cutoff,
+                                 float mask, int double_sided, uint32_t* list, uint32_t* count, hipStream_t s) {
+  if (ne <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wos_bvc_splat_list_kernel, dim3((int)((ne + 255) / 256)), dim3(256), 0, s, edd, end_, ein, ne,
+                     cutoff, mask, double_sided, list, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bvc_splat(const float* recs, int r0, int r1, int first, int last, float* state,
+                            const uint32_t* list, const uint32_t* count, const float* ept, int64_t ne,
+                            float absorption, float radius_clamp, float reg, float* sol, float* grad, hipStream_t s) {
   if (ne <= 0) return hipSuccess;
   hipLaunchKernelGGL(wos_bvc_splat_kernel, dim3((int)((ne + kSplatPts - 1) / kSplatPts)), dim3(kSplatPts * kSplatWaves),
-                     0, s, recs, nrec, ept, edd, end_, ein, ne, absorption, radius_clamp, reg, cutoff, mask,
-                     double_sided, sol, grad);
+                     0, s, recs, r0, r1, first, last, state, list, count, ept, ne, absorption, radius_clamp, reg, sol,
+                     grad);
+  return hipGetLastError();
+}
+
+// the estimated values of the boundary records [b0, b1): the solution, and a Dirichlet
+// sample's normal derivative (kinds 3, 4) -- written once the walks that estimate them are done
+__global__ __launch_bounds__(256) void wos_bvc_fill_kernel(float* __restrict__ recs, int64_t b0, int64_t b1,
+                                                           const float* __restrict__ bsol,
+                                                           const float* __restrict__ bdn) {
+  const int64_t i = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b1) return;
+  const int kind = (int)recs[i * kBvcRec + 7];
+  recs[i * kBvcRec + 5] = bsol[i];
+  recs[i * kBvcRec + 6] = (kind == kBvcDirichlet || kind == kBvcDirichletAligned) ? bdn[i] : 0.0f;
+}
+
+hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn, hipStream_t s) {
+  if (b1 <= b0) return hipSuccess;
+  hipLaunchKernelGGL(wos_bvc_fill_kernel, dim3((int)((b1 - b0 + 255) / 256)), dim3(256), 0, s, recs, b0, b1, bsol, bdn);
   return hipGetLastError();
 }
 

@@ -110,6 +110,8 @@ struct DevCtx {
   int stat_waiters = 0;        // wos_solve_stats calls waiting on a slot's event without the lock
   std::condition_variable no_waiters;
   TaskWs side[kSideWs];        // boundary value caching's side-stream workspaces (lazy)
+  hipStream_t bvc_dir = nullptr;  // boundary value caching: the Dirichlet samples' solve (lazy)
+  hipEvent_t bvc_dir_done = nullptr;
 };
 
 constexpr int kMaxDevices = 64;
@@ -128,6 +130,10 @@ void ctx_free(DevCtx& c) {
     q = StatSlot{};
   }
   if (c.done) hipEventDestroy(c.done);
+  if (c.bvc_dir_done) hipEventDestroy(c.bvc_dir_done);
+  if (c.bvc_dir) hipStreamDestroy(c.bvc_dir);
+  c.bvc_dir_done = nullptr;
+  c.bvc_dir = nullptr;
   for (TaskWs& w : c.side) {
     hipFree(w.tasks); hipFree(w.pstate); hipFree(w.counters);
     if (w.done) hipEventDestroy(w.done);
@@ -653,9 +659,24 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
   return task_view_in(c.d_tasks, c.d_pstate, c.pstate_cap, dim, T, wpp);
 }
 
+// Stream priorities of boundary value caching's walk sets: the Dirichlet samples' solve and
+// the Neumann samples' walks feed the splat (high), the near-boundary walks do not (low).
+#ifndef WOS_BVC_PRIO
+#define WOS_BVC_PRIO 1
+#endif
+#ifndef WOS_BVC_WPRIO
+#define WOS_BVC_WPRIO 1
+#endif
+
+int bvc_priority(bool high) {
+  int least = 0, greatest = 0;
+  if (!WOS_BVC_PRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+  return high ? greatest : least;
+}
+
 // a side workspace's stream, event and counters (created on first use)
-int side_ready(TaskWs& w) {
-  if (!w.stream) HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+int side_ready(TaskWs& w, int priority) {
+  if (!w.stream) HIP_TRY(hipStreamCreateWithPriority(&w.stream, hipStreamNonBlocking, priority));
   if (!w.done) HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
   if (!w.counters) HIP_TRY(hipMalloc((void**)&w.counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
   return WOS_OK;
@@ -830,6 +851,7 @@ struct SolveExtra {
   const float* ddir = nullptr;
   float* deriv = nullptr;
   bool force_estimate = false;
+  int wave_prio = 0;  // the walk / fold kernels' waves at this issue priority (0..3)
 };
 
 int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, int64_t n, int64_t index_base,
@@ -879,6 +901,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
 
   wos::DevParams dp = dev_params(prm);
   dp.force_estimate = ex.force_estimate ? 1 : 0;
+  dp.wave_prio = ex.wave_prio;
   {
     // diagonal draws + shuffle draws of the stratified samples
     const int k_needed = 2 * (2 * dp.n_pairs) * (dim - 1);
@@ -1202,21 +1225,33 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_bpt, nb, d_bdd, nullptr, nullptr, nullptr, st));
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_dc, nd, nullptr, nullptr, d_din, d_dsrc, st));
   HIP_TRY(wos::launch_bvc_point_info(sc0, d_ept, ne, d_edd, d_end, d_ein, nullptr, st));
+  // the splat's packed point list; the outputs of every other point are 0
+  uint32_t *d_slist = nullptr, *d_scount = nullptr;
+  HIP_TRY(B.get(&d_slist, ne)); HIP_TRY(B.get(&d_scount, 1));
+  HIP_TRY(hipMemsetAsync(d_scount, 0, sizeof(uint32_t), st));
+  HIP_TRY(hipMemsetAsync(d_sol, 0, ne * sizeof(float), st));
+  HIP_TRY(hipMemsetAsync(d_grad, 0, 2 * ne * sizeof(float), st));
+  HIP_TRY(wos::launch_bvc_splat_list(d_edd, d_end, d_ein, ne, bp->normal_offset, prm->boundary_distance_mask,
+                                     geom.double_sided, d_slist, d_scount, st));
   // the cache size is known once the domain candidates' inside test is: a samples buffer
   // too small for it fails here, before the walks, with counts[] filled for a retry
-  int64_t nd_keep = nd;
-  if (!geom.double_sided && nd > 0) {
-    std::vector<int32_t> din0(nd);
-    HIP_TRY(hipMemcpyAsync(din0.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    nd_keep = 0;
-    for (int64_t i = 0; i < nd; i++) nd_keep += din0[i] != 0;
-  } else if (geom.double_sided) {
-    nd_keep = 0;
-    for (int64_t i = 0; i < nd; i++) {
-      const float x = smp.dcand[2 * i], y = smp.dcand[2 * i + 1];
-      nd_keep += (x >= pmin[0] && y >= pmin[1] && x <= pmax[0] && y <= pmax[1]);
-    }
+  // (one host round trip: the inside test and source of the domain candidates, the
+  // evaluation points' Dirichlet distances)
+  std::vector<float> dsrc(nd), edd_h(has_dir ? ne : 0);
+  std::vector<int32_t> din(nd);
+  if (nd > 0) {
+    HIP_TRY(hipMemcpyAsync(din.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(dsrc.data(), d_dsrc, nd * sizeof(float), hipMemcpyDeviceToHost, st));
+  }
+  if (has_dir) HIP_TRY(hipMemcpyAsync(edd_h.data(), d_edd, ne * sizeof(float), hipMemcpyDeviceToHost, st));
+  if (nd > 0 || has_dir) HIP_TRY(hipStreamSynchronize(st));
+  std::vector<uint8_t> dkeep(nd);
+  int64_t nd_keep = 0;
+  for (int64_t i = 0; i < nd; i++) {
+    const float x = smp.dcand[2 * i], y = smp.dcand[2 * i + 1];
+    // insideSolveRegion (demo.cpp:302-304): the inside test, or the bounding box if double-sided
+    dkeep[i] = geom.double_sided ? (x >= pmin[0] && y >= pmin[1] && x <= pmax[0] && y <= pmax[1]) : din[i] != 0;
+    nd_keep += dkeep[i];
   }
   if (samples && samples_capacity < nb + nd_keep) {
     if (counts) { counts[0] = smp.nb_main; counts[1] = smp.nb_aligned; counts[2] = nd_keep; counts[3] = nb + nd_keep; }
@@ -1228,11 +1263,8 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   }
   // evaluation points within normalOffset of the Dirichlet boundary (splatter.h:160-196)
   std::vector<int64_t> near_idx;
-  std::vector<float> near_pt, edd_h;
+  std::vector<float> near_pt;
   if (has_dir) {
-    edd_h.resize(ne);
-    HIP_TRY(hipMemcpyAsync(edd_h.data(), d_edd, ne * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     for (int64_t i = 0; i < ne; i++)
       if (edd_h[i] < bp->normal_offset) {
         near_idx.push_back(i);
@@ -1251,8 +1283,34 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     HIP_TRY(hipMemcpy(d_ndd, ndd.data(), nn * sizeof(float), hipMemcpyHostToDevice));
   }
 
+  // ---- the cache (splatter order): boundary samples (value = the solution, filled in on the
+  // device once their walks are done; the Neumann value 0: pde.neumann, scene.h:176-181;
+  // Dirichlet samples also their normal derivative), then the domain samples inside the
+  // solve region (value = the source)
+  std::vector<float> recs;
+  recs.reserve((size_t)(nb + nd_keep) * wos::kBvcRec);
+  for (int64_t i = 0; i < nb; i++) {
+    const bool al = smp.aligned[i] != 0, dir = smp.dirichlet[i] != 0;
+    const int kind = dir ? (al ? wos::kBvcDirichletAligned : wos::kBvcDirichlet) : (al ? wos::kBvcAligned : wos::kBvcBoundary);
+    const float r[wos::kBvcRec] = {smp.bpt[2 * i], smp.bpt[2 * i + 1], smp.bnrm[2 * i], smp.bnrm[2 * i + 1],
+                                   al ? smp.pdf_aligned : smp.pdf_main, 0.0f, 0.0f, (float)kind};
+    recs.insert(recs.end(), r, r + wos::kBvcRec);
+  }
+  for (int64_t i = 0; i < nd; i++) {
+    if (!dkeep[i]) continue;
+    const float r[wos::kBvcRec] = {smp.dcand[2 * i], smp.dcand[2 * i + 1], 0.0f, 0.0f, smp.pdf_domain, dsrc[i], 0.0f,
+                                   (float)wos::kBvcDomain};
+    recs.insert(recs.end(), r, r + wos::kBvcRec);
+  }
+  const int64_t nd_kept = nd_keep;
+  const int64_t nrec = nb + nd_kept;
+  float *d_recs = nullptr, *d_state = nullptr;
+  HIP_TRY(B.get(&d_recs, (size_t)nrec * wos::kBvcRec));
+  HIP_TRY(B.get(&d_state, (size_t)18 * ne));
+  if (nrec > 0) HIP_TRY(hipMemcpy(d_recs, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice));
+
   // ---- Three independent walk sets, on three streams (their tails overlap the others' bulk):
-  //   the call's stream  the Dirichlet samples' estimateSolutionAndGradient along the normal
+  //   bvc_dir            the Dirichlet samples' estimateSolutionAndGradient along the normal
   //                      (nWalksForCachedGradientEstimates, keyed by the sample index) on the
   //                      solve pipeline, solution and derivative unmasked;
   //   side[0]            estimateSolution walks (walk_on_stars.h:353-464) of the Neumann
@@ -1305,11 +1363,14 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   side_points[1] = nn;
   for (int k = 0; k < kSideWs; k++) {
     TaskWs& w = c.side[k];
-    int rc = side_ready(w);
+    int rc = side_ready(w, bvc_priority(k == 0));
     if (rc == WOS_OK) rc = ensure_tasks_in(w.tasks, w.task_cap, w.pstate, w.pstate_cap, 2, side_tasks[k], side_points[k]);
     if (rc != WOS_OK) return rc;
   }
+  if (!c.bvc_dir) HIP_TRY(hipStreamCreateWithPriority(&c.bvc_dir, hipStreamNonBlocking, bvc_priority(true)));
+  if (!c.bvc_dir_done) HIP_TRY(hipEventCreateWithFlags(&c.bvc_dir_done, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(q.bev[1], st));
+  HIP_TRY(hipStreamWaitEvent(c.bvc_dir, q.bev[1], 0));
   for (TaskWs& w : c.side) {
     HIP_TRY(hipStreamWaitEvent(w.stream, q.bev[1], 0));
     HIP_TRY(wos::launch_zero(w.counters, wos::kNumCounterSlots, nullptr, 0, w.stream));
@@ -1319,17 +1380,19 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (dir_solve) {
     SolveExtra ex;
     ex.force_estimate = true;
+    ex.wave_prio = WOS_BVC_WPRIO ? 2 : 0;
     for (const Run& r : runs) {
       if (!r.dir) continue;
       ex.ddir = d_ddir + 2 * r.b0;
       ex.deriv = d_bdn + r.b0;
       wos_stats rs{};
       int rc = solve_locked(s, &gp, d_bpt + 2 * r.b0, r.b1 - r.b0, r.b0, 1, d_bsol + r.b0, d_dgrad, d_bnest + r.b0,
-                            nullptr, &rs, st, WOS_PTRS_DEVICE | WOS_ASYNC, ex);
+                            nullptr, &rs, c.bvc_dir, WOS_PTRS_DEVICE | WOS_ASYNC, ex);
       if (rc != WOS_OK) return rc;
       dtickets.push_back(rs.ticket);
     }
   }
+  HIP_TRY(hipEventRecord(c.bvc_dir_done, c.bvc_dir));
 
   bool first_walk[kSideWs] = {true, true};
   auto walks = [&](int k, const float* pts_d, const float* nrm_d, const uint8_t* al_d, const float* dd_d, int64_t np_,
@@ -1343,6 +1406,9 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     dp.jump = c.d_jump;
     dp.n_jump = c.n_jump;
     dp.rej_tab = c.d_rejtab;
+    // the Neumann samples' harmonic walks run longest (reflecting, up to maxWalkLength): top
+    // issue priority; the near-boundary walks feed nothing downstream: none
+    dp.wave_prio = WOS_BVC_WPRIO && k == 0 ? 3 : 0;
     const int64_t wpp = n_walks;
     wos::DevTasks tk = task_view_in(w.tasks, w.pstate, w.pstate_cap, 2, np_ * wpp, (int32_t)wpp);
     tk.n0 = tk.bdir;
@@ -1381,56 +1447,37 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     int rc = walks(1, d_npt, nullptr, nullptr, d_ndd, nn, 0, bp->n_walks_solution, 0, 7u, d_nsol, d_nnest);
     if (rc != WOS_OK) return rc;
   }
-  for (TaskWs& w : c.side) HIP_TRY(hipEventRecord(w.done, w.stream));
   q.walk_lds = (int32_t)wl.shmem_walk;
   q.star_grid = dsc.sgrid != nullptr;
   q.geom_global = dsc.geom_global;
   q.dir_grid = dsc.dgrid != nullptr;
 
-  // ---- the cache, once the boundary samples' estimates are in (the Dirichlet solves on this
-  // stream, side[0]): boundary samples (solution; the Neumann value 0: pde.neumann,
-  // scene.h:176-181; Dirichlet samples their normal derivative), then the domain samples
-  // inside the solve region (source).  The near-boundary walks keep running on side[1].
+  // ---- the splat in two launches over the cache order: the records whose values side[0]
+  // estimates (the Neumann samples before the first Dirichlet sample of the solve; all the
+  // boundary samples without one) as soon as side[0]'s walks are done, beside the
+  // Dirichlet solve; then the rest on the call's stream, continuing the same statistics
+  int64_t p1 = nb;
+  if (dir_solve)
+    for (int64_t i = 0; i < nb; i++)
+      if (smp.dirichlet[i]) { p1 = i; break; }
+  const float ab = s->dev.absorption;
+  const bool part1 = p1 > 0, part1_last = p1 == nrec;
+  if (part1) {
+    HIP_TRY(wos::launch_bvc_fill(d_recs, 0, p1, d_bsol, d_bdn, c.side[0].stream));
+    HIP_TRY(wos::launch_bvc_splat(d_recs, 0, (int)p1, 1, part1_last ? 1 : 0, d_state, d_slist, d_scount, d_ept, ne,
+                                  ab, bp->radius_clamp, bp->kernel_regularization, d_sol, d_grad, c.side[0].stream));
+  }
+  for (TaskWs& w : c.side) HIP_TRY(hipEventRecord(w.done, w.stream));
+  HIP_TRY(hipStreamWaitEvent(st, c.bvc_dir_done, 0));
   HIP_TRY(hipStreamWaitEvent(st, c.side[0].done, 0));
-  std::vector<float> bsol(nb), bdn(nb), dsrc(nd), nsol(nn);
-  std::vector<int32_t> din(nd);
-  if (nb > 0) {
-    HIP_TRY(hipMemcpyAsync(bsol.data(), d_bsol, nb * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(bdn.data(), d_bdn, nb * sizeof(float), hipMemcpyDeviceToHost, st));
-  }
-  if (nd > 0) {
-    HIP_TRY(hipMemcpyAsync(dsrc.data(), d_dsrc, nd * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(din.data(), d_din, nd * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  }
-  HIP_TRY(hipStreamSynchronize(st));
-  std::vector<float> recs;
-  recs.reserve((size_t)(nb + nd) * wos::kBvcRec);
-  for (int64_t i = 0; i < nb; i++) {
-    const bool al = smp.aligned[i] != 0, dir = smp.dirichlet[i] != 0;
-    const int kind = dir ? (al ? wos::kBvcDirichletAligned : wos::kBvcDirichlet) : (al ? wos::kBvcAligned : wos::kBvcBoundary);
-    const float r[wos::kBvcRec] = {smp.bpt[2 * i], smp.bpt[2 * i + 1], smp.bnrm[2 * i], smp.bnrm[2 * i + 1],
-                                   al ? smp.pdf_aligned : smp.pdf_main, bsol[i], dir ? bdn[i] : 0.0f, (float)kind};
-    recs.insert(recs.end(), r, r + wos::kBvcRec);
-  }
-  int64_t nd_kept = 0;
-  for (int64_t i = 0; i < nd; i++) {
-    const float x = smp.dcand[2 * i], y = smp.dcand[2 * i + 1];
-    // insideSolveRegion (demo.cpp:302-304): the inside test, or the bounding box if double-sided
-    const bool keep = geom.double_sided ? (x >= pmin[0] && y >= pmin[1] && x <= pmax[0] && y <= pmax[1]) : din[i] != 0;
-    if (!keep) continue;
-    const float r[wos::kBvcRec] = {x, y, 0.0f, 0.0f, smp.pdf_domain, dsrc[i], 0.0f, (float)wos::kBvcDomain};
-    recs.insert(recs.end(), r, r + wos::kBvcRec);
-    nd_kept++;
-  }
-  const int64_t nrec = nb + nd_kept;
-  float* d_recs = nullptr;
-  HIP_TRY(B.get(&d_recs, (size_t)nrec * wos::kBvcRec));
-  if (nrec > 0)
-    HIP_TRY(hipMemcpyAsync(d_recs, recs.data(), recs.size() * sizeof(float), hipMemcpyHostToDevice, st));
   HIP_TRY(hipEventRecord(q.bev[2], st));
-  HIP_TRY(wos::launch_bvc_splat(d_recs, (int)nrec, d_ept, d_edd, d_end, d_ein, ne, s->dev.absorption,
-                                bp->radius_clamp, bp->kernel_regularization, bp->normal_offset,
-                                prm->boundary_distance_mask, geom.double_sided, d_sol, d_grad, st));
+  if (!(part1 && part1_last)) {
+    HIP_TRY(wos::launch_bvc_fill(d_recs, p1, nb, d_bsol, d_bdn, st));
+    HIP_TRY(wos::launch_bvc_splat(d_recs, part1 ? (int)p1 : 0, (int)nrec, part1 ? 0 : 1, 1, d_state, d_slist,
+                                  d_scount, d_ept, ne, ab, bp->radius_clamp, bp->kernel_regularization, d_sol,
+                                  d_grad, st));
+  }
+  std::vector<float> nsol(nn);
   HIP_TRY(hipStreamWaitEvent(st, c.side[1].done, 0));
   HIP_TRY(hipEventRecord(q.bev[3], st));
   HIP_TRY(hipEventRecord(q.ev1, st));
@@ -1444,6 +1491,8 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (nn > 0) HIP_TRY(hipMemcpyAsync(nsol.data(), d_nsol, nn * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(solution, d_sol, ne * sizeof(float), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(grad, d_grad, 2 * ne * sizeof(float), hipMemcpyDeviceToHost, st));
+  if (samples && nrec > 0)  // the cache with its estimated values
+    HIP_TRY(hipMemcpyAsync(recs.data(), d_recs, recs.size() * sizeof(float), hipMemcpyDeviceToHost, st));
   std::vector<float> end_h(nn > 0 ? ne : 0);
   std::vector<int32_t> ein_h(nn > 0 ? ne : 0);
   if (nn > 0) {

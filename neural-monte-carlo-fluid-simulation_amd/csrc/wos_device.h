@@ -3505,6 +3505,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #endif
 }
 
+// issue priority of the calling wave (s_setprio takes an immediate), uniform level 0..3
+__device__ __forceinline__ void wave_priority(int level) {
+  if (level == 1) __builtin_amdgcn_s_setprio(1);
+  else if (level == 2) __builtin_amdgcn_s_setprio(2);
+  else if (level >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 // ---- kernel 2: walks ---------------------------------------------------------
 // The state a walk task starts from (the hand-out of walk_on_stars.h:494-579 after
 // the first ball; BSTART: estimateSolution's boundary start, :437-439) ...
@@ -3673,6 +3680,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   auto divw = [&](uint32_t x) -> uint32_t { return wsh >= 0 ? x >> wsh : x / wpp; };
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
   uint32_t c_iters = 0;
+  wave_priority(prm.wave_prio);
 
   DIAG_T0(t_wave);
   // ---- task supply: a window [wq, we) of the global queue (wave-uniform; lane i
@@ -3866,6 +3874,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
                                                                int32_t* __restrict__ steps_out) {
   constexpr int NF = 3 + 2 * DIM;  // code | total | first | bdir[DIM] | sdir[DIM]
   constexpr int LD = kFoldChunk + 1;
+  wave_priority(prm.wave_prio);
   __shared__ float lds[NF][kFoldPoints][LD];
   const int tid = threadIdx.x;
   const int64_t p0 = (int64_t)blockIdx.x * kFoldPoints;

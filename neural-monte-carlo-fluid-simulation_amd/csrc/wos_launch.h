@@ -51,9 +51,12 @@ hipError_t launch_walks_bstart(const DevScene& sc, const DevParams& prm, const D
                                size_t shmem, int geom_floats, hipStream_t s);
 hipError_t occupancy_walk_bstart(bool geom_global, size_t shmem, int* blocks, bool robust = false);
 hipError_t launch_bvc_fold(const DevTasks& tk, int64_t nb, float* sol, int32_t* nest, hipStream_t s);
-hipError_t launch_bvc_splat(const float* recs, int nrec, const float* ept, const float* edd, const float* end_,
-                            const int32_t* ein, int64_t ne, float absorption, float radius_clamp, float reg,
-                            float cutoff, float mask, int double_sided, float* sol, float* grad, hipStream_t s);
+hipError_t launch_bvc_splat_list(const float* edd, const float* end_, const int32_t* ein, int64_t ne, float cutoff,
+                                 float mask, int double_sided, uint32_t* list, uint32_t* count, hipStream_t s);
+hipError_t launch_bvc_splat(const float* recs, int r0, int r1, int first, int last, float* state,
+                            const uint32_t* list, const uint32_t* count, const float* ept, int64_t ne,
+                            float absorption, float radius_clamp, float reg, float* sol, float* grad, hipStream_t s);
+hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn, hipStream_t s);
 // robust float semantics (wos_robust.hip): the same launches with Gfn<DIM, true>;
 // the launchers above dispatch here when prm.robust is set
 hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,

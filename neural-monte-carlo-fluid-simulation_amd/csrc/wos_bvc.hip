@@ -406,6 +406,8 @@ template __global__ void wos_walk_kernel<2, true, true>(const DevScene, const De
                                                           int64_t, unsigned long long*, unsigned int*, int);
 
 // ---- host launchers ----------------------------------------------------------
+void diag_dump_bstart(const char* tag) { diag_print(tag, HIP_SYMBOL(g_diag)); }
+
 hipError_t launch_bvc_point_info(const DevScene& sc, const float* pts, int64_t n, float* dd, float* nd,
                                  int32_t* inside, float* src, hipStream_t s) {
   if (n <= 0) return hipSuccess;

@@ -1504,6 +1504,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   c.inflight = false;
   for (int k = 0; k < wos::kNumCounters; k++) q.h_cnt[k] += cnt1[k];
   wos::diag_dump("bvc");  // DIAG builds only
+  wos::diag_dump_bstart("bvc-bstart");
   // the pointwise estimates near the Dirichlet boundary replace the (unsplatted) points'
   // statistics: solution = the estimate, gradient 0 (evalPt.reset, splatter.h:186-192),
   // then saveEvaluationGrid's mask (grid.h:404-408)

@@ -198,10 +198,13 @@ hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t 
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3, false>, kBlock, shmem);
 }
 
-void diag_dump(const char* tag) {
+void diag_dump(const char* tag) { diag_print(tag, HIP_SYMBOL(g_diag)); }
+
+// g_diag is per translation unit: `sym` is the calling unit's copy
+void diag_print(const char* tag, const void* sym) {
 #if WOS_DIAG
   unsigned long long d[D_NUM];
-  hipMemcpyFromSymbol(d, HIP_SYMBOL(g_diag), sizeof(d));
+  hipMemcpyFromSymbol(d, sym, sizeof(d));
   fprintf(stderr, "[diag %s] iters %llu lanes/iter %.2f  cycles/iter: step %.0f star %.0f ray %.0f sample %.0f loop %.0f  ray_overflow %llu\n",
           tag, d[D_ITERS], (double)d[D_LANES] / (double)(d[D_ITERS] ? d[D_ITERS] : 1),
           (double)d[D_STEP] / d[D_ITERS], (double)d[D_STAR] / d[D_ITERS], (double)d[D_RAY] / d[D_ITERS],
@@ -237,9 +240,10 @@ void diag_dump(const char* tag) {
   fprintf(stderr, "[diag %s] <=2 live lanes star detail: prologue %.0f  list build+sync %.0f  star total (in-function) %.0f\n", tag,
           d[D_L_S_PRE] / li, d[D_L_S_BUILD] / li, d[D_L_S_POST] / li);
   unsigned long long z[D_NUM] = {};
-  hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
+  hipMemcpyToSymbol(sym, z, sizeof(z));
 #else
   (void)tag;
+  (void)sym;
 #endif
 }
 

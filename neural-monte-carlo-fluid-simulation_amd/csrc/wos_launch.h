@@ -37,6 +37,8 @@ size_t walk_wave_lds_bytes(int dim);
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks,
                                    bool robust = false);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
+void diag_dump_bstart(const char* tag);  // ... of the boundary-start walk kernels (wos_bvc.hip)
+void diag_print(const char* tag, const void* sym);
 hipError_t launch_math_selftest(int which, const double* x, double* out, int64_t n, hipStream_t s);
 
 // boundary value caching (wos_bvc.hip), 2D

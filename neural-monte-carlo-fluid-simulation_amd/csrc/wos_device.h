@@ -435,6 +435,35 @@ __device__ __forceinline__ uint32_t wave_min_u32_solo(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Inclusive prefix sum over the wave: in-row shifts by 1, 2, 4, 8 (DPP row_shr, zero from
+// outside the row), then row 15's / row 31's sums broadcast into the following rows
+// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3) -- six VALU adds instead
+// of six ds_bpermute round trips (≈ 80 cycles each).  Needs the full exec mask (as the
+// cooperative queries have); otherwise the shuffle form.
+#ifndef WOS_DPP_SCAN
+#define WOS_DPP_SCAN 1
+#endif
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v, int lane) {
+  if (WOS_DPP_SCAN && __builtin_amdgcn_read_exec() == ~0ull) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+  }
+  for (int dlt = 1; dlt < kWave; dlt <<= 1) {
+    const uint32_t u = __shfl_up(v, dlt);
+    if (lane >= dlt) v += u;
+  }
+  return v;
+}
+// lane 63's value (the total of an inclusive sum), wave-uniform
+__device__ __forceinline__ uint32_t wave_last_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, kWave - 1);
+}
+
 // a lane's float value, wave-uniform
 __device__ __forceinline__ float lane_bcast(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -2470,12 +2499,8 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
       }
     }
     const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
+    const uint32_t incl = wave_incl_sum_u32(cnt, lane);
+    const uint32_t total = wave_last_u32(incl);
     uint32_t pos = incl - cnt;
     for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
     wave_sync();
@@ -2708,12 +2733,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     // of the LDS list: the wave pays for the sum of the list lengths / 64 instead of
     // the longest list; accepted candidates fold into the owner like the group scan
     const uint32_t cnt = use_cell ? (uint32_t)(c_end - c_beg) : 0u;
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
+    const uint32_t incl = wave_incl_sum_u32(cnt, lane);
+    const uint32_t total = wave_last_u32(incl);
     const uint32_t first = incl - cnt;
     DIAG_ADD_IF(D_L_S_PFX, t_s1, lone);
     DIAG_T0(t_s2);
@@ -2799,12 +2820,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
       }
     }
     const uint32_t cnt = (uint32_t)__popc(mask);
-    uint32_t incl = cnt;
-    for (int dlt = 1; dlt < kWave; dlt <<= 1) {
-      const uint32_t v = __shfl_up(incl, dlt);
-      if (lane >= dlt) incl += v;
-    }
-    const uint32_t total = __shfl(incl, kWave - 1);
+    const uint32_t incl = wave_incl_sum_u32(cnt, lane);
+    const uint32_t total = wave_last_u32(incl);
     uint32_t pos = incl - cnt;
     for (uint32_t m = mask; m; m &= m - 1) L->list[pos++] = ((uint32_t)lane << 26) | (uint32_t)(g0 + __builtin_ctz(m));
     wave_sync();
@@ -3725,9 +3742,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
             qdone |= 1u << x;  // exhausted: never drawn from again by this wave
           }
         }
-        c = __shfl(c, 0);
-        len = __shfl(len, 0);
-        qdone = (uint32_t)__shfl((int)qdone, 0);
+        c = (unsigned int)__builtin_amdgcn_readlane((int)c, 0);
+        len = (unsigned int)__builtin_amdgcn_readlane((int)len, 0);
+        qdone = (uint32_t)__builtin_amdgcn_readlane((int)qdone, 0);
         if (c == 0xFFFFFFFFu) { exhausted = true; break; }
         wq = c;
         we = (T - c) < len ? T : c + len;

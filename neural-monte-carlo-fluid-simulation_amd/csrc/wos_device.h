@@ -3792,8 +3792,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         const int k = __popcll(need);
         const int take = k < S ? k : S;
         const int src = (head + (rank < take ? rank : 0)) & (kWave - 1);
-        const uint32_t v_t = (uint32_t)__shfl((int)s_t, src);
-        const uint32_t v_ok = (uint32_t)__shfl((int)s_ok, src);
+        // the staged task index with its point's estimate bit on top (tasks < 2^31): one shuffle
+        const uint32_t v_pk = (uint32_t)__shfl((int)(s_t | (s_ok ? 0x80000000u : 0u)), src);
+        const uint32_t v_t = v_pk & 0x7FFFFFFFu;
+        const uint32_t v_ok = v_pk >> 31;
         float v_pt[DIM], v_thr = 0.0f, v_tsrc = 0.0f, v_dd = 0.0f;
         if (t < 0 && rank < take && v_ok) {  // the task record from memory, at hand-out
           for (int kk = 0; kk < DIM; kk++) v_pt[kk] = tk.pt[kk * tk.T + v_t];

@@ -143,6 +143,7 @@ typedef struct wos_solver_params {
 #define WOS_SCHED_FULL_NEUMANN  0x2u  /* keep the walk kernel's Neumann term even when it is provably +0 */
 #define WOS_SCHED_NO_STAR_GRID  0x4u  /* no star-radius cell grid: the cooperative group scan alone */
 #define WOS_SCHED_NO_DIR_GRID   0x8u  /* no Dirichlet-distance cell grid (2D): the culled scans alone */
+#define WOS_SCHED_NO_TAIL_SPREAD 0x10u /* no hand-over of walks to idle sibling waves once the queue is dry */
 
 void wos_default_params(wos_solver_params *p);
 

@@ -3657,6 +3657,76 @@ constexpr unsigned int kTaskHead = WOS_TASK_HEAD;           // head windows per 
 static_assert((kTaskQueues & (kTaskQueues - 1)) == 0 && kTaskQueues <= (unsigned)kMaxTaskQueues, "power of two");
 
 
+// ---- tail spreading inside a workgroup ------------------------------------------
+// Once the walk queue is dry, a wave whose walks have all ended would leave its SIMD
+// idle while a sibling wave of the same workgroup still carries many walks, each of
+// its iterations paying for all of them.  Instead the idle wave announces itself
+// (s_idle), and a sibling with >= 2 live walks hands it the upper half of them: the
+// whole per-lane walk state, word for word, through the idle wave's LDS scratch (which
+// it is not using) -- the walks continue bit for bit on another SIMD.  s_busy counts
+// the waves holding walks (a donor counts its recipient before handing over), so an
+// idle wave leaves once it reaches 0: no walk is left anywhere in the workgroup and
+// none can appear (the queue is dry).
+// The kernels with SPR = true hand over (2D, LDS geometry; chosen per solve,
+// DevParams::tail_spread): the extra live state costs the throughput path scratch, so
+// scenes whose walks are short (absorbing Dirichlet boundaries) and 3D keep SPR = false.
+// WOS_TAIL_SPREAD=2 (A/B builds only) turns it on in every instantiation.
+#ifndef WOS_TAIL_SPREAD
+#define WOS_TAIL_SPREAD 0
+#endif
+constexpr int kSpreadMax = 32;  // walks per hand-over
+// words of one walk's state: WalkState, Gfn, the PCG32 state, ddist, firstR, wsteps, task
+template <int DIM>
+constexpr int walk_pack_words() { return (3 * DIM + 6 + (WOS_DEFER_TEXEL ? 4 : 0)) + (1 + 3 * DIM + 9) + 2 + 4; }
+// every member is moved (the struct sizes, bools padded to a word, match the counts)
+static_assert(sizeof(WalkState<2>) == 4 * (3 * 2 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<2> members");
+static_assert(sizeof(WalkState<3>) == 4 * (3 * 3 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<3> members");
+static_assert(sizeof(Gfn<2, false>) == 4 * (1 + 3 * 2 + 9) && sizeof(Gfn<3, true>) == 4 * (1 + 3 * 3 + 9), "Gfn members");
+static_assert(sizeof(Pcg32) == 8, "Pcg32 state");
+// one walk's state into / out of mailbox slot `slot` (word-major, kSpreadMax slots per word)
+template <int DIM, bool RB>
+__device__ __forceinline__ void spread_put(uint32_t* mb, int slot, const WalkState<DIM>& st, const Gfn<DIM, RB>& g,
+                                           const Pcg32& ws, float ddist, float firstR, uint32_t wsteps, uint32_t t) {
+  int q = 0;
+  auto put = [&](uint32_t v) { mb[(q++) * kSpreadMax + slot] = v; };
+  auto putf = [&](float v) { put(__float_as_uint(v)); };
+  for (int k = 0; k < DIM; k++) { putf(st.pt[k]); putf(st.n[k]); putf(st.prevDir[k]); }
+  putf(st.prevDist); putf(st.throughput); put(st.onNeumann ? 1u : 0u); put((uint32_t)st.walkLength);
+  putf(st.totalNeumann); putf(st.totalSource);
+#if WOS_DEFER_TEXEL
+  putf(st.pThr); putf(st.pNrm); putf(st.pTex); put(st.pend ? 1u : 0u);
+#endif
+  put((uint32_t)g.yukawa);
+  for (int k = 0; k < DIM; k++) { putf(g.c[k]); putf(g.yVol[k]); putf(g.ySurf[k]); }
+  putf(g.R); putf(g.r); putf(g.lambda); putf(g.sqrtLambda); putf(g.muR); putf(g.A0); putf(g.A1); putf(g.B0); putf(g.B1);
+  put((uint32_t)ws.state); put((uint32_t)(ws.state >> 32));
+  putf(ddist); putf(firstR); put(wsteps); put(t);
+}
+template <int DIM, bool RB>
+__device__ __forceinline__ void spread_get(const uint32_t* mb, int slot, WalkState<DIM>& st, Gfn<DIM, RB>& g,
+                                           Pcg32& ws, float& ddist, float& firstR, uint32_t& wsteps, int64_t& t) {
+  int q = 0;
+  auto get = [&]() { return mb[(q++) * kSpreadMax + slot]; };
+  auto getf = [&]() { return __uint_as_float(get()); };
+  for (int k = 0; k < DIM; k++) { st.pt[k] = getf(); st.n[k] = getf(); st.prevDir[k] = getf(); }
+  st.prevDist = getf(); st.throughput = getf(); st.onNeumann = get() != 0u; st.walkLength = (int)get();
+  st.totalNeumann = getf(); st.totalSource = getf();
+#if WOS_DEFER_TEXEL
+  st.pThr = getf(); st.pNrm = getf(); st.pTex = getf(); st.pend = get() != 0u;
+#endif
+  g.yukawa = (int)get();
+  for (int k = 0; k < DIM; k++) { g.c[k] = getf(); g.yVol[k] = getf(); g.ySurf[k] = getf(); }
+  g.R = getf(); g.r = getf(); g.lambda = getf(); g.sqrtLambda = getf(); g.muR = getf();
+  g.A0 = getf(); g.A1 = getf(); g.B0 = getf(); g.B1 = getf();
+  const uint32_t lo = get(), hi = get();
+  ws.state = ((uint64_t)hi << 32) | lo;
+  ddist = getf(); firstR = getf(); wsteps = get(); t = (int64_t)get();
+}
+struct SpreadLDS {
+  uint32_t busy, idle;
+  uint32_t mbox[kBlock / kWave];
+};
+
 #ifndef WOS_WALK_WAVES_PER_EU
 #define WOS_WALK_WAVES_PER_EU 4
 #endif
@@ -3666,15 +3736,18 @@ static_assert((kTaskQueues & (kTaskQueues - 1)) == 0 && kTaskQueues <= (unsigned
 // BSTART: the tasks are boundary-start walks (estimateSolution, walk_on_stars.h:353-464:
 // start normal, first sphere radius, on-Neumann flag from DevTasks::n0/r0/sflags, no
 // first ball, walk stream tag 6) -- boundary value caching (wos_bvc.hip).
-template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool NEU = true>
+template <int DIM, bool GG, bool BSTART = false, bool RB = false, bool NEU = true, bool SPR = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2 ? WOS_WALK_WAVES_PER_EU : WOS_WALK_WAVES_PER_EU3))) void wos_walk_kernel(
     const DevScene sc_arg, const DevParams prm_arg, const DevTasks tk_arg, int64_t base, int64_t stride,
     unsigned long long* __restrict__ counters, unsigned int* __restrict__ tqueue, int geom_floats) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ unsigned int s_ctr[C_NUM];
+  __shared__ SpreadLDS s_spread;
   const DevScene& sc = sc_arg;
   const DevParams& prm = prm_arg;
   const DevTasks& tk = tk_arg;
+  static_assert(walk_pack_words<DIM>() * kSpreadMax * 4 <= (int)walk_scratch_bytes<DIM>(), "mailbox fits the scratch");
+  constexpr bool kSpread = SPR || WOS_TAIL_SPREAD == 2;
   const int lane = threadIdx.x & (kWave - 1);
   stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
@@ -3685,6 +3758,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   RayLDS<DIM>* rayL = reinterpret_cast<RayLDS<DIM>*>(wscratch);
   RejLDS* rejL = reinterpret_cast<RejLDS*>(wscratch);
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) { s_spread.busy = blockDim.x / kWave; s_spread.idle = 0u; }
+  if (threadIdx.x < kBlock / kWave) s_spread.mbox[threadIdx.x] = 0u;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -3823,7 +3898,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       }
     }
     if (__ballot(t >= 0) == 0) {
-      if (S == 0 && exhausted) break;  // queue drained and every lane idle
+      if (S == 0 && exhausted) {  // queue drained and every lane idle
+        if (!kSpread) break;
+        // idle: announce, then take a sibling's hand-over or leave once no wave holds walks
+        if (lane == 0) {
+          __hip_atomic_fetch_or(&s_spread.idle, 1u << wave_u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_sub(&s_spread.busy, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        uint32_t n = 0;
+        for (;;) {
+          n = __hip_atomic_load(&s_spread.mbox[wave_u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+          if (n != 0u) break;
+          const uint32_t busy = (uint32_t)__builtin_amdgcn_readfirstlane(
+              (int)__hip_atomic_load(&s_spread.busy, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if (busy == 0u) break;
+          __builtin_amdgcn_s_sleep(4);
+        }
+        if (n == 0u) break;
+        // the hand-over: slot i of the mailbox (word-major, kSpreadMax slots) -> lane i
+        const uint32_t* mb = reinterpret_cast<const uint32_t*>(wscratch);
+        if ((uint32_t)lane < n) spread_get<DIM, RB>(mb, lane, st, g, ws, ddist, firstR, wsteps, t);
+        wave_sync();
+        if (lane == 0) __hip_atomic_store(&s_spread.mbox[wave_u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        continue;
+      }
       refill(tk);
       continue;
     }
@@ -3838,6 +3937,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;
+    }
+    if (kSpread && exhausted && S == 0) {
+      const uint64_t live = __ballot(t >= 0);
+      const int k = __popcll(live);
+      if (k >= 2 && __builtin_amdgcn_readfirstlane(
+                        (int)__hip_atomic_load(&s_spread.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0) {
+        int to = -1;
+        if (lane == 0) {
+          uint32_t m = __hip_atomic_load(&s_spread.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          while (m != 0u) {
+            const uint32_t b = 1u << __builtin_ctz(m);
+            const uint32_t old =
+                __hip_atomic_fetch_and(&s_spread.idle, ~b, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (old & b) {
+              // the recipient holds walks from here on: counted before it can see them
+              __hip_atomic_fetch_add(&s_spread.busy, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              to = __builtin_ctz(b);
+              break;
+            }
+            m = old & ~b;
+          }
+        }
+        to = __builtin_amdgcn_readlane(to, 0);
+        if (to >= 0) {
+          // the upper half of the live walks (by lane rank), at most kSpreadMax
+          const int kd = (k / 2) < kSpreadMax ? (k / 2) : kSpreadMax;
+          const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+          const bool give = t >= 0 && rank >= k - kd;
+          uint32_t* mb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem + geom_floats) +
+                                                     to * walk_scratch_bytes<DIM>());
+          if (give) {
+            spread_put<DIM, RB>(mb, rank - (k - kd), st, g, ws, ddist, firstR, wsteps, (uint32_t)t);
+            t = -1;
+          }
+          wave_sync();
+          if (lane == 0)
+            __hip_atomic_store(&s_spread.mbox[to], (uint32_t)kd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
     }
     refill(tk);
 #if WOS_DIAG

@@ -56,6 +56,13 @@ template __global__ void wos_point_setup_kernel<3>(const DevScene, const DevPara
                                                                       unsigned long long*, unsigned int*, int)
 WOS_WALK(2, false);
 WOS_WALK(2, true);
+// 2D, LDS geometry, the tail-spreading instantiations (DevParams::tail_spread)
+template __global__ void wos_walk_kernel<2, false, false, false, true, true>(const DevScene, const DevParams,
+                                                                            const DevTasks, int64_t, int64_t,
+                                                                            unsigned long long*, unsigned int*, int);
+template __global__ void wos_walk_kernel<2, false, false, false, false, true>(const DevScene, const DevParams,
+                                                                             const DevTasks, int64_t, int64_t,
+                                                                             unsigned long long*, unsigned int*, int);
 WOS_WALK(3, false);
 WOS_WALK(3, true);
 #undef WOS_WALK
@@ -161,7 +168,18 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
                          counters, tqueue, geom_floats);                                                         \
   } while (0)
   if (dim == 2) {
-    if (sc.geom_global) WOS_LAUNCH_WALK(2, true); else WOS_LAUNCH_WALK(2, false);
+    if (sc.geom_global) {
+      WOS_LAUNCH_WALK(2, true);
+    } else if (prm.tail_spread) {
+      if (prm.neumann_inert)
+        hipLaunchKernelGGL((wos_walk_kernel<2, false, false, false, false, true>), dim3(grid), dim3(kBlock), shmem, s,
+                           sc, prm, tk, base, stride, counters, tqueue, geom_floats);
+      else
+        hipLaunchKernelGGL((wos_walk_kernel<2, false, false, false, true, true>), dim3(grid), dim3(kBlock), shmem, s,
+                           sc, prm, tk, base, stride, counters, tqueue, geom_floats);
+    } else {
+      WOS_LAUNCH_WALK(2, false);
+    }
   } else {
     if (sc.geom_global) WOS_LAUNCH_WALK(3, true); else WOS_LAUNCH_WALK(3, false);
   }

@@ -123,6 +123,7 @@ struct DevParams {
   int32_t neumann_inert;    // 1: no ball can reach the float-overflow regime (walk kernel without the Neumann term)
   int32_t force_estimate;   // 1: estimate every point, inside the domain or not (BVC's Dirichlet samples:
                             // BoundarySampler::computeEstimates solves at every sample, boundary_sampler.h:125-166)
+  int32_t tail_spread;      // 1: the walk kernel instantiation that hands walks to idle sibling waves
   int32_t wave_prio;        // 0..3: the walk / fold kernels' waves issue at this priority (s_setprio) --
                             // boundary value caching's concurrent walk sets, longest chain highest
   uint64_t seed;

@@ -68,6 +68,7 @@ SCHED_GEOM_GLOBAL = 0x1
 SCHED_FULL_NEUMANN = 0x2
 SCHED_NO_STAR_GRID = 0x4
 SCHED_NO_DIR_GRID = 0x8
+SCHED_NO_TAIL_SPREAD = 0x10
 
 
 class BvcParams(C.Structure):

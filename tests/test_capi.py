@@ -90,3 +90,14 @@ def test_scene_create_without_gpu_reports_device_error():
     v, ix = objparse.load(workloads.KARMAN_OBJ, 2)
     with pytest.raises(wos_amd.WosError, match="no HIP device"):
         wos_amd.WosScene(v, ix, np.zeros((4, 4), np.float32), 350.0)
+
+
+def test_schedule_bits_match_header():
+    # wos_solver_params.schedule bits: include/wos.h WOS_SCHED_* == wos_amd._lib SCHED_*
+    txt = open(HEADER).read()
+    bits = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define WOS_(SCHED_\w+)\s+0x([0-9a-fA-F]+)u", txt)}
+    assert set(bits) == {"SCHED_GEOM_GLOBAL", "SCHED_FULL_NEUMANN", "SCHED_NO_STAR_GRID", "SCHED_NO_DIR_GRID",
+                         "SCHED_NO_TAIL_SPREAD"}
+    for name, v in bits.items():
+        assert getattr(_lib, name) == v, name
+    assert len(set(bits.values())) == len(bits) and all(v & (v - 1) == 0 for v in bits.values())

@@ -983,11 +983,10 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
                         !(prm->schedule & WOS_SCHED_FULL_NEUMANN)) ? 1 : 0;
   }
   // Walks handed to idle sibling waves once the queue is dry (the walk kernel's SPR
-  // instantiation): 2D scenes without Dirichlet geometry, whose reflecting walks leave long
-  // tails (karman -4 %, its stride-8 shard -9 %); absorbing Dirichlet scenes (short walks)
-  // and 3D pay more for the extra live state than the tails return (profiles/r4zb_*)
-  dp.tail_spread = (dim == 2 && host.n_dprims == 0 && !dp.robust && !dsc.geom_global &&
-                    !(prm->schedule & WOS_SCHED_NO_TAIL_SPREAD)) ? 1 : 0;
+  // instantiation): 2D scenes with LDS geometry (karman -4 %, its stride-8 shard -13 %,
+  // config C neutral); 3D pays more for the extra live state than its short tails return
+  // (profiles/r4zc_*, r4ze_*)
+  dp.tail_spread = (dim == 2 && !dp.robust && !dsc.geom_global && !(prm->schedule & WOS_SCHED_NO_TAIL_SPREAD)) ? 1 : 0;
   const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
   const int64_t n_chunks = n > 0 ? (n + chunk - 1) / chunk : 0;
   int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;

@@ -3668,16 +3668,19 @@ static_assert((kTaskQueues & (kTaskQueues - 1)) == 0 && kTaskQueues <= (unsigned
 // idle wave leaves once it reaches 0: no walk is left anywhere in the workgroup and
 // none can appear (the queue is dry).
 // The kernels with SPR = true hand over (2D, LDS geometry; chosen per solve,
-// DevParams::tail_spread): the extra live state costs the throughput path scratch, so
-// scenes whose walks are short (absorbing Dirichlet boundaries) and 3D keep SPR = false.
+// DevParams::tail_spread); 3D keeps SPR = false (its extra live state costs the throughput
+// path scratch that its short tails do not return).  Only the loop-carried state moves.
 // WOS_TAIL_SPREAD=2 (A/B builds only) turns it on in every instantiation.
 #ifndef WOS_TAIL_SPREAD
 #define WOS_TAIL_SPREAD 0
 #endif
 constexpr int kSpreadMax = 32;  // walks per hand-over
-// words of one walk's state: WalkState, Gfn, the PCG32 state, ddist, firstR, wsteps, task
+// words of one walk's state between two steps: WalkState, the Green's function's kind and
+// absorption (its ball -- c, R, r, y*, muR and the Bessel members -- is rebuilt by update_ball
+// before any use in the next step, so it is not loop-carried and not moved), the PCG32 state,
+// ddist, wsteps, task
 template <int DIM>
-constexpr int walk_pack_words() { return (3 * DIM + 6 + (WOS_DEFER_TEXEL ? 4 : 0)) + (1 + 3 * DIM + 9) + 2 + 4; }
+constexpr int walk_pack_words() { return (3 * DIM + 6 + (WOS_DEFER_TEXEL ? 4 : 0)) + 3 + 2 + 3; }
 // every member is moved (the struct sizes, bools padded to a word, match the counts)
 static_assert(sizeof(WalkState<2>) == 4 * (3 * 2 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<2> members");
 static_assert(sizeof(WalkState<3>) == 4 * (3 * 3 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<3> members");
@@ -3696,11 +3699,10 @@ __device__ __forceinline__ void spread_put(uint32_t* mb, int slot, const WalkSta
 #if WOS_DEFER_TEXEL
   putf(st.pThr); putf(st.pNrm); putf(st.pTex); put(st.pend ? 1u : 0u);
 #endif
-  put((uint32_t)g.yukawa);
-  for (int k = 0; k < DIM; k++) { putf(g.c[k]); putf(g.yVol[k]); putf(g.ySurf[k]); }
-  putf(g.R); putf(g.r); putf(g.lambda); putf(g.sqrtLambda); putf(g.muR); putf(g.A0); putf(g.A1); putf(g.B0); putf(g.B1);
+  put((uint32_t)g.yukawa); putf(g.lambda); putf(g.sqrtLambda);
   put((uint32_t)ws.state); put((uint32_t)(ws.state >> 32));
-  putf(ddist); putf(firstR); put(wsteps); put(t);
+  (void)firstR;  // 0 after every step (a boundary-start walk's first-sphere radius is used once)
+  putf(ddist); put(wsteps); put(t);
 }
 template <int DIM, bool RB>
 __device__ __forceinline__ void spread_get(const uint32_t* mb, int slot, WalkState<DIM>& st, Gfn<DIM, RB>& g,
@@ -3714,13 +3716,10 @@ __device__ __forceinline__ void spread_get(const uint32_t* mb, int slot, WalkSta
 #if WOS_DEFER_TEXEL
   st.pThr = getf(); st.pNrm = getf(); st.pTex = getf(); st.pend = get() != 0u;
 #endif
-  g.yukawa = (int)get();
-  for (int k = 0; k < DIM; k++) { g.c[k] = getf(); g.yVol[k] = getf(); g.ySurf[k] = getf(); }
-  g.R = getf(); g.r = getf(); g.lambda = getf(); g.sqrtLambda = getf(); g.muR = getf();
-  g.A0 = getf(); g.A1 = getf(); g.B0 = getf(); g.B1 = getf();
+  g.yukawa = (int)get(); g.lambda = getf(); g.sqrtLambda = getf();
   const uint32_t lo = get(), hi = get();
   ws.state = ((uint64_t)hi << 32) | lo;
-  ddist = getf(); firstR = getf(); wsteps = get(); t = (int64_t)get();
+  ddist = getf(); firstR = 0.0f; wsteps = get(); t = (int64_t)get();
 }
 struct SpreadLDS {
   uint32_t busy, idle;

@@ -38,6 +38,7 @@ PKG = os.path.join(REPO, "neural-monte-carlo-fluid-simulation_amd")
 sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
+from wos_amd import dist as wdist  # noqa: E402  (pure Python: no library load at import)
 
 # MI355X_MICROARCH.md chip table (spec, dense)
 HBM_PEAK_GBS = 8000.0
@@ -186,27 +187,6 @@ def cpu_baseline(cfg, n_threads, budget_s):
     }
 
 
-def make_gather(world, dist, n_local, n_pad, dim, dev, torch):
-    """The one all-gather of [p, grad] per projection: every rank sends its shard
-    padded to n_pad rows into a (world * n_pad, 1 + dim) buffer.  With the gloo
-    backend (CPU-only rehearsal of the N-rank path, tests/test_bench_dist.py) the
-    payload is staged through host memory; with nccl (RCCL) it stays in HBM."""
-    if world == 1:
-        return None
-    staged = dist.get_backend() == "gloo" and dev.type != "cpu"
-    bdev = torch.device("cpu") if staged else dev
-    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=bdev)
-    buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=bdev)
-
-    def gather(p, g):
-        send[:n_local, 0] = p.to(bdev)
-        send[:n_local, 1:] = g.to(bdev)
-        dist.all_gather_into_tensor(buf, send)
-
-    gather.buf = buf
-    return gather
-
-
 def timed_projections(scene, x, params, base, stride, steps, warmup, blocking, world, dist, torch, gather=None):
     """Time `steps` projections of the points `x` (global indices base + i * stride),
     each followed by `gather(p, grad)` (the RCCL all-gather for N > 1), bracketed by a
@@ -265,7 +245,7 @@ def strong_projection(a, scene, params, world, rank, dim, dist, torch, dev, work
     n_local = local.shape[0]
     n_pad = (n_all + world - 1) // world
     x = torch.from_numpy(local).to(dev)
-    gather = make_gather(world, dist, n_local, n_pad, dim, dev, torch)
+    gather = wdist.make_gather(world, dist, n_local, n_pad, dim, dev, torch)
 
     elapsed, stats = timed_projections(scene, x, params, rank, world, a.steps, a.warmup, a.blocking,
                                        world, dist, torch, gather)
@@ -323,7 +303,7 @@ def main():
     n_local = local.shape[0]
     n_pad = (n_all + world - 1) // world
     x = torch.from_numpy(local).to(dev)
-    gather = make_gather(world, dist, n_local, n_pad, dim, dev, torch)
+    gather = wdist.make_gather(world, dist, n_local, n_pad, dim, dev, torch)
 
     elapsed, stats = timed_projections(scene, x, params, rank, world, a.steps, a.warmup, a.blocking,
                                        world, dist, torch, gather)

@@ -329,9 +329,9 @@ __global__ __launch_bounds__(kSplatPts * kSplatWaves) void wos_bvc_splat_kernel(
   if ((int64_t)blockIdx.x * kSplatPts >= nl) return;  // block-uniform
   const int lane = threadIdx.x & (kSplatPts - 1);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kSplatPts));
-  const int64_t j = (int64_t)blockIdx.x * kSplatPts + lane;  // list slot
-  const bool valid = j < nl;
-  const int64_t i = valid ? (int64_t)list[j] : 0;
+  const int64_t slot = (int64_t)blockIdx.x * kSplatPts + lane;  // list slot
+  const bool valid = slot < nl;
+  const int64_t i = valid ? (int64_t)list[slot] : 0;
   FreeSpace2 gf;
   gf.yukawa = absorption > 0.0f;
   gf.lambda = absorption;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kSplatPts * kSplatWaves) void wos_bvc_splat_kernel(
   // this wave's component of the three classes' statistics and their counts
   float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f;
   int n0 = 0, n1 = 0, n2 = 0;
-  float* sw = state + (size_t)(wave < 3 ? wave : 0) * 6 * ne + j;  // this wave's component, by slot
+  float* sw = state + (size_t)(wave < 3 ? wave : 0) * 6 * ne + slot;  // this wave's component, by slot
   if (!first && valid && wave < 3) {
     m0 = sw[0]; m1 = sw[ne]; m2 = sw[2 * ne];
     n0 = __float_as_int(sw[3 * ne]); n1 = __float_as_int(sw[4 * ne]); n2 = __float_as_int(sw[5 * ne]);

@@ -13,6 +13,9 @@
 #include "wos_bvc.h"
 
 #include <cmath>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
 
 #include "wos_detmath.h"
 
@@ -76,8 +79,10 @@ struct Seg {
 
 // The sampler's boundary (boundary_sampler.h:87-412): the Neumann segments, then the Dirichlet
 // ones, whose vertices carry the sampler's own normals (computeNormals :193-236: unit segment
-// normals summed per vertex, normalised; per part -- a vertex shared with a Neumann segment
-// keeps its Dirichlet normal).
+// normals summed per vertex, normalised).  The reference runs it over the scene's ONE mesh
+// (demo.cpp:316 passes scene.vertices / scene.segments), so a vertex shared by a Neumann and a
+// Dirichlet segment sums both segments' normals; here the two parts arrive as separate meshes,
+// and a Dirichlet vertex is welded to every Neumann segment end at the same position.
 struct Boundary {
   const float *v, *dv;
   const int32_t *ix, *dix;
@@ -110,16 +115,50 @@ struct Boundary {
   }
 };
 
+// unit normal of segment (pa, pb) (lineSegmentNormal<2>(pa, pb, true): Eigen normalized())
+void unit_normal(const Seg& g, float* n) {
+  const float s0 = g.pb[0] - g.pa[0], s1 = g.pb[1] - g.pa[1];
+  n[0] = s1;
+  n[1] = -s0;
+  const float z = n[0] * n[0] + n[1] * n[1];
+  if (z > 0.0f) { const float r = std::sqrt(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+}
+
+// position key of a vertex (+0 and -0 compare equal, as the float comparison does)
+uint64_t pos_key(const float* p) {
+  uint32_t a, b;
+  const float x = p[0] + 0.0f, y = p[1] + 0.0f;
+  std::memcpy(&a, &x, 4);
+  std::memcpy(&b, &y, 4);
+  return ((uint64_t)a << 32) | b;
+}
+
 void dirichlet_normals(Boundary& B, int ndv) {
   B.dn.assign((size_t)2 * ndv, 0.0f);
+  // Dirichlet segments first, then the Neumann segment ends welded onto Dirichlet vertices: a
+  // junction vertex has one segment of each kind, and a sum of two terms does not depend on
+  // their order, so this equals the reference's one-mesh order (a vertex where three or more
+  // segments meet could differ in the last bit)
   for (int p = 0; p < B.ndp; p++) {
-    const Seg g = B.raw(B.np + p);
-    const float s0 = g.pb[0] - g.pa[0], s1 = g.pb[1] - g.pa[1];
-    float n[2] = {s1, -s0};
-    const float z = n[0] * n[0] + n[1] * n[1];
-    if (z > 0.0f) { const float r = std::sqrt(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+    float n[2];
+    unit_normal(B.raw(B.np + p), n);
     for (int q = 0; q < 2; q++)
       for (int k = 0; k < 2; k++) B.dn[2 * B.dix[2 * p + q] + k] += n[k];
+  }
+  if (B.np > 0 && B.ndp > 0) {
+    std::unordered_map<uint64_t, std::vector<int>> at;
+    for (int i = 0; i < ndv; i++) at[pos_key(B.dv + 2 * i)].push_back(i);
+    for (int p = 0; p < B.np; p++) {
+      const Seg g = B.raw(p);
+      float n[2];
+      unit_normal(g, n);
+      for (const float* e : {g.pa, g.pb}) {
+        const auto it = at.find(pos_key(e));
+        if (it == at.end()) continue;
+        for (const int i : it->second)
+          for (int k = 0; k < 2; k++) B.dn[2 * i + k] += n[k];
+      }
+    }
   }
   for (int i = 0; i < ndv; i++) {
     const float z = B.dn[2 * i] * B.dn[2 * i] + B.dn[2 * i + 1] * B.dn[2 * i + 1];

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <list>
 #include <cstdlib>
 #include <cstring>
@@ -51,8 +52,13 @@ hipError_t upload(T** dst, const std::vector<T>& src) {
   *dst = nullptr;
   if (src.empty()) return hipSuccess;
   hipError_t e = hipMalloc((void**)dst, src.size() * sizeof(T));
-  if (e != hipSuccess) return e;
-  return hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { *dst = nullptr; return e; }
+  e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {  // no half-initialised buffer is ever handed out
+    hipFree(*dst);
+    *dst = nullptr;
+  }
+  return e;
 }
 
 // ---- per-device solve workspace ---------------------------------------------
@@ -308,10 +314,11 @@ int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
   for (const Geom::Grid& x : g.grids)
     if (x.prec == prec && x.min_r == min_r) { *out = &x; return WOS_OK; }
   Geom::Grid x{prec, min_r, false, {}, nullptr};
-  x.ok = wos::build_star_grid(g.host, prec, min_r, kStarGridBudget, x.grid);
-  if (x.ok) {
-    HIP_TRY(hipMalloc((void**)&x.d, x.grid.words.size() * sizeof(uint32_t)));
-    HIP_TRY(hipMemcpy(x.d, x.grid.words.data(), x.grid.words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  // cached (ok or not) only once its upload has succeeded: a failed upload is reported and
+  // the next solve builds the grid again
+  if (wos::build_star_grid(g.host, prec, min_r, kStarGridBudget, x.grid)) {
+    HIP_TRY(upload(&x.d, x.grid.words));
+    x.ok = true;
   }
   g.grids.push_back(std::move(x));
   *out = &g.grids.back();
@@ -321,13 +328,12 @@ int star_grid(Geom& g, float prec, float min_r, const Geom::Grid** out) {
 int dir_grid(Geom& g, bool* ok) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.dgrid_built) {
+    // built / ok only once the upload has succeeded (upload leaves d_dgrid null on failure),
+    // so no later solve reads a half-initialised grid
+    const bool have = wos::build_dirichlet_grid(g.host, g.dgrid);
+    if (have) HIP_TRY(upload(&g.d_dgrid, g.dgrid.words));
+    g.dgrid_ok = have;
     g.dgrid_built = true;
-    g.dgrid_ok = wos::build_dirichlet_grid(g.host, g.dgrid);
-    if (g.dgrid_ok) {
-      HIP_TRY(hipMalloc((void**)&g.d_dgrid, g.dgrid.words.size() * sizeof(uint32_t)));
-      HIP_TRY(hipMemcpy(g.d_dgrid, g.dgrid.words.data(), g.dgrid.words.size() * sizeof(uint32_t),
-                        hipMemcpyHostToDevice));
-    }
   }
   *ok = g.dgrid_ok;
   return WOS_OK;
@@ -924,7 +930,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   size_t shmem_walk = wl.shmem_walk;
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   // the first-ball kernel stages no geometry (the point-setup kernel did the queries)
-  const size_t shmem_fb = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats);
+  const size_t shmem_fb = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats, dp.n_pairs);
   // scenes beyond the LDS budget (or WOS_SCHED_GEOM_GLOBAL): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
@@ -994,9 +1000,11 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     int rc = ensure_tasks(c, dim, chunk * wpp, chunk);
     if (rc != WOS_OK) return rc;
     HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, false, shmem_fb, &bpc_fb, dp.robust != 0));
-    grid_fb = (int)std::min<int64_t>((chunk + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
+    const int64_t fb_waves = (chunk + wos::first_ball_points_per_wave(dp.n_pairs) - 1) / wos::first_ball_points_per_wave(dp.n_pairs);
+    grid_fb = (int)std::min<int64_t>((fb_waves + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
-    HIP_TRY(wos::occupancy_blocks_per_cu(1, dim, dsc.geom_global != 0, shmem_walk, &bpc_walk, dp.robust != 0));
+    // the walk instantiation launch_walks will dispatch (tail spreading has its own LDS and state)
+    HIP_TRY(wos::occupancy_walk_blocks_per_cu(dim, dsc.geom_global != 0, dp, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
   const uint64_t ticket = c.next_ticket++;
@@ -1132,7 +1140,15 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (bp->n_walks_solution < 1) return fail(WOS_E_INVALID, "wos_bvc: nWalksForCachedSolutionEstimates must be >= 1");
   if (bp->boundary_cache_size < 0 || bp->domain_cache_size < 0) return fail(WOS_E_INVALID, "wos_bvc: negative cache size");
   if (prm->max_walk_length < 0) return fail(WOS_E_INVALID, "wos_bvc: maxWalkLength must be >= 0");
-  if (bp->grid_box[2] < 0.0f || bp->grid_box[3] < 0.0f) return fail(WOS_E_INVALID, "wos_bvc: negative grid_box extent");
+  {
+    // both extents 0: the scene's bounding box; else both finite and > 0 (and a finite corner)
+    const float* gb = bp->grid_box;
+    const bool unset = gb[2] == 0.0f && gb[3] == 0.0f;
+    const bool valid = std::isfinite(gb[0]) && std::isfinite(gb[1]) && std::isfinite(gb[2]) && std::isfinite(gb[3]) &&
+                       gb[2] > 0.0f && gb[3] > 0.0f;
+    if (!unset && !valid)
+      return fail(WOS_E_INVALID, "wos_bvc: grid_box needs both extents 0 (the scene's box) or both finite and > 0");
+  }
   std::lock_guard<std::mutex> lock(s->mu);
   Geom& geom = *s->geom;
   const wos::HostScene& host = geom.host;

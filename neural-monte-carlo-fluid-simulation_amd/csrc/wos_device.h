@@ -2963,6 +2963,24 @@ __host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
   return ((a > b ? a : b) + 15) & ~size_t(15);
 }
 
+// Query points per first-ball wave.  One lane runs one antithetic pair, so a point
+// with n_pairs <= 32 (64 walks or fewer: config D's 64 walks are 32 pairs) would leave
+// lanes n_pairs..63 out of the per-pair arithmetic; the wave takes
+// min(64 / n_pairs, kFbMaxPack) consecutive points of the queue instead, lane l
+// running pair l % n_pairs of point slot l / n_pairs.  Each point's stratified
+// samples are built in turn into its own LDS slot; seeds stay keyed by the global
+// point index, so results do not depend on the packing.  The cap bounds the
+// sequential stratified-sample builds per wave for tiny n_pairs.
+#ifndef WOS_FB_PACK
+#define WOS_FB_PACK 1
+#endif
+constexpr int kFbMaxPack = 4;
+__host__ __device__ constexpr int fb_points_per_wave(int n_pairs) {
+  return (WOS_FB_PACK && n_pairs > 0 && 2 * n_pairs <= kWave)
+             ? (kWave / n_pairs < kFbMaxPack ? kWave / n_pairs : kFbMaxPack)
+             : 1;
+}
+
 template <int DIM>
 __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
                                           char* scratch, int lane) {
@@ -3432,75 +3450,112 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
-  float* strat = smem + wave * (2 * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
-  int* partner = (int*)(strat + lhs_floats);
-  RejLDS* rejL = reinterpret_cast<RejLDS*>(strat + 2 * lhs_floats);
+  const int npairs = prm.n_pairs;
+  // P points per wave (fb_points_per_wave): slot s holds its stratified samples and
+  // shuffle partners at wbase + 2 s lhs_floats; the rejection sampler's / shuffle's
+  // scratch follows the P slots
+  const int P = fb_points_per_wave(npairs);
+  float* wbase = smem + wave * (2 * P * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
+  RejLDS* rejL = reinterpret_cast<RejLDS*>(wbase + 2 * P * lhs_floats);
+  // this lane's point slot and pair (P == 1: all lanes serve the one point, pairs w0 + lane);
+  // span = lanes per slot, so lane s * span is slot s's first lane (wave-uniform)
+  const int span = P > 1 ? npairs : kWave;
+  const int slot = P > 1 ? lane / npairs : 0;
+  const int wl = lane - slot * span;
+  const bool used = slot < P;
+  const int myslot = used ? slot : 0;
 
   uint32_t c_iters = 0, c_pts = 0;
-  const int npairs = prm.n_pairs;
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
 
-  // point queue, one point ahead: the next index is taken (and its coordinates,
-  // radius and state loaded) while the current point is processed, so neither the
-  // queue atomic nor the point loads sit on a point's critical path.  Points are
-  // taken kPtGrab at a time (one queue atomic per chunk: a single-address atomic per
-  // point serialises at ~13 ns, which had bounded the whole kernel).
+  // point queue, one chunk of P points ahead: the next index is taken (and each lane's
+  // point coordinates, radius and state loaded) while the current chunk is processed, so
+  // neither the queue atomic nor the point loads sit on a point's critical path.  Points
+  // are taken kPtGrab chunks at a time (one queue atomic per grab: a single-address
+  // atomic per point serialises at ~13 ns, which had bounded the whole kernel).
+  const unsigned int take = kPtGrab * (unsigned int)P;
   unsigned int idx = 0;
-  if (lane == 0) idx = atomicAdd(work, kPtGrab);
+  if (lane == 0) idx = atomicAdd(work, take);
   idx = __shfl(idx, 0);
-  unsigned int cend = idx + kPtGrab;
+  unsigned int cend = idx + take;
   float xn[DIM], rn = 0.0f;
   bool en = false;
   // 2D Yukawa, reference semantics: the first ball's Bessel members come from the setup kernel
   const bool pre = !RB && DIM == 2 && yuk0;
   float bn[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int k = 0; k < DIM; k++) xn[k] = (int64_t)idx < n ? pts[(int64_t)idx * DIM + k] : 0.0f;
-  if ((int64_t)idx < n) {
-    rn = tk.prad[idx];
-    en = (tk.pstate[idx] & kPtEstimate) != 0;
-    if (pre)
-      for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + idx];
+  {
+    const unsigned int li = idx + (unsigned int)myslot;
+    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)li < n ? pts[(int64_t)li * DIM + k] : 0.0f;
+    if ((int64_t)li < n) {
+      rn = tk.prad[li];
+      en = (tk.pstate[li] & kPtEstimate) != 0;
+      if (pre)
+        for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + li];
+    }
   }
   for (;;) {
     if ((int64_t)idx >= n) break;
-    const unsigned int pidx = idx;
-    const int64_t gidx = base + (int64_t)pidx * stride;
     float x[DIM];
     for (int k = 0; k < DIM; k++) x[k] = xn[k];
-    const float firstR = rn;
-    const bool estimate = en;
+    float firstR = rn;
+    const bool estimate = en && used;
     float pb[4];
     for (int k = 0; k < 4; k++) pb[k] = bn[k];
-    const bool grab = idx + 1 >= cend;  // wave-uniform
+    const bool grab = idx + (unsigned int)P >= cend;  // wave-uniform
     unsigned int nidx_l0 = 0;
-    if (grab && lane == 0) nidx_l0 = atomicAdd(work, kPtGrab);
+    if (grab && lane == 0) nidx_l0 = atomicAdd(work, take);
     DIAG_T0(t_fb0);
-    // the next point: its index (the atomic has returned by now), coordinates, radius, state
+    // the next chunk: its index (the atomic has returned by now), coordinates, radius, state
     unsigned int nidx, ncend = cend;
     if (grab) {
       nidx = (unsigned int)__shfl((int)nidx_l0, 0);
-      ncend = nidx + kPtGrab;
+      ncend = nidx + take;
     } else {
-      nidx = idx + 1;
+      nidx = idx + (unsigned int)P;
     }
-    for (int k = 0; k < DIM; k++) xn[k] = (int64_t)nidx < n ? pts[(int64_t)nidx * DIM + k] : 0.0f;
-    if ((int64_t)nidx < n) {
-      rn = tk.prad[nidx];
-      en = (tk.pstate[nidx] & kPtEstimate) != 0;
-      if (pre)
-        for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + nidx];
+    {
+      const unsigned int li = nidx + (unsigned int)myslot;
+      for (int k = 0; k < DIM; k++) xn[k] = (int64_t)li < n ? pts[(int64_t)li * DIM + k] : 0.0f;
+      en = false;
+      if ((int64_t)li < n) {
+        rn = tk.prad[li];
+        en = (tk.pstate[li] & kPtEstimate) != 0;
+        if (pre)
+          for (int k = 0; k < 4; k++) bn[k] = tk.pball[k * tk.pball_stride + li];
+      }
     }
-    if (!estimate) { idx = nidx; cend = ncend; continue; }
-    c_pts += lane == 0;
+    // estimated slots: bit s * span set when point idx + s is estimated
+    const uint64_t em = __ballot(estimate && wl == 0);
+    if (em == 0) { idx = nidx; cend = ncend; continue; }
+    c_pts += lane == 0 ? (uint32_t)__popcll(em) : 0u;
     DIAG_ADD(D_FB_SETUP, t_fb0);
-    DIAG_COUNT(D_FB_PTS, 1);
+    DIAG_COUNT(D_FB_PTS, __popcll(em));
     DIAG_T0(t_fb1);
-    build_lhs<DIM>(prm, gidx, strat, partner, reinterpret_cast<char*>(rejL), lane);
+    for (int s = 0; s < P; s++) {
+      if (!((em >> (s * span)) & 1ull)) continue;
+      float* strat_s = wbase + 2 * s * lhs_floats;
+      build_lhs<DIM>(prm, base + (int64_t)(idx + (unsigned int)s) * stride, strat_s,
+                     reinterpret_cast<int*>(strat_s + lhs_floats), reinterpret_cast<char*>(rejL), lane);
+    }
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
-    for (int w0 = 0; w0 < npairs; w0 += kWave) {
-      const int w = w0 + lane;
-      first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, w < npairs, w,
+    // lanes without a point of their own (an unestimated slot, or beyond P slots) run the
+    // first estimated slot's pair-0 arithmetic and write nothing (3D: they still serve the
+    // cooperative sampler)
+    const int fs = (int)(__builtin_ctzll(em) / (unsigned)span);
+    const int es = estimate ? myslot : fs;
+    if (!estimate) {
+      for (int k = 0; k < DIM; k++) x[k] = lane_bcast(x[k], fs * span);
+      firstR = lane_bcast(firstR, fs * span);
+      for (int k = 0; k < 4; k++) pb[k] = lane_bcast(pb[k], fs * span);
+    }
+    const unsigned int pidx = idx + (unsigned int)es;
+    const int64_t gidx = base + (int64_t)pidx * stride;
+    const float* strat = wbase + 2 * es * lhs_floats;
+    const int wend = P > 1 ? 1 : npairs;
+    for (int w0 = 0; w0 < wend; w0 += kWave) {
+      const int w = w0 + wl;
+      first_balls<DIM, RB>(sc, prm, tk, x, firstR, strat, gidx, estimate && w < npairs, w,
                            (int64_t)pidx * tk.wpp + (int64_t)w * prm.n_anti, yuk0, &c_iters, rejL, lane,
                            pb, tk.ddir ? tk.ddir + (int64_t)pidx * DIM : nullptr);
     }

@@ -198,9 +198,12 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
   return hipGetLastError();
 }
 
-size_t first_ball_wave_lds_bytes(int lhs_floats) {
-  return (size_t)2 * lhs_floats * sizeof(float) + fb_union_bytes(lhs_floats);
+// P points' stratified samples and partners (fb_points_per_wave), then the sampler / shuffle scratch
+size_t first_ball_wave_lds_bytes(int lhs_floats, int n_pairs) {
+  return (size_t)2 * fb_points_per_wave(n_pairs) * lhs_floats * sizeof(float) + fb_union_bytes(lhs_floats);
 }
+
+int first_ball_points_per_wave(int n_pairs) { return fb_points_per_wave(n_pairs); }
 
 size_t walk_wave_lds_bytes(int dim) { return dim == 2 ? walk_scratch_bytes<2>() : walk_scratch_bytes<3>(); }
 
@@ -214,6 +217,24 @@ hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t 
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<2, false>, kBlock, shmem);
   return geom_global ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3, true>, kBlock, shmem)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wos_walk_kernel<3, false>, kBlock, shmem);
+}
+
+// residency of the walk instantiation launch_walks dispatches for these parameters (the
+// tail-spreading and Neumann-inert kernels differ in static LDS and registers)
+hipError_t occupancy_walk_blocks_per_cu(int dim, bool geom_global, const DevParams& prm, size_t shmem, int* blocks) {
+  if (prm.robust) return occupancy_rb(1, dim, geom_global, shmem, blocks);
+#define WOS_OCC(K) hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, K, kBlock, shmem)
+  const bool inert = prm.neumann_inert != 0;
+  if (dim == 2) {
+    if (geom_global) return inert ? WOS_OCC((wos_walk_kernel<2, true, false, false, false>)) : WOS_OCC((wos_walk_kernel<2, true>));
+    if (prm.tail_spread)
+      return inert ? WOS_OCC((wos_walk_kernel<2, false, false, false, false, true>))
+                   : WOS_OCC((wos_walk_kernel<2, false, false, false, true, true>));
+    return inert ? WOS_OCC((wos_walk_kernel<2, false, false, false, false>)) : WOS_OCC((wos_walk_kernel<2, false>));
+  }
+  if (geom_global) return inert ? WOS_OCC((wos_walk_kernel<3, true, false, false, false>)) : WOS_OCC((wos_walk_kernel<3, true>));
+  return inert ? WOS_OCC((wos_walk_kernel<3, false, false, false, false>)) : WOS_OCC((wos_walk_kernel<3, false>));
+#undef WOS_OCC
 }
 
 void diag_dump(const char* tag) { diag_print(tag, HIP_SYMBOL(g_diag)); }

@@ -29,13 +29,15 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s);
 // per-wave LDS scratch of the first-ball kernel
-size_t first_ball_wave_lds_bytes(int lhs_floats);
+size_t first_ball_wave_lds_bytes(int lhs_floats, int n_pairs);
+int first_ball_points_per_wave(int n_pairs);
 // per-wave LDS scratch of the walk kernel (after the staged geometry, 16-B aligned)
 size_t walk_wave_lds_bytes(int dim);
 // which: 0 first-ball kernel, 1 walk kernel (the instantiation for LDS-staged or global geometry);
 // robust: the robust-float instantiations (wos_robust.hip)
 hipError_t occupancy_blocks_per_cu(int which, int dim, bool geom_global, size_t shmem, int* blocks,
                                    bool robust = false);
+hipError_t occupancy_walk_blocks_per_cu(int dim, bool geom_global, const DevParams& prm, size_t shmem, int* blocks);
 void diag_dump(const char* tag);  // WOS_DIAG builds: print + reset the walk-kernel diagnostics
 void diag_dump_bstart(const char* tag);  // ... of the boundary-start walk kernels (wos_bvc.hip)
 void diag_print(const char* tag, const void* sym);

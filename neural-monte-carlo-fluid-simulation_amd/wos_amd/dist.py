@@ -18,12 +18,18 @@ def shard(n, rank, world):
     return idx, n_pad
 
 
-def sharded_projection(solve_local, pts, rank, world, dim, group=None, device=None):
+def sharded_projection(solve_local, pts, rank, world, dim, group=None, device=None, force_gather=False):
     """Solve all `pts` ([N, dim], identical on every rank) across `world` ranks.
 
     solve_local(local_pts, index_base, index_stride) -> (p [n_local], grad [n_local, dim])
     as torch tensors on `device` (any device the process group's backend accepts).
     Returns full (p [N], grad [N, dim]) torch tensors on every rank.
+
+    One code path for every backend: the shard, padded to n_pad rows, goes through ONE
+    `all_gather_into_tensor` into a (world * n_pad, 1 + dim) buffer (RCCL over xGMI with
+    "nccl", gloo in the CPU tests), and the field is reassembled by a view: global point
+    i = j * world + r is row j of rank r's block.  `force_gather` runs the collective even
+    at world 1 (exercises the RCCL call on a one-GPU lease).
     """
     import torch
     import torch.distributed as dist
@@ -37,18 +43,34 @@ def sharded_projection(solve_local, pts, rank, world, dim, group=None, device=No
     send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=device)
     send[: idx.size, 0] = p
     send[: idx.size, 1:] = g
-    if world > 1:
-        if dist.get_backend(group) == "nccl":
-            buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=device)
-            dist.all_gather_into_tensor(buf, send, group=group)
-            parts = list(buf.view(world, n_pad, 1 + dim))
-        else:
-            parts = [torch.empty_like(send) for _ in range(world)]
-            dist.all_gather(parts, send, group=group)
+    if world > 1 or force_gather:
+        buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=device)
+        dist.all_gather_into_tensor(buf, send, group=group)
     else:
-        parts = [send]
-    full = torch.empty(n, 1 + dim, dtype=torch.float32, device=device)
-    for r in range(world):
-        cnt = len(range(r, n, world))
-        full[r::world] = parts[r][:cnt]
+        buf = send
+    # (world, n_pad) blocks -> point order r + world * j; the padded rows (j >= count of
+    # rank r) are exactly the indices >= n
+    full = buf.view(world, n_pad, 1 + dim).transpose(0, 1).reshape(world * n_pad, 1 + dim)[:n]
     return full[:, 0].contiguous(), full[:, 1:].contiguous()
+
+
+def make_gather(world, dist, n_local, n_pad, dim, dev, torch):
+    """bench.py's per-projection gather, on the same collective as sharded_projection:
+    every rank sends its shard padded to n_pad rows into a (world * n_pad, 1 + dim)
+    buffer with ONE all_gather_into_tensor.  With the gloo backend (CPU-only rehearsal
+    of the N-rank path, tests/test_bench_dist.py) the payload is staged through host
+    memory; with nccl (RCCL) it stays in HBM.  None at world 1 (nothing to exchange)."""
+    if world == 1:
+        return None
+    staged = dist.get_backend() == "gloo" and dev.type != "cpu"
+    bdev = torch.device("cpu") if staged else dev
+    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=bdev)
+    buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=bdev)
+
+    def gather(p, g):
+        send[:n_local, 0] = p.to(bdev)
+        send[:n_local, 1:] = g.to(bdev)
+        dist.all_gather_into_tensor(buf, send)
+
+    gather.buf = buf
+    return gather

@@ -1961,8 +1961,9 @@ static int cdf_sample(const float *table, int size, float u)
 /* The BoundarySampler's boundary (boundary_sampler.h:87-412): every segment of the scene, here the
  * Neumann segments then the Dirichlet ones (the reference: the OBJ's order, typed by
  * onNeumannBoundary at the midpoint, demo.cpp:300-313); Dirichlet vertices carry the sampler's
- * own vertex normals (computeNormals :193-236: unit segment normals summed, normalised), per
- * part (a vertex shared by a Neumann and a Dirichlet segment keeps its Dirichlet normal). */
+ * own vertex normals (computeNormals :193-236: unit segment normals summed, normalised) over the
+ * scene's one mesh (demo.cpp:316): a Dirichlet vertex also sums the normals of the Neumann
+ * segments ending at its position (the two parts arrive as separate meshes; welded by position). */
 typedef struct {
     int ns, nn;                 /* segments, of which the first nn are Neumann */
     const float *(*a), *(*b);   /* endpoints */
@@ -1984,6 +1985,19 @@ static void bseg_build(const scene_t *sc, bseg_t *B)
         float z = n[0] * n[0] + n[1] * n[1];
         if (z > 0.0f) { float r = sqrtf(z); n[0] = n[0] / r; n[1] = n[1] / r; }
         for (int q = 0; q < 2; q++) { float *v = B->dn[D->ix[p][q]]; v[0] += n[0]; v[1] += n[1]; }
+    }
+    /* junctions: Neumann segment ends at a Dirichlet vertex's position (brute force) */
+    for (int p = 0; p < N->np && D->np > 0; p++) {
+        const float *pa = N->v[N->ix[p][0]], *pb = N->v[N->ix[p][1]];
+        float s0 = pb[0] - pa[0], s1 = pb[1] - pa[1];
+        float n[2] = {s1, -s0};
+        float z = n[0] * n[0] + n[1] * n[1];
+        if (z > 0.0f) { float r = sqrtf(z); n[0] = n[0] / r; n[1] = n[1] / r; }
+        for (int q = 0; q < 2; q++) {
+            const float *e = q ? pb : pa;
+            for (int i = 0; i < D->nv; i++)
+                if (D->v[i][0] == e[0] && D->v[i][1] == e[1]) { B->dn[i][0] += n[0]; B->dn[i][1] += n[1]; }
+        }
     }
     for (int i = 0; i < D->nv; i++) {
         float z = B->dn[i][0] * B->dn[i][0] + B->dn[i][1] * B->dn[i][1];

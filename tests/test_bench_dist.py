@@ -55,7 +55,7 @@ def _worker(rank, world, port, out_dir):
     pts = np.zeros((n_all, 2), np.float32)
     local = pts[rank::world]
     n_pad = (n_all + world - 1) // world
-    gather = bench.make_gather(world, dist, local.shape[0], n_pad, 2, dev, torch)
+    gather = bench.wdist.make_gather(world, dist, local.shape[0], n_pad, 2, dev, torch)
     scene = _IndexScene()
     el, stats = bench.timed_projections(scene, torch.from_numpy(local), None, rank, world, 4, 1, False,
                                         world, dist, torch, gather)

@@ -98,6 +98,42 @@ def test_bvc_dirichlet_disk_kat(oracle):
     assert abs(float(np.mean(derivs)) / dn - 1.0) < 0.1, (np.mean(derivs), dn)
 
 
+def test_bvc_junction_normals_welded(oracle):
+    """Sampler vertex normals over the scene's one mesh (advisor finding, round 4): at a
+    Neumann/Dirichlet junction both segments' normals are summed (boundary_sampler.h:193-236 run
+    on scene.vertices / scene.segments, demo.cpp:316), so the displaced Dirichlet bottom side of
+    bvc_cases.junction_square runs from (d, d) to (1 - d, d), d = normalOffset / sqrt 2."""
+    c = bvc_cases.junction_square()
+    sc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], **c["kw"])
+    sol, _, smp, counts, _ = oracle.bvc(sc, oracle.make_params(c["solver"], c["output"], seed=0x400),
+                                        oracle.bvc_params(c["solver"], c["output"]))
+    d = smp[smp[:, 7] == 3]
+    assert d.shape[0] > 64 and (smp[:, 7] == 0).sum() > 64  # Dirichlet and Neumann samples
+    off = np.float32(5e-3)  # normalOffsetForCachedDirichletSamples = 5 epsilonShell
+    delta = float(off) / np.sqrt(2.0)
+    np.testing.assert_allclose(d[:, 1], delta, rtol=0, atol=2e-7)
+    assert d[:, 0].min() >= delta - 1e-6 and d[:, 0].max() <= 1.0 - delta + 1e-6
+    assert np.isfinite(sol).all()
+
+
+def test_bvc_junction_kat(oracle):
+    """Mixed boundary with Neumann/Dirichlet junctions (bvc_cases.junction_square): the splatted
+    estimate over 8 keys matches u = cosh(mu (1 - y)) / cosh(mu) away from the corners
+    (projection within 2 %, RMS < 4 %)."""
+    c = bvc_cases.junction_square()
+    sc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], **c["kw"])
+    sols = [oracle.bvc(sc, oracle.make_params(c["solver"], c["output"], seed=0x500 + s),
+                       oracle.bvc_params(c["solver"], c["output"]))[0] for s in range(8)]
+    m = np.mean(sols, 0)
+    eps = np.float32(np.finfo(np.float32).eps)
+    lo, hi = np.zeros(2, np.float32) - eps, np.ones(2, np.float32) + eps
+    X, Y, pe = bvc_cases.junction_reference(32, c["absorption"], lo, hi)
+    sel = (X > 0.15) & (X < 0.85) & (Y > 0.05) & (Y < 0.8)
+    ratio = float((m[sel] * pe[sel]).sum() / (pe[sel] ** 2).sum())
+    rel = float(np.sqrt(np.mean((m[sel] - pe[sel]) ** 2)) / np.sqrt(np.mean(pe[sel] ** 2)))
+    assert abs(ratio - 1.0) < 0.02 and rel < 0.04, (ratio, rel)
+
+
 def test_bvc_rejects_3d(oracle):
     from wos_amd import workloads
     cfg = workloads.cube_config(res=8, n_walks=8)

@@ -77,6 +77,78 @@ def test_shard_covers_all_points_once():
             assert all(shard(n, r, w)[0].size <= shard(n, r, w)[1] for r in range(w))
 
 
+def _forced_gather_worker(rank, world, port, out_dir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "neural-monte-carlo-fluid-simulation_amd")]
+    import torch
+    import torch.distributed as dist
+    from wos_amd import dist as wdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1001
+    pts = torch.arange(2 * n, dtype=torch.float32).reshape(n, 2)
+
+    def solve_local(local, base, stride):  # a point's "solution" is a function of its global index
+        gi = torch.arange(base, n, stride, dtype=torch.float32)
+        assert gi.shape[0] == local.shape[0]
+        return gi * 0.5, torch.stack([gi, -gi], 1)
+
+    p, g = wdist.sharded_projection(solve_local, pts, rank, world, 2, force_gather=True)
+    torch.save({"p": p, "g": g}, os.path.join(out_dir, f"fg{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_forced_gather_reassembles_point_order(tmp_path, world):
+    """The one all_gather_into_tensor path (every backend, forced at world 1 as the
+    RCCL GPU test runs it) puts global point i = r + world * j back at row i."""
+    import torch
+    port = _free_port()
+    mp.start_processes(_forced_gather_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    gi = torch.arange(1001, dtype=torch.float32)
+    for r in range(world):
+        d = torch.load(tmp_path / f"fg{r}.pt", weights_only=True)
+        assert torch.equal(d["p"], gi * 0.5)
+        assert torch.equal(d["g"], torch.stack([gi, -gi], 1))
+
+
+@pytest.mark.gpu
+def test_sharded_projection_rccl_world1(tmp_path, gpu, oracle):
+    """The product's RCCL gather on MI355X: a world-1 "nccl" (RCCL) process group on
+    the lease's one GPU (RCCL refuses two ranks on one GPU), the device-side
+    all_gather_into_tensor forced through wos_amd.dist.sharded_projection; the field
+    equals an unsharded engine solve and the oracle, bit for bit."""
+    import subprocess
+    import sys
+    from wos_amd import WosScene, solver_params, workloads
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_engine_worker.py")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, worker, "0", "1", str(port), str(tmp_path), "nccl"], env=env,
+                       capture_output=True, text=True, timeout=150)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "RCCL all_gather_into_tensor" in r.stdout
+    cfg = workloads.config_by_name("B")
+    pts = cfg["points"][:4099]
+    prm = solver_params(dict(cfg["solver"], nWalks=64), cfg["output"])
+    sc = WosScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0, watertight=True)
+    p1, g1, _ = sc.solve(pts, prm)
+    sc.close()
+    osc = oracle.OracleScene(cfg["vertices"], cfg["prims"], cfg["source"], 350.0)
+    po, go, _, _, _ = oracle.solve(osc, oracle.make_params(dict(cfg["solver"], nWalks=64), cfg["output"]),
+                                   pts[::41], index_base=0, index_stride=41)
+    np.testing.assert_array_equal(p1[::41], po)
+    np.testing.assert_array_equal(g1[::41], go)
+    d = np.load(tmp_path / "rank0.npz")
+    np.testing.assert_array_equal(d["p"], p1)
+    np.testing.assert_array_equal(d["g"], g1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2])
 def test_sharded_projection_hip_engine(tmp_path, gpu, oracle, world):

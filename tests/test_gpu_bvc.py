@@ -108,6 +108,36 @@ def test_bvc_mixed_boundary_bit_exact(gpu, oracle, fd):
         assert info["stats"][k] == ost[k], k
 
 
+def test_bvc_junction_bit_exact_and_kat(gpu, oracle):
+    """Neumann/Dirichlet junctions (bvc_cases.junction_square): the host sampler welds the two
+    parts' normals like the oracle (samples, solution and gradient bit for bit), and the HIP BVC
+    matches u = cosh(mu (1 - y)) / cosh(mu) away from the corners (8 keys: projection within 2 %,
+    RMS < 4 % in 0.15 < x < 0.85, y < 0.8)."""
+    import bvc_cases
+    c = bvc_cases.junction_square()
+    sc = WosScene(c["vertices"], c["prims"], c["source"], c["absorption"], watertight=True, **c["kw"])
+    osc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], **c["kw"])
+    small = dict(c["solver"], boundaryCacheSize=128, nWalksForCachedGradientEstimates=32,
+                 nWalksForCachedSolutionEstimates=16)
+    out = dict(c["output"], gridRes=16)
+    sol, grad, info = sc.bvc(solver_params(small, out), bvc_params(small, out))
+    osol, ograd, osmp, _, _ = oracle.bvc(osc, oracle.make_params(small, out), oracle.bvc_params(small, out))
+    _bits(info["samples"], osmp)
+    _bits(sol, osol)
+    _bits(grad, ograd)
+    sols = [sc.bvc(solver_params(c["solver"], c["output"], seed=0x500 + s), bvc_params(c["solver"], c["output"]))[0]
+            for s in range(8)]
+    sc.close()
+    m = np.mean(sols, 0)
+    eps = np.float32(np.finfo(np.float32).eps)
+    lo, hi = np.array([0, 0], np.float32) - eps, np.array([1, 1], np.float32) + eps
+    X, Y, pe = bvc_cases.junction_reference(32, c["absorption"], lo, hi)
+    sel = (X > 0.15) & (X < 0.85) & (Y > 0.05) & (Y < 0.8)
+    ratio = float((m[sel] * pe[sel]).sum() / (pe[sel] ** 2).sum())
+    rel = float(np.sqrt(np.mean((m[sel] - pe[sel]) ** 2)) / np.sqrt(np.mean(pe[sel] ** 2)))
+    assert abs(ratio - 1.0) < 0.02 and rel < 0.04, (ratio, rel)
+
+
 def test_bvc_dirichlet_disk_kat_gpu(gpu):
     """The oracle's Dirichlet-disk BVC KAT (tests/test_bvc.py) on the HIP path: u = I0(2r)/I0(2)."""
     import kat_cases

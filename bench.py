@@ -413,8 +413,11 @@ def main():
                 "device_handoff_ms": pt["device_fresh_scene_ms"],
                 "reference_handoff_ms": pt["ref_style_ms"],
                 "scene_create_ms": pt["scene_create_ms"],
-                "note": "device: Scene(cfg, div CUDA tensor) + wost(CUDA points), outputs on device; reference: "
-                        "div/points via .cpu().numpy(), nested-list outputs, grad p back to the device",
+                "device_scene_reuse_ms": pt["device_scene_reuse_ms"],
+                "device_handoff_breakdown": pt["device_handoff_breakdown"],
+                "note": "device: Scene(cfg, div CUDA tensor) + wost(CUDA points), outputs on device, synced per call; "
+                        "reference: div/points via .cpu().numpy(), nested-list outputs, grad p back to the device; "
+                        "scene_create_ms: Scene(cfg, div numpy); device_scene_reuse_ms: one Scene, set_source + wost",
             }
         if world == 1 and not a.no_cpu_baseline:
             sys.path.insert(0, os.path.join(REPO, "tests"))

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 8
+#define WOS_ABI_VERSION 9
 
 enum {
     WOS_OK = 0,
@@ -77,6 +77,16 @@ typedef struct wos_scene_desc {
     int32_t dirichlet_image_dims[2]; /* H, W */
     float dirichlet_image_box[4];    /* x0, y0, ex, ey: the rectangle the image covers */
     int32_t dirichlet_image_on_device;
+    /* optional image-valued Neumann data h (2D, ABI 9): pde.neumann at a boundary sample y is
+       Image::get((y - x0) / ex, (y - y0) / ey) (the upstream demo's pde.neumann, scene.h:175-181
+       commented in the fork: uv = (x - bbox.pMin) / bbox.extent(); image.h:53-58).  It enters the
+       walk's Neumann term throughput * alpha * G * h / pdf at every step (walk_on_stars.h:212-260)
+       and a BVC Neumann sample's normal derivative (boundary_sampler.h:126-133).  NULL: h = 0,
+       the reference's pde.neumann (scene.h:176-181, scene_3d.h:108-111) */
+    const float *neumann_image;      /* [H][W] row-major, row ~ y */
+    int32_t neumann_image_dims[2];   /* H, W */
+    float neumann_image_box[4];      /* x0, y0, ex, ey */
+    int32_t neumann_image_on_device;
 } wos_scene_desc;
 
 typedef struct wos_scene wos_scene;

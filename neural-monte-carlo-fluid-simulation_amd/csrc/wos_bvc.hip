@@ -478,21 +478,29 @@ hipError_t launch_bvc_splat(const float* recs, int r0, int r1, int first, int la
   return hipGetLastError();
 }
 
-// the estimated values of the boundary records [b0, b1): the solution, and a Dirichlet
-// sample's normal derivative (kinds 3, 4) -- written once the walks that estimate them are done
+// the estimated values of the boundary records [b0, b1): the solution, and the normal
+// derivative -- a Dirichlet sample's estimate (kinds 3, 4), a Neumann sample's pde.neumann at its
+// point (kinds 0, 1; boundary_sampler.h:126-133: 0 in the reference's scenes, the image-valued h
+// when the scene has one) -- written once the walks that estimate them are done
 __global__ __launch_bounds__(256) void wos_bvc_fill_kernel(float* __restrict__ recs, int64_t b0, int64_t b1,
                                                            const float* __restrict__ bsol,
-                                                           const float* __restrict__ bdn) {
+                                                           const float* __restrict__ bdn, const DevScene sc,
+                                                           int ignore_neumann) {
   const int64_t i = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= b1) return;
-  const int kind = (int)recs[i * kBvcRec + 7];
-  recs[i * kBvcRec + 5] = bsol[i];
-  recs[i * kBvcRec + 6] = (kind == kBvcDirichlet || kind == kBvcDirichletAligned) ? bdn[i] : 0.0f;
+  float* R = recs + i * kBvcRec;
+  const int kind = (int)R[7];
+  R[5] = bsol[i];
+  R[6] = (kind == kBvcDirichlet || kind == kBvcDirichletAligned) ? bdn[i]
+         : ignore_neumann                                       ? 0.0f
+                                                                : neumann_value(sc, R);
 }
 
-hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn, hipStream_t s) {
+hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn,
+                           const DevScene& sc, int ignore_neumann, hipStream_t s) {
   if (b1 <= b0) return hipSuccess;
-  hipLaunchKernelGGL(wos_bvc_fill_kernel, dim3((int)((b1 - b0 + 255) / 256)), dim3(256), 0, s, recs, b0, b1, bsol, bdn);
+  hipLaunchKernelGGL(wos_bvc_fill_kernel, dim3((int)((b1 - b0 + 255) / 256)), dim3(256), 0, s, recs, b0, b1, bsol, bdn,
+                     sc, ignore_neumann);
   return hipGetLastError();
 }
 

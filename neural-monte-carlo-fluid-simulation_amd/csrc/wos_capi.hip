@@ -348,6 +348,7 @@ struct wos_scene {
   float* d_source = nullptr;
   size_t source_cap = 0;  // floats
   float* d_dimg = nullptr;  // image-valued Dirichlet data (wos_scene_desc.dirichlet_image)
+  float* d_nimg = nullptr;  // image-valued Neumann data (wos_scene_desc.neumann_image)
   std::mutex mu;          // solve vs set_source on the same scene
 };
 
@@ -435,6 +436,18 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
       return fail(WOS_E_INVALID, "wos_scene_create: dirichlet_image_box extent must be > 0");
     ndimg = (size_t)d->dirichlet_image_dims[0] * d->dirichlet_image_dims[1];
   }
+  size_t nnimg = 0;
+  if (d->neumann_image) {
+    if (d->dim != 2) return fail(WOS_E_INVALID, "wos_scene_create: neumann_image is 2D only");
+    if (d->neumann_image_dims[0] < 1 || d->neumann_image_dims[1] < 1 ||
+        (int64_t)d->neumann_image_dims[0] * d->neumann_image_dims[1] > (int64_t)1 << 28)
+      return fail(WOS_E_INVALID, "wos_scene_create: bad neumann_image dims");
+    const float* nb = d->neumann_image_box;
+    if (!std::isfinite(nb[0]) || !std::isfinite(nb[1]) || !(nb[2] > 0.0f) || !(nb[3] > 0.0f) ||
+        !std::isfinite(nb[2]) || !std::isfinite(nb[3]))
+      return fail(WOS_E_INVALID, "wos_scene_create: neumann_image_box needs a finite corner and extents > 0");
+    nnimg = (size_t)d->neumann_image_dims[0] * d->neumann_image_dims[1];
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(WOS_E_DEVICE, "wos_scene_create: no HIP device available");
@@ -465,6 +478,19 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
       e = hipMemcpy(s->d_dimg, d->dirichlet_image, ndimg * sizeof(float),
                     d->dirichlet_image_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
     if (e != hipSuccess) {
+      hipFree(s->d_dimg);
+      hipFree(s->d_source);
+      delete s;
+      return fail(WOS_E_DEVICE, std::string("wos_scene_create: ") + hipGetErrorString(e));
+    }
+  }
+  if (nnimg) {
+    hipError_t e = hipMalloc((void**)&s->d_nimg, nnimg * sizeof(float));
+    if (e == hipSuccess)
+      e = hipMemcpy(s->d_nimg, d->neumann_image, nnimg * sizeof(float),
+                    d->neumann_image_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      hipFree(s->d_nimg);
       hipFree(s->d_dimg);
       hipFree(s->d_source);
       delete s;
@@ -506,6 +532,9 @@ int wos_scene_create(const wos_scene_desc* d, int32_t device, wos_scene** out) {
   ds.dimg = s->d_dimg;
   for (int k = 0; k < 2; k++) ds.ddims[k] = ndimg ? d->dirichlet_image_dims[k] : 0;
   for (int k = 0; k < 4; k++) ds.dbox[k] = ndimg ? d->dirichlet_image_box[k] : 0.0f;
+  ds.nimg = s->d_nimg;
+  for (int k = 0; k < 2; k++) ds.ndims[k] = nnimg ? d->neumann_image_dims[k] : 0;
+  for (int k = 0; k < 4; k++) ds.nbox[k] = nnimg ? d->neumann_image_box[k] : 0.0f;
   ds.watertight = d->is_watertight;
   ds.double_sided = d->is_double_sided;
   *out = s;
@@ -550,6 +579,7 @@ int wos_scene_destroy(wos_scene* s) {
     if (c.inflight) hipEventSynchronize(c.done);  // an async solve may still read the source
     hipFree(s->d_source);
     hipFree(s->d_dimg);
+    hipFree(s->d_nimg);
   }
   delete s;
   return WOS_OK;
@@ -985,7 +1015,8 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     double diag2 = 0.0;
     for (int k = 0; k < 3; k++) diag2 += (double)host.ext[k] * host.ext[k];
     const double mu_r = std::sqrt(std::max(0.0, (double)s->dev.absorption)) * std::sqrt(diag2) * 1.01;
-    dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0 &&
+    // (image-valued h makes the term non-zero at every step: never inert)
+    dp.neumann_inert = (!dp.robust && s->dev.watertight && !s->dev.double_sided && mu_r < 80.0 && !s->dev.nimg &&
                         !(prm->schedule & WOS_SCHED_FULL_NEUMANN)) ? 1 : 0;
   }
   // Walks handed to idle sibling waves once the queue is dry (the walk kernel's SPR
@@ -1484,7 +1515,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   const float ab = s->dev.absorption;
   const bool part1 = p1 > 0, part1_last = p1 == nrec;
   if (part1) {
-    HIP_TRY(wos::launch_bvc_fill(d_recs, 0, p1, d_bsol, d_bdn, c.side[0].stream));
+    HIP_TRY(wos::launch_bvc_fill(d_recs, 0, p1, d_bsol, d_bdn, s->dev, prm->ignore_neumann, c.side[0].stream));
     HIP_TRY(wos::launch_bvc_splat(d_recs, 0, (int)p1, 1, part1_last ? 1 : 0, d_state, d_slist, d_scount, d_ept, ne,
                                   ab, bp->radius_clamp, bp->kernel_regularization, d_sol, d_grad, c.side[0].stream));
   }
@@ -1493,7 +1524,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   HIP_TRY(hipStreamWaitEvent(st, c.side[0].done, 0));
   HIP_TRY(hipEventRecord(q.bev[2], st));
   if (!(part1 && part1_last)) {
-    HIP_TRY(wos::launch_bvc_fill(d_recs, p1, nb, d_bsol, d_bdn, st));
+    HIP_TRY(wos::launch_bvc_fill(d_recs, p1, nb, d_bsol, d_bdn, s->dev, prm->ignore_neumann, st));
     HIP_TRY(wos::launch_bvc_splat(d_recs, part1 ? (int)p1 : 0, (int)nrec, part1 ? 0 : 1, 1, d_state, d_slist,
                                   d_scount, d_ept, ne, ab, bp->radius_clamp, bp->kernel_regularization, d_sol,
                                   d_grad, st));

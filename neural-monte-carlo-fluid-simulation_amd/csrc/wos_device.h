@@ -1033,6 +1033,19 @@ __device__ float dirichlet_value(const DevScene& sc, const float* x) {
   return sc.g_dirichlet;
 }
 
+// h at a Neumann boundary sample y (walk_on_stars.h:253-256): the upstream demo's pde.neumann
+// (scene.h:175-181, commented in the fork: uv = (y - bbox.pMin) / bbox.extent()) over sc.nbox,
+// looked up as Image::get (image.h:53-58); 0 without an image (the reference's h, scene.h:176-181)
+__device__ __forceinline__ float neumann_value(const DevScene& sc, const float* y) {
+  if (sc.nimg == nullptr) return 0.0f;
+  const float ux = (y[0] - sc.nbox[0]) / sc.nbox[2];
+  const float uy = (y[1] - sc.nbox[1]) / sc.nbox[3];
+  const int h = sc.ndims[0], w = sc.ndims[1];
+  const int i = sclamp(cvt_trunc(uy * (float)h), 0, h - 1);
+  const int j = sclamp(cvt_trunc(ux * (float)w), 0, w - 1);
+  return sc.nimg[(size_t)i * w + j];
+}
+
 template <int DIM>
 __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x) {
   for (int k = 0; k < DIM; k++)
@@ -2160,10 +2173,12 @@ __device__ __forceinline__ int fcpw_stochastic_pick(const DevScene& sc, const fl
 
 // Neumann boundary sample (walk_on_stars.h:212-260).  With the reference's h == 0
 // (scene.h:176-181) the term is exactly +0 unless G or the throughput is
-// non-finite; only then the stochastic sample is evaluated.
+// non-finite; only then the stochastic sample is evaluated -- at every step with
+// image-valued h (DevScene::nimg).  flip: this step flipped the walk's normal
+// (flipNormalOrientation, double-sided scenes); prec: silhouettePrecision.
 template <int DIM, bool RB>
 __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* prims, const Gfn<DIM, RB>& g,
-                                          WalkState<DIM>& st, float R, const float* rn) {
+                                             WalkState<DIM>& st, float R, const float* rn, bool flip, float prec) {
   constexpr int PS = Layout<DIM>::prim;
   const int np = sc.n_prims;
   const float* x = st.pt;
@@ -2194,6 +2209,21 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
   for (int k = 0; k < DIM; k++) dts[k] = sp[k] - x[k];
   float distToSample = normv<DIM>(dts);
   float alpha = st.onNeumann ? 2.0f : 1.0f;
+  if (sc.double_sided) {
+    // the sample normal faces the walk (walk_on_stars.h:219-247): flipped with the walk's normal,
+    // or when the sample lies behind it beyond the precision band -- on a concave boundary
+    // (alpha 2) only when it also lies behind the walk's own normal
+    float ds[DIM];
+    for (int k = 0; k < DIM; k++) ds[k] = dts[k] / distToSample;
+    if (flip) {
+      for (int k = 0; k < DIM; k++) sn[k] *= -1.0f;
+    } else if (dotv<DIM>(ds, sn) < -prec) {
+      bool f = true;
+      if (alpha > 1.0f) f = dotv<DIM>(ds, st.n) < -prec;
+      if (f)
+        for (int k = 0; k < DIM; k++) sn[k] *= -1.0f;
+    }
+  }
   if (pdf > 0.0f && distToSample < R) {
     float p1[DIM], p2[DIM], mn[DIM];
     for (int k = 0; k < DIM; k++) mn[k] = -st.n[k];
@@ -2206,7 +2236,7 @@ __device__ __forceinline__ void neumann_term(const DevScene& sc, const float* pr
     for (int k = 0; k < DIM; k++) dd[k] /= dn;
     if (!ray_occluded<DIM>(prims, np, p1, dd, dn)) {
       float G = g.evaluate_xy(x, sp);
-      float hval = 0.0f;
+      float hval = DIM == 2 ? neumann_value(sc, sp) : 0.0f;
       st.totalNeumann += st.throughput * alpha * G * hval / pdf;
     }
   }
@@ -2274,7 +2304,7 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
 template <int DIM, bool RB, bool NEU = true>
 __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParams& prm, const LGeom& G,
                                               Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, float starRadius,
-                                              const float* dir, const float* org, bool hit, Hit& ip) {
+                                              const float* dir, const float* org, bool hit, Hit& ip, bool flip) {
   const int np = sc.n_prims;
   const float* prims = G.prim;
   if (!hit) {
@@ -2286,7 +2316,8 @@ __device__ __forceinline__ void walk_step_end(const DevScene& sc, const DevParam
     for (int k = 0; k < DIM; k++) rn[k] = smp.nextf();
     if constexpr (NEU) {
       bool nonfinite = !__builtin_isfinite(st.throughput) || (g.yukawa == 1 && g.muR > 85.0f);
-      if (nonfinite && np > 0) neumann_term<DIM>(sc, prims, g, st, starRadius, rn);
+      if ((nonfinite || sc.nimg != nullptr) && np > 0)
+        neumann_term<DIM>(sc, prims, g, st, starRadius, rn, flip, prm.silhouette_precision);
     } else {
       (void)np; (void)prims;
     }
@@ -3649,7 +3680,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   const bool hit = ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
   DIAG_ADD_LONE(D_RAY, D_L_RAY, t_ray, lone);
   DIAG_T0(t_end);
-  if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip);
+  if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip, flip);
   DIAG_ADD_LONE(D_END, D_L_END, t_end, lone);
   float sp[DIM], pdf_unused;
   for (int k = 0; k < DIM; k++) sp[k] = 0.0f;

@@ -60,7 +60,8 @@ hipError_t launch_bvc_splat_list(const float* edd, const float* end_, const int3
 hipError_t launch_bvc_splat(const float* recs, int r0, int r1, int first, int last, float* state,
                             const uint32_t* list, const uint32_t* count, const float* ept, int64_t ne,
                             float absorption, float radius_clamp, float reg, float* sol, float* grad, hipStream_t s);
-hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn, hipStream_t s);
+hipError_t launch_bvc_fill(float* recs, int64_t b0, int64_t b1, const float* bsol, const float* bdn,
+                           const DevScene& sc, int ignore_neumann, hipStream_t s);
 // robust float semantics (wos_robust.hip): the same launches with Gfn<DIM, true>;
 // the launchers above dispatch here when prm.robust is set
 hipError_t launch_first_balls_rb(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,

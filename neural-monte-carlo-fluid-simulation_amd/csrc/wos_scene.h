@@ -86,6 +86,11 @@ struct DevScene {
   const float* dimg;
   int32_t ddims[2];
   float dbox[4];
+  // image-valued Neumann data h (wos_scene_desc.neumann_image; nullptr: h = 0, the reference's):
+  // [ndims[0]][ndims[1]] over the rectangle nbox = (x0, y0, ex, ey)
+  const float* nimg;
+  int32_t ndims[2];
+  float nbox[4];
   int32_t watertight;
   int32_t double_sided;
   // star-radius cell grid (wos_host_scene.h StarGrid; nullptr: none): u16 cell

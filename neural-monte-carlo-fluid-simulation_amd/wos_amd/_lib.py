@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 8  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 9  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_E_CAPACITY = -4
 WOS_PTRS_DEVICE = 0x1
@@ -37,6 +37,8 @@ class SceneDesc(C.Structure):
         ("source", C.c_void_p), ("source_dims", C.c_int32 * 3), ("source_on_device", C.c_int32),
         ("dirichlet_image", C.c_void_p), ("dirichlet_image_dims", C.c_int32 * 2),
         ("dirichlet_image_box", C.c_float * 4), ("dirichlet_image_on_device", C.c_int32),
+        ("neumann_image", C.c_void_p), ("neumann_image_dims", C.c_int32 * 2),
+        ("neumann_image_box", C.c_float * 4), ("neumann_image_on_device", C.c_int32),
     ]
 
 

@@ -103,12 +103,14 @@ class WosScene:
     """Geometry + source field resident on one GPU."""
 
     def __init__(self, vertices, prims, source=None, absorption=0.0, *, dvertices=None, dprims=None,
-                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, watertight=True,
-                 double_sided=False, device=0):
+                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, neumann_image=None,
+                 neumann_image_box=None, watertight=True, double_sided=False, device=0):
         """dirichlet_image (2D, optional): g as an image [H, W] (row ~ y) over the rectangle
         dirichlet_image_box = (x0, y0, ex, ey), evaluated at each walk's projection onto the
         Dirichlet boundary (the upstream demo's pde.dirichlet, scene.h:202-207); replaces the
-        constant dirichlet_value."""
+        constant dirichlet_value.  neumann_image (2D, optional): the Neumann data h as an image
+        [H, W] over neumann_image_box, evaluated at the walks' stochastic boundary samples and at
+        BVC's Neumann samples (the upstream demo's pde.neumann, scene.h:175-181); default h = 0."""
         L = _lib.load()
         v = np.ascontiguousarray(vertices, dtype=np.float32)
         ix = np.ascontiguousarray(prims, dtype=np.int32)
@@ -146,6 +148,13 @@ class WosScene:
             for k in range(4):
                 d.dirichlet_image_box[k] = float(dirichlet_image_box[k])
             keep.append(dimg)
+        if neumann_image is not None:
+            nimg, on_dev = self._image(neumann_image, neumann_image_box, "neumann_image")
+            d.neumann_image, d.neumann_image_on_device = (nimg.data_ptr() if on_dev else nimg.ctypes.data), on_dev
+            d.neumann_image_dims[0], d.neumann_image_dims[1] = int(nimg.shape[0]), int(nimg.shape[1])
+            for k in range(4):
+                d.neumann_image_box[k] = float(neumann_image_box[k])
+            keep.append(nimg)
         d.absorption = float(absorption)
         d.is_watertight = int(bool(watertight))
         d.is_double_sided = int(bool(double_sided))
@@ -174,6 +183,21 @@ class WosScene:
         check(L.wos_scene_create(C.byref(d), self.device, C.byref(h)), "wos_scene_create")
         self._h = h
         del keep
+
+    @staticmethod
+    def _image(img, box, name):
+        """A 2-D float32 image for the C ABI: (contiguous array or CUDA tensor, on_device)."""
+        if box is None or len(box) != 4:
+            raise WosError(f"{name} needs {name}_box = (x0, y0, ex, ey)")
+        if _is_torch(img) and img.is_cuda:
+            out, on_dev = img.detach().to(dtype=__import__("torch").float32).contiguous(), 1
+        else:
+            if _is_torch(img):
+                img = img.detach().cpu().numpy()
+            out, on_dev = np.ascontiguousarray(img, dtype=np.float32), 0
+        if len(out.shape) != 2:
+            raise WosError(f"{name} must be 2-D, got shape {tuple(out.shape)}")
+        return out, on_dev
 
     def set_source(self, source, stream=None):
         """Replace the source grid (-div u) in place: the geometry stays resident.

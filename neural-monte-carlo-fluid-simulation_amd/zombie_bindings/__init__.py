@@ -14,11 +14,14 @@ Differences, all deliberate (DESIGN.md "Boundary"):
 Like the reference, 2D and 3D wost solve at the query points they are given
 (createSolutionGrid(..., pts), zombie/demo/grid.h:69-102; createSolutionGrid_3d,
 zombie3d/demo/grid.h:105-146 iterates the passed points).
-bvc (boundary value caching) runs on the GPU too (2D all-Neumann scenes, the only
-kind the reference builds).
+bvc (boundary value caching) runs on the GPU too (2D scenes: Neumann and, through
+the optional Dirichlet geometry below, mixed boundaries).
 Extensions: numpy / torch inputs are accepted without nested-list conversion, a
-torch CUDA tensor of points stays on the GPU; optional scene key
-"dirichletBoundary" (OBJ) + "dirichletValue" adds Dirichlet geometry.
+torch CUDA tensor of points stays on the GPU; optional scene keys
+"dirichletBoundary" (OBJ) + "dirichletValue" add Dirichlet geometry, and
+"neumannBoundaryValue" (PFM / PNG, the upstream demo's key, scene.h:29) gives the
+Neumann data h as an image over the scene's bounding box (default h = 0, as the
+reference's pde.neumann).
 """
 import os
 
@@ -35,6 +38,31 @@ def _required(d, key):
     if key not in d:
         raise KeyError(f"Missing required setting: {key}")
     return d[key]
+
+
+# Parsed boundary meshes by (path, size, mtime, dim, flip, normalize): the time-stepper builds
+# a new Scene(sceneConfig, div) every projection (model_split.py:191) on the same OBJ, whose
+# parse would otherwise be repeated each time (the geometry's prepared device records are
+# cached by content in the library, wos_capi.hip geom_get)
+_obj_cache = {}
+
+
+def _load_boundary(path, dim, flip, normalize):
+    try:
+        st = os.stat(path)
+        key = (os.fspath(path), st.st_size, st.st_mtime_ns, dim, flip, normalize)
+    except OSError:
+        key = None  # let the parser report the missing file
+    hit = _obj_cache.get(key) if key is not None else None
+    if hit is None:
+        hit = _engine.load_obj(path, dim, flip, normalize)
+        for a in hit:
+            a.setflags(write=False)  # shared by every Scene of this mesh
+        if key is not None:
+            if len(_obj_cache) >= 16:
+                _obj_cache.pop(next(iter(_obj_cache)))
+            _obj_cache[key] = hit
+    return hit
 
 
 def _read_pfm(path):
@@ -70,16 +98,29 @@ class Scene:
             normalize = bool(config.get("normalizeDomain", False))
         else:  # scene_3d.h reads flipOrientation/normalizeDomain but never applies them
             flip, normalize = False, False
-        v, ix = _engine.load_obj(boundary, dim, flip, normalize)
+        v, ix = _load_boundary(boundary, dim, flip, normalize)
         dv = dix = None
         if config.get("dirichletBoundary"):
-            dv, dix = _engine.load_obj(config["dirichletBoundary"], dim, flip, normalize)
+            dv, dix = _load_boundary(config["dirichletBoundary"], dim, flip, normalize)
+        nkw = {}
+        if config.get("neumannBoundaryValue"):
+            if dim != 2:
+                raise ValueError("neumannBoundaryValue is 2D (zombie3d's pde.neumann is 0, scene_3d.h:108-111)")
+            # the upstream demo's Neumann image (scene.h:29,40 commented in the fork), read as
+            # pde.neumann reads it: uv = (x - bbox.pMin) / bbox.extent() (scene.h:175-181), over
+            # the FLT_EPSILON-padded box of the boundary (computeBoundingBox)
+            allv = v if dv is None else np.concatenate([v, dv])
+            eps = np.float32(np.finfo(np.float32).eps)
+            lo = (allv.min(0) - eps).astype(np.float32)
+            ext = ((allv.max(0) + eps).astype(np.float32) - lo).astype(np.float32)
+            nkw = {"neumann_image": _image.read_image(config["neumannBoundaryValue"]),
+                   "neumann_image_box": (float(lo[0]), float(lo[1]), float(ext[0]), float(ext[1]))}
         if device is None:
             device = int(os.environ.get("WOS_DEVICE", os.environ.get("LOCAL_RANK", 0)))
         self._scene = _engine.WosScene(v, ix, src, absorption, dvertices=dv, dprims=dix,
                                        dirichlet_value=float(config.get("dirichletValue", 0.0)),
                                        watertight=self.is_watertight, double_sided=self.is_double_sided,
-                                       device=device)
+                                       device=device, **nkw)
         self.bbox = self._scene.info()
         self.last_stats = None
 

@@ -1018,6 +1018,7 @@ typedef struct {
     int watertight, double_sided;
     const float *src; int sdims[3];
     const float *dimg; int ddims[2]; float dbox[4];
+    const float *nimg; int ndims[2]; float nbox[4];   /* image-valued Neumann data (NULL: h = 0) */
 } scene_t;
 
 static int scene_build(scene_t *sc, const oracle_scene_desc *d)
@@ -1049,6 +1050,13 @@ static int scene_build(scene_t *sc, const oracle_scene_desc *d)
         sc->ddims[0] = d->dirichlet_image_dims[0]; sc->ddims[1] = d->dirichlet_image_dims[1];
         for (int k = 0; k < 4; k++) sc->dbox[k] = d->dirichlet_image_box[k];
         if (!(sc->dbox[2] > 0.0f) || !(sc->dbox[3] > 0.0f)) return -1;
+    }
+    if (d->neumann_image) {
+        if (d->dim != 2 || d->neumann_image_dims[0] < 1 || d->neumann_image_dims[1] < 1) return -1;
+        sc->nimg = d->neumann_image;
+        sc->ndims[0] = d->neumann_image_dims[0]; sc->ndims[1] = d->neumann_image_dims[1];
+        for (int k = 0; k < 4; k++) sc->nbox[k] = d->neumann_image_box[k];
+        if (!(sc->nbox[2] > 0.0f) || !(sc->nbox[3] > 0.0f)) return -1;
     }
     return 0;
 }
@@ -1144,6 +1152,20 @@ static float dirichlet_value(const scene_t *sc, const float *x)
     int i = sclampi(cvt_trunc(uy * (float)h), 0, h - 1);
     int j = sclampi(cvt_trunc(ux * (float)w), 0, w - 1);
     return sc->dimg[(size_t)i * w + j];
+}
+
+/* h at a Neumann boundary sample y: the upstream demo's pde.neumann (scene.h:175-181, commented
+ * in the fork: uv = (y - bbox.pMin) / bbox.extent()) over the image's box, then Image::get
+ * (image.h:53-58); pde.neumannDoubleSided reads the same image for either side. */
+static float neumann_value(const scene_t *sc, const float *y)
+{
+    if (!sc->nimg) return 0.0f;
+    float ux = (y[0] - sc->nbox[0]) / sc->nbox[2];
+    float uy = (y[1] - sc->nbox[1]) / sc->nbox[3];
+    int h = sc->ndims[0], w = sc->ndims[1];
+    int i = sclampi(cvt_trunc(uy * (float)h), 0, h - 1);
+    int j = sclampi(cvt_trunc(ux * (float)w), 0, w - 1);
+    return sc->nimg[(size_t)i * w + j];
 }
 
 /* ------------------------------------------------------------------------- */
@@ -1471,12 +1493,15 @@ typedef struct {
 
 /* Neumann boundary sample + contribution (walk_on_stars.h:212-260).  With the
  * reference's h == 0 (scene.h:176-181) the term is exactly +0 unless G or the
- * throughput is non-finite; only then is the stochastic sample run. */
-static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float R, const float *rn)
+ * throughput is non-finite; only then is the stochastic sample run.  Image-valued
+ * h (sc->nimg) runs it at every step.  `flip`: the step flipped the walk's normal
+ * (flipNormalOrientation, double-sided scenes); `prec`: silhouettePrecision. */
+static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float R, const float *rn, int flip,
+                         float prec)
 {
     const geom_t *ng = &sc->neu;
     int nonfinite = !isfinite(st->throughput) || (g->yukawa && !g->scaled && g->muR > 85.0f);
-    if (!nonfinite || ng->np <= 0) return;
+    if ((!nonfinite && !sc->nimg) || ng->np <= 0) return;
     const float *x = st->pt;
     /* sampleNeumann: fcpw's stochastic traversal picks the primitive (randNums[0]) */
     float sel_pdf = 0.0f;
@@ -1504,6 +1529,21 @@ static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float 
     if (sc->dim == 2) dts[2] = 0.0f;
     float distToSample = norm3(dts);
     float alpha = st->onNeumann ? 2.0f : 1.0f;
+    if (sc->double_sided) {
+        /* the sample normal faces the walk (walk_on_stars.h:219-247): flipped with the walk's
+         * normal, or when the sample lies behind it beyond the precision band -- on a concave
+         * boundary (alpha 2) only when it also lies behind the walk's own normal */
+        float ds[3];
+        for (int k = 0; k < 3; k++) ds[k] = dts[k] / distToSample;
+        if (sc->dim == 2) ds[2] = 0.0f;
+        if (flip) {
+            for (int k = 0; k < 3; k++) sn[k] *= -1.0f;
+        } else if (dot3(ds, sn) < -prec) {
+            int f = 1;
+            if (alpha > 1.0f) f = dot3(ds, st->n) < -prec;
+            if (f) for (int k = 0; k < 3; k++) sn[k] *= -1.0f;
+        }
+    }
     if (pdf > 0.0f && distToSample < R) {
         /* intersectsWithNeumann (fcpw_scene_loader.h:485-499) -> hasLineOfSight (primitive.h:225-235) */
         float p1[3], p2[3], mn[3];
@@ -1518,7 +1558,7 @@ static void neumann_term(const scene_t *sc, const gfn_t *g, wstate_t *st, float 
         int occluded = ray_first_hit(ng, p1, dd, dn, &h, 1);
         if (!occluded) {
             float G = gfn_evaluate_xy(g, x, sp);
-            float hval = 0.0f;
+            float hval = neumann_value(sc, sp);
             st->totalNeumann += st->throughput * alpha * G * hval / pdf;
         }
     }
@@ -1578,7 +1618,7 @@ static int walk(const scene_t *sc, const oracle_params *prm, float dirichletDist
         if (!prm->ignore_neumann) {
             float rn[3] = {0, 0, 0};
             for (int k = 0; k < dim; k++) rn[k] = pcg_float(smp);
-            neumann_term(sc, g, st, starRadius, rn);
+            neumann_term(sc, g, st, starRadius, rn, flip, prm->silhouette_precision);
         }
         if (!prm->ignore_source) {
             float pdf, sp[3];
@@ -2265,7 +2305,9 @@ int oracle_bvc(const oracle_scene_desc *scene, const oracle_params *prm, const o
         int kind = (int)R[7], al = kind == KB_NEUMANN_ALIGNED || kind == KB_DIRICHLET_ALIGNED;
         if (kind == KB_NEUMANN || kind == KB_NEUMANN_ALIGNED) {
             R[5] = bvc_estimate(&sc, prm, R, R + 2, al, 1, bp->n_walks_solution, (uint64_t)i, 6u, &pc);
-            R[6] = 0.0f;  /* pde.neumann == 0 (scene.h:176-181) */
+            /* normalDerivative = pde.neumann(pt) (boundary_sampler.h:126-133): 0 in the reference's
+             * scenes (scene.h:176-181), the image-valued h when given */
+            R[6] = prm->ignore_neumann ? 0.0f : neumann_value(&sc, R);
             continue;
         }
         float x[3] = {R[0], R[1], 0.0f};

@@ -48,6 +48,13 @@ typedef struct oracle_scene_desc {
     const float *dirichlet_image;
     int32_t dirichlet_image_dims[2];
     float dirichlet_image_box[4];
+    /* optional image-valued Neumann data h (2D): [h][w] row-major, row ~ y, over the rectangle
+       neumann_image_box = {x0, y0, ex, ey}: h(y) = Image::get((y - x0) / ex, (y - y0) / ey) at a
+       stochastic boundary sample y (the upstream demo's pde.neumann, scene.h:175-181 commented in
+       the fork, which has h = 0); NULL: h = 0 */
+    const float *neumann_image;
+    int32_t neumann_image_dims[2];
+    float neumann_image_box[4];
 } oracle_scene_desc;
 
 typedef struct oracle_params {

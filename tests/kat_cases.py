@@ -81,6 +81,51 @@ def disk2d_dirichlet(lam=4.0, n_walks=256, npts=800, seed=3):
             "kw": {"dvertices": dv, "dprims": dix, "dirichlet_value": 1.0}}
 
 
+def disk2d_neumann_flux(lam=10.0, mode=0, n_walks=128, npts=600, seed=4, n_seg=256, img_res=2048):
+    """Unit disk (counter-clockwise polygon, n_seg sides), NON-ZERO Neumann data h, f = 0:
+    the walks' Neumann term throughput * alpha * G * h / pdf (walk_on_stars.h:212-260) carries
+    the whole solution.  mode 0: u = I0(mu r), h = mu I1(mu) (constant flux, a 1 x 1 image);
+    mode 1: u = I1(mu r) cos(theta), h = mu I1'(mu) cos(theta) = mu (I0(mu) - I1(mu)/mu) x on the
+    unit circle (a 1 x img_res image varying with x: the nearest-texel lookup is within half a
+    texel of x).  The polygon's inscribed circle lies d = 1 - cos(pi/n_seg) inside the unit
+    circle, and on a side the exact flux of u differs from the
+    segment's h by a factor within [cos(pi/n_seg), 1/cos(pi/n_seg)] (second order in pi/n_seg,
+    ~d); the texel offset (mode 1) adds |h'| ex / 2 img_res to the boundary data.  Bias bound:
+    max|grad u| (= max h) times 3 d, plus that texel term."""
+    mu = np.sqrt(lam)
+    v, ix = workloads.circle_2d((0.0, 0.0), 1.0, n_seg, clockwise=False)
+    rng = np.random.default_rng(seed)
+    r = np.sqrt(rng.uniform(0.0, 0.85 ** 2, npts))
+    t = rng.uniform(0, 2 * np.pi, npts)
+    pts = np.stack([r * np.cos(t), r * np.sin(t)], -1).astype(np.float32)
+    pmin = v.min(0) - EPS32
+    ext = (v.max(0) + EPS32) - pmin
+    box = (float(pmin[0]), float(pmin[1]), float(ext[0]), float(ext[1]))
+    i1p = special.i0(mu) - special.i1(mu) / mu
+    if mode == 0:
+        pe = special.i0(mu * r)
+        gr = mu * special.i1(mu * r)
+        grad = np.stack([gr * np.cos(t), gr * np.sin(t)], -1)
+        img = np.full((1, 1), mu * special.i1(mu), np.float32)
+        hmax, texel = mu * special.i1(mu), 0.0
+    else:
+        # u = I1(mu r) x / r: grad = (I1'(mu r) mu - I1(mu r)/r) cos t r_hat - I1(mu r)/r sin t t_hat
+        i1 = special.i1(mu * r)
+        d1 = mu * (special.i0(mu * r) - special.i1(mu * r) / np.maximum(mu * r, 1e-12))
+        pe = i1 * np.cos(t)
+        ur, ut = d1 * np.cos(t), -i1 / np.maximum(r, 1e-12) * np.sin(t)
+        grad = np.stack([ur * np.cos(t) - ut * np.sin(t), ur * np.sin(t) + ut * np.cos(t)], -1)
+        xs = pmin[0] + (np.arange(img_res) + 0.5) / img_res * ext[0]
+        img = (mu * i1p * xs).astype(np.float32)[None, :]
+        hmax, texel = mu * i1p, mu * i1p * ext[0] / (2 * img_res)
+    bias = hmax * 3.0 * (1.0 - np.cos(np.pi / n_seg)) + texel
+    solver = _solver(n_walks, ignoreSource=True, ignoreNeumann=False)
+    return {"name": f"disk2d_neumann_l{lam:g}_mode{mode}", "dim": 2, "vertices": v, "prims": ix,
+            "source": np.zeros((2, 2), np.float32), "absorption": lam, "solver": solver,
+            "output": {"boundaryDistanceMask": 1e-3}, "points": pts, "p": pe, "grad": grad, "bias": bias,
+            "kw": {"neumann_image": img, "neumann_image_box": box}}
+
+
 def cube3d(lam=350.0, m=1, n=1, l=1, n_walks=128, npts=600, res=82, seed=5, scale=1.0, robust=False):
     """scenes/cube.obj (the reference's examples/*/cube.obj, [-1,1]^3 up to 1e-6), scaled
     by `scale`, Neumann walls, f = cos(m pi (x+s)/2s) cos(n pi (y+s)/2s) cos(l pi (z+s)/2s):

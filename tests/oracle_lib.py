@@ -25,6 +25,8 @@ class SceneDesc(C.Structure):
         ("source", C.POINTER(C.c_float)), ("source_dims", C.c_int32 * 3),
         ("dirichlet_image", C.POINTER(C.c_float)), ("dirichlet_image_dims", C.c_int32 * 2),
         ("dirichlet_image_box", C.c_float * 4),
+        ("neumann_image", C.POINTER(C.c_float)), ("neumann_image_dims", C.c_int32 * 2),
+        ("neumann_image_box", C.c_float * 4),
     ]
 
 
@@ -118,8 +120,8 @@ class OracleScene:
     """Keeps numpy buffers alive for the SceneDesc pointers."""
 
     def __init__(self, vertices, prims, source, absorption, *, dvertices=None, dprims=None,
-                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, watertight=True,
-                 double_sided=False):
+                 dirichlet_value=0.0, dirichlet_image=None, dirichlet_image_box=None, neumann_image=None,
+                 neumann_image_box=None, watertight=True, double_sided=False):
         self.v = np.ascontiguousarray(vertices, dtype=np.float32)
         self.ix = np.ascontiguousarray(prims, dtype=np.int32)
         self.dim = int(self.v.shape[1])
@@ -147,6 +149,12 @@ class OracleScene:
             d.dirichlet_image_dims[0], d.dirichlet_image_dims[1] = self.dimg.shape
             for k in range(4):
                 d.dirichlet_image_box[k] = float(dirichlet_image_box[k])
+        self.nimg = None if neumann_image is None else np.ascontiguousarray(neumann_image, dtype=np.float32)
+        if self.nimg is not None:
+            d.neumann_image = _fptr(self.nimg)
+            d.neumann_image_dims[0], d.neumann_image_dims[1] = self.nimg.shape
+            for k in range(4):
+                d.neumann_image_box[k] = float(neumann_image_box[k])
         self.desc = d
 
 

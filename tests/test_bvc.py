@@ -134,6 +134,34 @@ def test_bvc_junction_kat(oracle):
     assert abs(ratio - 1.0) < 0.02 and rel < 0.04, (ratio, rel)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_bvc_neumann_flux_kat(oracle, mode):
+    """BVC with non-zero Neumann data (kat_cases.disk2d_neumann_flux, lambda 10): the Neumann
+    samples carry normalDerivative = h (boundary_sampler.h:126-133), splatted as G h - P u
+    (splatter.h:214-264); over 8 keys the field matches u = I0(mu r) (mode 0) / I1(mu r) cos(theta)
+    (mode 1) in r < 0.7: projection within 1 %, RMS < 2 %."""
+    from scipy import special
+    c = kat_cases.disk2d_neumann_flux(10.0, mode)
+    solver = dict(c["solver"], boundaryCacheSize=1024, domainCacheSize=64, nWalksForCachedSolutionEstimates=64)
+    out = {"gridRes": 32, "boundaryDistanceMask": 1e-3}
+    sc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], **c["kw"])
+    sols = [oracle.bvc(sc, oracle.make_params(solver, out, seed=0x600 + k), oracle.bvc_params(solver, out))[0]
+            for k in range(8)]
+    m = np.mean(sols, 0)
+    eps = np.float32(np.finfo(np.float32).eps)
+    lo, hi = c["vertices"].min(0) - eps, c["vertices"].max(0) + eps
+    t = np.arange(32, dtype=np.float32) / np.float32(32)
+    X, Y = np.meshgrid(t * (hi[0] - lo[0]) + lo[0], t * (hi[1] - lo[1]) + lo[1], indexing="ij")
+    X, Y = X.astype(np.float64), Y.astype(np.float64)
+    r, th = np.sqrt(X ** 2 + Y ** 2), np.arctan2(Y, X)
+    mu = np.sqrt(10.0)
+    pe = special.i0(mu * r) if mode == 0 else special.i1(mu * r) * np.cos(th)
+    sel = r < 0.7
+    ratio = float((m[sel] * pe[sel]).sum() / (pe[sel] ** 2).sum())
+    rel = float(np.sqrt(np.mean((m[sel] - pe[sel]) ** 2)) / np.sqrt(np.mean(pe[sel] ** 2)))
+    assert abs(ratio - 1.0) < 0.01 and rel < 0.02, (ratio, rel)
+
+
 def test_bvc_rejects_3d(oracle):
     from wos_amd import workloads
     cfg = workloads.cube_config(res=8, n_walks=8)

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert wos_amd.load_library().wos_abi_version() == wos_amd._lib.ABI_VERSION == 8
+    assert wos_amd.load_library().wos_abi_version() == wos_amd._lib.ABI_VERSION == 9
 
 
 @pytest.mark.parametrize("path,dim", [(workloads.KARMAN_OBJ, 2), (workloads.SQUARE_OBJ, 2), (workloads.CUBE_OBJ, 3)])

@@ -138,6 +138,27 @@ def test_bvc_junction_bit_exact_and_kat(gpu, oracle):
     assert abs(ratio - 1.0) < 0.02 and rel < 0.04, (ratio, rel)
 
 
+def test_bvc_neumann_data_bit_exact(gpu, oracle):
+    """BVC with image-valued Neumann data (ABI 9): a Neumann sample's normal derivative is
+    pde.neumann at its point (boundary_sampler.h:126-133) and the boundary-start walks carry
+    the Neumann term -- samples, solution and gradient GPU == oracle bit for bit (the flux
+    disk of kat_cases, reduced cache and walk counts)."""
+    import kat_cases
+    c = kat_cases.disk2d_neumann_flux(10.0, 1)
+    solver = dict(c["solver"], boundaryCacheSize=256, domainCacheSize=64, nWalksForCachedSolutionEstimates=16)
+    out = {"gridRes": 16, "boundaryDistanceMask": 1e-3}
+    sc = WosScene(c["vertices"], c["prims"], c["source"], c["absorption"], watertight=True, **c["kw"])
+    osc = oracle.OracleScene(c["vertices"], c["prims"], c["source"], c["absorption"], **c["kw"])
+    sol, grad, info = sc.bvc(solver_params(solver, out), bvc_params(solver, out))
+    osol, ograd, osmp, _, _ = oracle.bvc(osc, oracle.make_params(solver, out), oracle.bvc_params(solver, out))
+    sc.close()
+    kinds = info["samples"][:, 7]
+    assert (kinds == 0).sum() > 0 and np.abs(info["samples"][kinds == 0, 6]).max() > 0  # h carried
+    _bits(info["samples"], osmp)
+    _bits(sol, osol)
+    _bits(grad, ograd)
+
+
 def test_bvc_dirichlet_disk_kat_gpu(gpu):
     """The oracle's Dirichlet-disk BVC KAT (tests/test_bvc.py) on the HIP path: u = I0(2r)/I0(2)."""
     import kat_cases

@@ -33,6 +33,9 @@ CASES = {
     "lshape2d_l350_m1n2": lambda: kat_cases.lshape2d(350.0, 1, 2),
     "lprism3d_l50_m111": lambda: kat_cases.lprism3d(50.0, 1, 1, 1),
     "lprism3d_l350_m210": lambda: kat_cases.lprism3d(350.0, 2, 1, 0),
+    # non-zero Neumann data h (image-valued, ABI 9): the solution comes from the Neumann term
+    "disk2d_neumann_l10_mode0": lambda: kat_cases.disk2d_neumann_flux(10.0, 0),
+    "disk2d_neumann_l10_mode1": lambda: kat_cases.disk2d_neumann_flux(10.0, 1),
 }
 
 

@@ -225,6 +225,52 @@ def test_double_sided_bit_exact(gpu, oracle, dim):
     _compare(oracle, osc, sc, cfg, pts)
 
 
+def _h_image(v, res=(37, 53)):
+    """A smooth, sign-changing Neumann image over the padded bbox of `v` (rows ~ y)."""
+    eps = np.float32(np.finfo(np.float32).eps)
+    pmin = v.min(0) - eps
+    ext = (v.max(0) + eps) - pmin
+    y, x = np.meshgrid(np.linspace(0, 1, res[0]), np.linspace(0, 1, res[1]), indexing="ij")
+    img = (np.sin(5 * x + 1) * np.cos(3 * y) + 0.3).astype(np.float32)
+    return img, (float(pmin[0]), float(pmin[1]), float(ext[0]), float(ext[1]))
+
+
+@pytest.mark.parametrize("case", ["disk", "karman", "karman_double_sided", "lshape"])
+def test_neumann_data_bit_exact(gpu, oracle, case):
+    """Image-valued Neumann data h (ABI 9): the walks' Neumann term at every step -- fcpw's
+    stochastic boundary sample, the line-of-sight test, G, h at the sample
+    (walk_on_stars.h:212-260), and in double-sided scenes the sample normal's flips
+    (:219-247) -- GPU == oracle bit for bit: the flux disk KAT scene, karman (Yukawa
+    lambda 350, the walk kernel with the Neumann term on), karman double-sided, the L."""
+    import kat_cases
+    if case == "disk":
+        c = kat_cases.disk2d_neumann_flux(10.0, 1, npts=300, n_walks=32)
+        v, ix, src, lam, kw = c["vertices"], c["prims"], c["source"], c["absorption"], dict(c["kw"])
+        cfg, pts, ds = {"solver": c["solver"], "output": c["output"]}, c["points"], False
+    elif case == "lshape":
+        c = kat_cases.lshape2d(10.0, 2, 1)
+        v, ix, src, lam = c["vertices"], c["prims"], c["source"], c["absorption"]
+        img, box = _h_image(v)
+        kw = {"neumann_image": img, "neumann_image_box": box}
+        cfg, pts, ds = {"solver": c["solver"], "output": c["output"]}, c["points"][:400], False
+    else:
+        cfg = workloads.karman_config(n_walks=32)
+        v, ix = objparse.load(cfg["obj"], 2)
+        src, lam = cfg["source"], float(cfg["scene"]["absorptionCoeff"])
+        img, box = _h_image(v)
+        kw = {"neumann_image": img, "neumann_image_box": box}
+        pts, ds = cfg["points"][:1024], case == "karman_double_sided"
+    osc = oracle.OracleScene(v, ix, src, lam, watertight=True, double_sided=ds, **kw)
+    sc = WosScene(v, ix, src, lam, watertight=True, double_sided=ds, **kw)
+    p1, g1, _ = _compare(oracle, osc, sc, cfg, pts)
+    # the term is live: h = 0 gives a different field
+    sc0 = WosScene(v, ix, src, lam, watertight=True, double_sided=ds)
+    p0, _, _ = sc0.solve(pts, solver_params(cfg["solver"], cfg["output"], seed=0x5EED0001))
+    assert np.abs(p1 - p0).max() > 0
+    sc.close()
+    sc0.close()
+
+
 @pytest.mark.parametrize("which", ["lshape2d", "lprism3d"])
 def test_nonconvex_l_bit_exact(gpu, oracle, which):
     """The non-convex KAT scenes (kat_cases.lshape2d / lprism3d): the reflex vertex /

@@ -119,6 +119,37 @@ def test_scene_dict_image_equals_matrix_scene(gpu, tmp_path, fmt):
 
 
 @pytest.mark.gpu
+def test_scene_neumann_image_key(gpu, tmp_path):
+    """Scene key "neumannBoundaryValue" (the upstream demo's Neumann image, scene.h:29): read
+    like the source image, laid over the scene's padded bounding box (pde.neumann's uv,
+    scene.h:175-181); equals WosScene with the same image and box bit for bit, and differs
+    from h = 0."""
+    from wos_amd import WosScene, solver_params
+    scene_cfg, solver, output = _configs()
+    cfg = workloads.karman_config(n_walks=32)
+    img = (np.linspace(-1.0, 1.0, 24 * 40, dtype=np.float32).reshape(24, 40)) ** 3
+    path = tmp_path / "h.pfm"
+    with open(path, "wb") as f:
+        f.write(b"Pf\n40 24\n-1\n" + img.astype("<f4").tobytes())
+    sc = zombie_bindings.Scene(dict(scene_cfg, neumannBoundaryValue=str(path)), cfg["source"])
+    bb = sc.bbox
+    lo, hi = np.array(bb["bbox_min"], np.float32), np.array(bb["bbox_max"], np.float32)
+    pts = cfg["points"][:256]
+    _, p1, g1 = zombie_bindings.wost(sc, solver, output, pts, return_numpy=True)
+    v, ix = zombie_bindings._load_boundary(scene_cfg["boundary"], 2, bool(scene_cfg.get("flipOrientation", False)),
+                                           bool(scene_cfg.get("normalizeDomain", False)))
+    ws = WosScene(v, ix, cfg["source"], float(scene_cfg["absorptionCoeff"]), watertight=sc.is_watertight,
+                  neumann_image=img, neumann_image_box=(lo[0], lo[1], (hi - lo)[0], (hi - lo)[1]))
+    p2, g2, _ = ws.solve(pts, solver_params(solver, output))
+    ws.close()
+    np.testing.assert_array_equal(p1, p2)
+    np.testing.assert_array_equal(g1, g2)
+    _, p0, _ = zombie_bindings.wost(zombie_bindings.Scene(scene_cfg, cfg["source"]), solver, output, pts,
+                                    return_numpy=True)
+    assert np.abs(p1 - p0).max() > 0
+
+
+@pytest.mark.gpu
 def test_wost_end_to_end_like_model_split(gpu):
     """model_split.py:185-202: Scene(sceneConfig, div) then wost(...) -> (samples, p, grad)."""
     scene_cfg, solver, output = _configs()

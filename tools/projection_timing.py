@@ -72,7 +72,51 @@ def projection_timings(steps=10, n_walks=128):
     st = keep.last_stats
     res["kernel_ms"] = st["kernel_ms"]
     res["walk_steps"] = st["walk_steps"]
+    res["device_handoff_breakdown"] = handoff_breakdown(steps, scene_cfg, solver, output, div_t, pts_t)
     return res
+
+
+def handoff_breakdown(steps, scene_cfg, solver, output, div_t, pts_t):
+    """device_fresh_scene_ms itemised: the stages of one Scene(cfg, div CUDA) + wost(CUDA
+    points) call, each bracketed by host clocks in one call (median over `steps` calls):
+    OBJ parse (a fresh parse; Scene() itself takes the cached one), scene create (host prep
+    from the geometry cache + source copy), solver-parameter parsing, the solve's enqueue,
+    the wait for its completion, the statistics read-back and the scene's destruction;
+    `gpu_kernel_ms` is the solve's first-to-last kernel time on the device clock."""
+    from wos_amd import engine
+    path = scene_cfg["boundary"]
+    flip = bool(scene_cfg.get("flipOrientation", False))
+    norm = bool(scene_cfg.get("normalizeDomain", False))
+    keys = ["obj_parse_ms", "obj_cached_ms", "scene_create_ms", "params_ms", "enqueue_ms", "gpu_wait_ms",
+            "stats_ms", "destroy_ms", "sum_ms", "gpu_kernel_ms"]
+    rows = []
+    for it in range(steps + 1):
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        engine.load_obj(path, 2, flip, norm)
+        t.append(time.perf_counter())
+        zombie_bindings._load_boundary(path, 2, flip, norm)
+        t.append(time.perf_counter())
+        sc = zombie_bindings.Scene(scene_cfg, div_t)
+        t.append(time.perf_counter())
+        prm = engine.solver_params(solver, output)
+        t.append(time.perf_counter())
+        _, _, st = sc._scene.solve(pts_t, prm, sync=False)
+        t.append(time.perf_counter())
+        torch.cuda.current_stream().synchronize()
+        t.append(time.perf_counter())
+        full = sc._scene.solve_stats(st["ticket"])
+        t.append(time.perf_counter())
+        sc._scene.close()
+        t.append(time.perf_counter())
+        if it:
+            d = [(t[k + 1] - t[k]) * 1e3 for k in range(len(t) - 1)]
+            rows.append(d + [sum(d) - d[0], full["kernel_ms"]])
+    med = np.median(np.asarray(rows), 0)
+    out = {k: float(v) for k, v in zip(keys, med)}
+    out["note"] = ("sum_ms = obj_cached + scene_create + params + enqueue + gpu_wait + stats + destroy "
+                   "(what one Scene + wost call costs; obj_parse_ms is the uncached parse, shown for reference)")
+    return out
 
 
 def pipeline_timings(steps=5, n_points=65536, n_walks=128, vis_resolution=1000):

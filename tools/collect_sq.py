@@ -55,7 +55,7 @@ def main():
            sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", CONFIG, "--no-cpu-baseline",
            "--no-projection-wall", "--no-strong"]
     subprocess.run(cmd, check=True, cwd=REPO, env=dict(os.environ, TMPDIR="/tmp"),
-                   stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=150)
+                   stdout=open(os.path.join(OUT, "log.txt"), "w"), stderr=subprocess.STDOUT, timeout=280)
     per, dur, kname = {}, {}, {}
     for f in glob.glob(os.path.join(OUT, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):

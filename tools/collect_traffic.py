@@ -26,8 +26,7 @@ from bench import lib_sha16  # noqa: E402
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 CONFIG = sys.argv[2] if len(sys.argv) > 2 else "B"
-OUT = os.path.join(REPO, "gpurun_out", "traffic")
-POINTS, WALKS = 65536, 128
+OUT = os.path.join(REPO, "gpurun_out", f"traffic_{TAG}")  # per tag: the csv glob below must see only this run
 
 
 def run_pass(counter):
@@ -54,7 +53,7 @@ def main():
     write_kib, nw = run_pass("WRITE_SIZE")
     raw = (fetch_kib + write_kib) * 1024.0
     res = {
-        "points": POINTS, "walks": WALKS, "config": CONFIG, "lib_sha16": lib_sha16(), "kernel": "wos_walk_kernel",
+        "config": CONFIG, "lib_sha16": lib_sha16(), "kernel": "wos_walk_kernel",
         "fetch_bytes": fetch_kib * 1024.0, "write_bytes": write_kib * 1024.0, "dispatches": [nf, nw],
         "bytes_per_launch": raw,
         "bytes_per_launch_fetch_x2": 2.0 * fetch_kib * 1024.0 + write_kib * 1024.0,

@@ -44,7 +44,7 @@ from wos_amd import dist as wdist  # noqa: E402  (pure Python: no library load a
 HBM_PEAK_GBS = 8000.0
 FP32_VECTOR_PEAK_TFLOPS = 157.3
 FP64_VECTOR_PEAK_TFLOPS = 78.6
-LIB = os.path.join(PKG, "lib", "libwos_hip.so")
+LIB = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG, "lib", "libwos_hip.so")  # the library wos_amd loads
 
 
 def parse():

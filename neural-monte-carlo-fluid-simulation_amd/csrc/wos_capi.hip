@@ -1024,6 +1024,9 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   // config C neutral); 3D pays more for the extra live state than its short tails return
   // (profiles/r4zc_*, r4ze_*)
   dp.tail_spread = (dim == 2 && !dp.robust && !dsc.geom_global && !(prm->schedule & WOS_SCHED_NO_TAIL_SPREAD)) ? 1 : 0;
+#ifdef WOS_ACCT_NOSPREAD
+  dp.tail_spread = 0;  // HBM-accounting build: the walk kernel without tail spreading (no scratch)
+#endif
   const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
   const int64_t n_chunks = n > 0 ? (n + chunk - 1) / chunk : 0;
   int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;

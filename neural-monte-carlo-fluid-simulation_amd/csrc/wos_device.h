@@ -988,10 +988,38 @@ __device__ __forceinline__ void offset_point(const float* p, const float* n, flo
   }
 }
 
+// Cost probes (never shipped; tools/build_variant.sh): WOS_PROBE bit k evaluates one piece of
+// the walk step a second time on opaque copies of its inputs, results sunk -- the walks are
+// unchanged, so the kernel's SQ_INSTS_VALU and time minus the base build's are that piece's
+// dynamic instruction count and cost.  1: update_ball's Bessels (2D), 2: the direction-
+// sampled Poisson kernel's Bessels (2D), 4: a cooperative rejection item (draws + fast test).
+#ifndef WOS_PROBE
+#define WOS_PROBE 0
+#endif
+template <class T>
+__device__ __forceinline__ T probe_opaque(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void probe_sink(T v) {
+  asm volatile("" ::"v"(v));
+}
+
+// HBM-accounting builds (never shipped, wrong results; tools/build_variant.sh): the walk kernel
+// without its source-texel loads (WOS_ACCT_NOTEX) or its record stores (WOS_ACCT_NOREC) -- the
+// walks themselves are unchanged -- so differences of the PMC traffic attribute its bytes
+#ifndef WOS_ACCT_NOTEX
+#define WOS_ACCT_NOTEX 0
+#endif
+#ifndef WOS_ACCT_NOREC
+#define WOS_ACCT_NOREC 0
+#endif
+
 // PDE source lookup: scene.h:194-198 + image.h:53-58 (2D), scene_3d.h:120-126 (3D)
 template <int DIM>
 __device__ __forceinline__ float source_value(const DevScene& sc, const float* x) {
-  if (sc.source == nullptr) return 0.0f;
+  if (sc.source == nullptr || WOS_ACCT_NOTEX) return 0.0f;
   if constexpr (DIM == 2) {
     float ux = (x[0] - sc.pmin[0]) / sc.ext[0];
     float uy = (x[1] - sc.pmin[1]) / sc.ext[1];
@@ -1054,6 +1082,152 @@ __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x)
 }
 
 // float Bessel approximations (defined with the certified rejection fast path below)
+// ---- certified fast Bessel members (2D Yukawa) -------------------------------------
+// The reference stores K0, I0, K1, I1 at mu R as floats rounded from its double A&S
+// evaluation (distributions.h:581-588 -> bessel.hpp:373-555).  bessel_ik_fast evaluates the
+// same formulas with cheaper pieces -- FMA Horner, a 13-term Taylor exp after Cody-Waite
+// reduction, fdlibm's log with a Newton reciprocal instead of its division, hardware
+// reciprocal / rsqrt estimates refined by Newton steps, exp(-x) as 1/exp(x) -- accurate
+// to a few 1e-14 of the double value the reference computes (both ~20 roundings, the K
+// sums at x <= 2 conditioned <= 6).  A value is certified when v (1 - tol) and v (1 + tol)
+// round to the same float: the reference's double value lies between them and rounding
+// is monotone, so its float equals ours.  Uncertain lanes (P ~ 1e-5 per value) and
+// arguments outside [1e-6, 80] take the exact bessel_ik.  Results are bit-identical.
+#ifndef WOS_FAST_BESSEL
+#define WOS_FAST_BESSEL 1
+#endif
+constexpr double kFastBesselTol = 1e-13;
+constexpr float kFastBesselLo = 1e-6f, kFastBesselHi = 80.0f;
+
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double fast_rsqrt(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  for (int i = 0; i < 2; i++) {
+    const double h = (x * y) * y;
+    y = y * __builtin_fma(-0.5, h, 1.5);
+  }
+  return y;
+}
+// e^x, |x| <= 88
+__device__ __forceinline__ double fast_exp(double x) {
+  const double kd = __builtin_rint(x * 1.44269504088896338700e+00);
+  double r = __builtin_fma(-kd, 6.93147180369123816490e-01, x);
+  r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);
+  double p = 2.08767569878680989792e-09;  // 1/12!, then Horner down to 1 (|r| <= 0.347: 2e-16)
+  p = __builtin_fma(p, r, 2.50521083854417187751e-08);
+  p = __builtin_fma(p, r, 2.75573192239858906526e-07);
+  p = __builtin_fma(p, r, 2.75573192239858906526e-06);
+  p = __builtin_fma(p, r, 2.48015873015873015873e-05);
+  p = __builtin_fma(p, r, 1.98412698412698412698e-04);
+  p = __builtin_fma(p, r, 1.38888888888888888889e-03);
+  p = __builtin_fma(p, r, 8.33333333333333333333e-03);
+  p = __builtin_fma(p, r, 4.16666666666666666667e-02);
+  p = __builtin_fma(p, r, 1.66666666666666666667e-01);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)kd);
+}
+// log(x), x a positive normal double: dlog's reduction and polynomial (fdlibm) with
+// f / (2 + f) by a Newton reciprocal
+__device__ __forceinline__ double fast_log(double x) {
+  const uint64_t u = double_to_bits(x);
+  int e = (int)((u >> 52) & 0x7ff) - 1023;
+  double m = bits_to_double((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
+  if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+  const double f = m - 1.0;
+  const double s = f * fast_rcp(2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * __builtin_fma(w, __builtin_fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
+                                      3.999999999940941908e-01);
+  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, 1.479819860511658591e-01,
+                                                                         1.818357216161805012e-01),
+                                                       2.857142874366239149e-01),
+                                      6.666666666666735130e-01);
+  const double hfsq = 0.5 * f * f, dk = (double)e;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + t1 + t2) + dk * 1.90821492927058770002e-10)) - f);
+}
+__device__ __forceinline__ bool fast_certain(double v) {
+  const float f = (float)v;
+  return (float)(v * (1.0 - kFastBesselTol)) == f && (float)(v * (1.0 + kFastBesselTol)) == f;
+}
+// N0: K0, I0; N1: K1, I1 at x in [kFastBesselLo, kFastBesselHi], rounded to float; false when a
+// value is not certified (then call bessel_ik)
+template <bool N0, bool N1>
+__device__ __forceinline__ bool bessel_ik_fast(double x, float* i0, float* k0, float* i1, float* k1) {
+  double vi0 = 0.0, vi1 = 0.0, vk0 = 0.0, vk1 = 0.0;
+  double ex = 0.0, rsx = 0.0;  // e^x, 1/sqrt(x) (shared by the two large-x branches)
+  if (x > 2.0) { ex = fast_exp(x); rsx = fast_rsqrt(x); }
+  if (x < 3.75) {
+    double y = x * (1.0 / 3.75);
+    y = y * y;
+    if (N0)
+      vi0 = __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, 0.45813e-2, 0.360768e-1), 0.2659732), 1.2067492), 3.0899424), 3.5156229), 1.0);
+    if (N1)
+      vi1 = x * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, 0.32411e-3, 0.301532e-2), 0.2658733e-1), 0.15084934), 0.51498869), 0.87890594), 0.5);
+  } else {
+    const double y = 3.75 * fast_rcp(x);
+    const double e = ex * rsx;
+    if (N0)
+      vi0 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, 0.392377e-2, -0.1647633e-1), 0.2635537e-1),
+              -0.2057706e-1), 0.916281e-2), -0.157565e-2), 0.225319e-2), 0.1328592e-1), 0.39894228);
+    if (N1) {
+      double a = __builtin_fma(y, __builtin_fma(y, __builtin_fma(-y, 0.420059e-2, 0.1787654e-1), -0.2895312e-1),
+                               0.2282967e-1);
+      a = __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, a, -0.1031555e-1),
+                                                                          0.163801e-2), -0.362018e-2), -0.3988024e-1),
+                        0.39894228);
+      vi1 = a * e;
+    }
+  }
+  if (x <= 2.0) {
+    const double y = (x * x) * 0.25;
+    const double l = fast_log(x * 0.5);
+    if (N0)
+      vk0 = __builtin_fma(-l, vi0, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, __builtin_fma(y, 0.74e-5, 0.10750e-3), 0.262698e-2), 0.3488590e-1), 0.23069756),
+              0.42278420), -0.57721566));
+    if (N1)
+      vk1 = __builtin_fma(l, vi1, fast_rcp(x) * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, __builtin_fma(y, -0.4686e-4, -0.110404e-2), -0.1919402e-1), -0.18156897),
+              -0.67278579), 0.15443144), 1.0));
+  } else {
+    const double y = 2.0 * fast_rcp(x);
+    const double e = fast_rcp(ex) * rsx;
+    if (N0)
+      vk0 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, 0.53208e-3, -0.251540e-2), 0.587872e-2), -0.1062446e-1), 0.2189568e-1), -0.7832358e-1),
+              1.25331414);
+    if (N1)
+      vk1 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+              __builtin_fma(y, -0.68245e-3, 0.325614e-2), -0.780353e-2), 0.1504268e-1), -0.3655620e-1), 0.23498619),
+              1.25331414);
+  }
+  bool ok = true;
+  if (N0) { ok = ok && fast_certain(vi0) && fast_certain(vk0); *i0 = (float)vi0; *k0 = (float)vk0; }
+  if (N1) { ok = ok && fast_certain(vi1) && fast_certain(vk1); *i1 = (float)vi1; *k1 = (float)vk1; }
+  return ok;
+}
+
+// the exact evaluation (bessel_ik) rounded to float, for the lanes the fast path cannot certify:
+// out of line, so the throughput path keeps its registers
+struct F4 { float i0, k0, i1, k1; };
+template <bool N0, bool N1>
+__device__ __attribute__((noinline)) F4 bessel_ik_exact_f(double x) {
+  double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
+  bessel_ik<N0, N1>(x, N0 ? &a : nullptr, N0 ? &b : nullptr, N1 ? &c : nullptr, N1 ? &d : nullptr);
+  return F4{(float)a, (float)b, (float)c, (float)d};
+}
+
 __device__ __forceinline__ float i0_fast(float x);
 __device__ __forceinline__ float k0_fast(float x);
 __device__ __forceinline__ float i1_fast(float x);
@@ -1187,8 +1361,24 @@ struct Gfn {
       return;
     }
     if constexpr (DIM == 2) {
+      if (WOS_FAST_BESSEL) {
+        float fi0 = 0.0f, fk0 = 0.0f, fi1 = 0.0f, fk1 = 0.0f;
+        const bool ok = muR >= kFastBesselLo && muR <= kFastBesselHi &&
+                        bessel_ik_fast<true, true>((double)muR, &fi0, &fk0, &fi1, &fk1);
+        if (!ok) {
+          const F4 e = bessel_ik_exact_f<true, true>((double)muR);
+          fi0 = e.i0; fk0 = e.k0; fi1 = e.i1; fk1 = e.k1;
+        }
+        A0 = fk0; A1 = fi0; B0 = fk1; B1 = fi1;
+        return;
+      }
       double i0, k0, i1, k1;
       bessel_ik<true, true>((double)muR, &i0, &k0, &i1, &k1);
+      if (WOS_PROBE & 1) {
+        double p0, p1, p2, p3;
+        bessel_ik<true, true>(probe_opaque((double)muR), &p0, &p1, &p2, &p3);
+        probe_sink(p0); probe_sink(p1); probe_sink(p2); probe_sink(p3);
+      }
       A0 = (float)k0;
       A1 = (float)i0;
       B0 = (float)k1;
@@ -1327,9 +1517,21 @@ struct Gfn {
         // the ball update already evaluated -- the same double values, rounded the same
         K1mur = B0;
         I1mur = B1;
+      } else if (WOS_FAST_BESSEL) {
+        const bool ok = mur >= kFastBesselLo && mur <= kFastBesselHi &&
+                        bessel_ik_fast<false, true>((double)mur, nullptr, nullptr, &I1mur, &K1mur);
+        if (!ok) {
+          const F4 e = bessel_ik_exact_f<false, true>((double)mur);
+          I1mur = e.i1; K1mur = e.k1;
+        }
       } else {
         double i1, k1;
         bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
+        if (WOS_PROBE & 2) {
+          double p1, p2;
+          bessel_ik<false, true>(probe_opaque((double)mur), nullptr, nullptr, &p1, &p2);
+          probe_sink(p1); probe_sink(p2);
+        }
         K1mur = (float)k1;
         I1mur = (float)i1;
       }
@@ -1985,6 +2187,12 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           if (j < kRejMax) {
             const uint64_t st = rej_state(prm, L->s0[owner], j);
             const float u = draw_float(st);
+            if (WOS_PROBE & 4) {
+              const uint64_t st2 = rej_state(prm, probe_opaque(L->s0[owner]), probe_opaque(j));
+              const float u2 = draw_float(st2), x2 = draw_float(st2 * kPcgMult + kPcgInc);
+              if constexpr (DIM == 2)
+                probe_sink(rej_fast_decide(u2, x2 * L->R[owner], L->sqrtL[owner], L->c0[owner], L->c1[owner]));
+            }
             int dcs = 0;
             DIAG_LANE(D_RITEMS);
             if (u > L->qb[owner]) {
@@ -3704,9 +3912,10 @@ __device__ __forceinline__ void walk_finish(const DevScene& sc, const DevParams&
   const bool recorded = code == WC_DIRICHLET || code == WC_RR;
   if (recorded) {
     const float term = (code == WC_DIRICHLET && !prm.ignore_dirichlet) ? dirichlet_value<DIM>(sc, st.pt) : 0.0f;
-    tk.total[t] = st.throughput * term + st.totalNeumann + st.totalSource;
+    const float tot = st.throughput * term + st.totalNeumann + st.totalSource;
+    if (!WOS_ACCT_NOREC) tk.total[t] = tot;
   }
-  tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
+  if (!WOS_ACCT_NOREC) tk.code[t] = (wsteps << 1) | (recorded ? 1u : 0u);
   DIAG_MAX(D_WMAXLEN, wsteps);
   atomicAdd(&s_ctr[recorded ? C_STEPS : C_WASTED], wsteps);
   atomicAdd(&s_ctr[code == WC_DIRICHLET ? C_DIR : code == WC_RR ? C_RR : code == WC_ESCAPED ? C_ESC : C_MAXL], 1u);

@@ -1096,8 +1096,58 @@ __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x)
 #ifndef WOS_FAST_BESSEL
 #define WOS_FAST_BESSEL 1
 #endif
+#ifndef WOS_FAST_BESSEL_PK
+#define WOS_FAST_BESSEL_PK 1  // also the direction-sampled Poisson kernel's K1, I1
+#endif
 constexpr double kFastBesselTol = 1e-13;
 constexpr float kFastBesselLo = 1e-6f, kFastBesselHi = 80.0f;
+
+// The fast path's double constants live in LDS (s_fbc, staged by stage_fast_bessel in the walk
+// kernel, the only caller): as literals each would be two s_mov_b32 into an SGPR pair at its
+// use (VOP3 takes no 64-bit literal), and the walk kernel's SGPRs are already spilled to VGPR
+// lanes -- measured: literals pushed its scratch from 0 to ~500 B per lane.
+enum {
+  FB_EXP = 0,       // 1/12!, 1/11!, ..., 1/2!, 1, 1 (13)
+  FB_LN2HI = 13, FB_LN2LO = 14, FB_INVLN2 = 15,
+  FB_LG = 16,       // Lg1..Lg7
+  FB_I0S = 23,      // I0, x < 3.75: 0.45813e-2 ... 3.5156229, 1 (7, highest first)
+  FB_I1S = 30,      // I1, x < 3.75 (7)
+  FB_I0L = 37,      // I0, x >= 3.75 (9)
+  FB_I1L = 46,      // I1, x >= 3.75: inner 4, outer 6
+  FB_K0S = 56,      // K0, x <= 2 (7)
+  FB_K1S = 63,      // K1, x <= 2 (7)
+  FB_K0L = 70,      // K0, x > 2 (7)
+  FB_K1L = 77,      // K1, x > 2 (7)
+  FB_MISC = 84,     // 1/3.75, 3.75, sqrt(2), 1 - tol, 1 + tol
+  FB_N = 89
+};
+static __shared__ double s_fbc[FB_N];
+__host__ __device__ constexpr double fb_const(int k) {
+  constexpr double t[FB_N] = {
+      2.08767569878680989792e-09, 2.50521083854417187751e-08, 2.75573192239858906526e-07,
+      2.75573192239858906526e-06, 2.48015873015873015873e-05, 1.98412698412698412698e-04,
+      1.38888888888888888889e-03, 8.33333333333333333333e-03, 4.16666666666666666667e-02,
+      1.66666666666666666667e-01, 0.5, 1.0, 1.0,
+      6.93147180369123816490e-01, 1.90821492927058770002e-10, 1.44269504088896338700e+00,
+      6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01, 2.222219843214978396e-01,
+      1.818357216161805012e-01, 1.531383769920937332e-01, 1.479819860511658591e-01,
+      0.45813e-2, 0.360768e-1, 0.2659732, 1.2067492, 3.0899424, 3.5156229, 1.0,
+      0.32411e-3, 0.301532e-2, 0.2658733e-1, 0.15084934, 0.51498869, 0.87890594, 0.5,
+      0.392377e-2, -0.1647633e-1, 0.2635537e-1, -0.2057706e-1, 0.916281e-2, -0.157565e-2, 0.225319e-2,
+      0.1328592e-1, 0.39894228,
+      -0.420059e-2, 0.1787654e-1, -0.2895312e-1, 0.2282967e-1,
+      -0.1031555e-1, 0.163801e-2, -0.362018e-2, -0.3988024e-1, 0.39894228, 0.0,
+      0.74e-5, 0.10750e-3, 0.262698e-2, 0.3488590e-1, 0.23069756, 0.42278420, -0.57721566,
+      -0.4686e-4, -0.110404e-2, -0.1919402e-1, -0.18156897, -0.67278579, 0.15443144, 1.0,
+      0.53208e-3, -0.251540e-2, 0.587872e-2, -0.1062446e-1, 0.2189568e-1, -0.7832358e-1, 1.25331414,
+      -0.68245e-3, 0.325614e-2, -0.780353e-2, 0.1504268e-1, -0.3655620e-1, 0.23498619, 1.25331414,
+      1.0 / 3.75, 3.75, 1.4142135623730951, 1.0 - kFastBesselTol, 1.0 + kFastBesselTol};
+  return t[k];
+}
+__device__ __forceinline__ void stage_fast_bessel() {
+  for (int i = threadIdx.x; i < FB_N; i += blockDim.x) s_fbc[i] = fb_const(i);
+}
+#define FBC(k) s_fbc[k]
 
 __device__ __forceinline__ double fast_rcp(double x) {
   double r = __builtin_amdgcn_rcp(x);
@@ -1114,25 +1164,20 @@ __device__ __forceinline__ double fast_rsqrt(double x) {
   }
   return y;
 }
-// e^x, |x| <= 88
+// Horner from LDS: c[0] x^(n-1) + ... + c[n-1]
+template <int N>
+__device__ __forceinline__ double fb_poly(double x, int base) {
+  double p = FBC(base);
+#pragma unroll
+  for (int k = 1; k < N; k++) p = __builtin_fma(p, x, FBC(base + k));
+  return p;
+}
+// e^x, |x| <= 88 (Cody-Waite reduction, 13-term Taylor: |r| <= 0.347, 2e-16)
 __device__ __forceinline__ double fast_exp(double x) {
-  const double kd = __builtin_rint(x * 1.44269504088896338700e+00);
-  double r = __builtin_fma(-kd, 6.93147180369123816490e-01, x);
-  r = __builtin_fma(-kd, 1.90821492927058770002e-10, r);
-  double p = 2.08767569878680989792e-09;  // 1/12!, then Horner down to 1 (|r| <= 0.347: 2e-16)
-  p = __builtin_fma(p, r, 2.50521083854417187751e-08);
-  p = __builtin_fma(p, r, 2.75573192239858906526e-07);
-  p = __builtin_fma(p, r, 2.75573192239858906526e-06);
-  p = __builtin_fma(p, r, 2.48015873015873015873e-05);
-  p = __builtin_fma(p, r, 1.98412698412698412698e-04);
-  p = __builtin_fma(p, r, 1.38888888888888888889e-03);
-  p = __builtin_fma(p, r, 8.33333333333333333333e-03);
-  p = __builtin_fma(p, r, 4.16666666666666666667e-02);
-  p = __builtin_fma(p, r, 1.66666666666666666667e-01);
-  p = __builtin_fma(p, r, 0.5);
-  p = __builtin_fma(p, r, 1.0);
-  p = __builtin_fma(p, r, 1.0);
-  return __builtin_ldexp(p, (int)kd);
+  const double kd = __builtin_rint(x * FBC(FB_INVLN2));
+  double r = __builtin_fma(-kd, FBC(FB_LN2HI), x);
+  r = __builtin_fma(-kd, FBC(FB_LN2LO), r);
+  return __builtin_ldexp(fb_poly<13>(r, FB_EXP), (int)kd);
 }
 // log(x), x a positive normal double: dlog's reduction and polynomial (fdlibm) with
 // f / (2 + f) by a Newton reciprocal
@@ -1140,77 +1185,53 @@ __device__ __forceinline__ double fast_log(double x) {
   const uint64_t u = double_to_bits(x);
   int e = (int)((u >> 52) & 0x7ff) - 1023;
   double m = bits_to_double((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
-  if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+  if (m > FBC(FB_MISC + 2)) { m = m * 0.5; e += 1; }
   const double f = m - 1.0;
   const double s = f * fast_rcp(2.0 + f);
   const double z = s * s, w = z * z;
-  const double t1 = w * __builtin_fma(w, __builtin_fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
-                                      3.999999999940941908e-01);
-  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, 1.479819860511658591e-01,
-                                                                         1.818357216161805012e-01),
-                                                       2.857142874366239149e-01),
-                                      6.666666666666735130e-01);
+  const double t1 = w * __builtin_fma(w, __builtin_fma(w, FBC(FB_LG + 5), FBC(FB_LG + 3)), FBC(FB_LG + 1));
+  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, FBC(FB_LG + 6), FBC(FB_LG + 4)),
+                                                       FBC(FB_LG + 2)), FBC(FB_LG + 0));
   const double hfsq = 0.5 * f * f, dk = (double)e;
-  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + t1 + t2) + dk * 1.90821492927058770002e-10)) - f);
+  return dk * FBC(FB_LN2HI) - ((hfsq - (s * (hfsq + t1 + t2) + dk * FBC(FB_LN2LO))) - f);
 }
 __device__ __forceinline__ bool fast_certain(double v) {
   const float f = (float)v;
-  return (float)(v * (1.0 - kFastBesselTol)) == f && (float)(v * (1.0 + kFastBesselTol)) == f;
+  return (float)(v * FBC(FB_MISC + 3)) == f && (float)(v * FBC(FB_MISC + 4)) == f;
 }
 // N0: K0, I0; N1: K1, I1 at x in [kFastBesselLo, kFastBesselHi], rounded to float; false when a
-// value is not certified (then call bessel_ik)
+// value is not certified (then the exact bessel_ik).  Reads s_fbc: walk kernel only.
 template <bool N0, bool N1>
 __device__ __forceinline__ bool bessel_ik_fast(double x, float* i0, float* k0, float* i1, float* k1) {
   double vi0 = 0.0, vi1 = 0.0, vk0 = 0.0, vk1 = 0.0;
   double ex = 0.0, rsx = 0.0;  // e^x, 1/sqrt(x) (shared by the two large-x branches)
   if (x > 2.0) { ex = fast_exp(x); rsx = fast_rsqrt(x); }
   if (x < 3.75) {
-    double y = x * (1.0 / 3.75);
+    double y = x * FBC(FB_MISC + 0);
     y = y * y;
-    if (N0)
-      vi0 = __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, 0.45813e-2, 0.360768e-1), 0.2659732), 1.2067492), 3.0899424), 3.5156229), 1.0);
-    if (N1)
-      vi1 = x * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, 0.32411e-3, 0.301532e-2), 0.2658733e-1), 0.15084934), 0.51498869), 0.87890594), 0.5);
+    if (N0) vi0 = fb_poly<7>(y, FB_I0S);
+    if (N1) vi1 = x * fb_poly<7>(y, FB_I1S);
   } else {
-    const double y = 3.75 * fast_rcp(x);
+    const double y = FBC(FB_MISC + 1) * fast_rcp(x);
     const double e = ex * rsx;
-    if (N0)
-      vi0 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, 0.392377e-2, -0.1647633e-1), 0.2635537e-1),
-              -0.2057706e-1), 0.916281e-2), -0.157565e-2), 0.225319e-2), 0.1328592e-1), 0.39894228);
+    if (N0) vi0 = e * fb_poly<9>(y, FB_I0L);
     if (N1) {
-      double a = __builtin_fma(y, __builtin_fma(y, __builtin_fma(-y, 0.420059e-2, 0.1787654e-1), -0.2895312e-1),
-                               0.2282967e-1);
-      a = __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, a, -0.1031555e-1),
-                                                                          0.163801e-2), -0.362018e-2), -0.3988024e-1),
-                        0.39894228);
-      vi1 = a * e;
+      const double a = fb_poly<4>(y, FB_I1L);
+      vi1 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
+                __builtin_fma(y, a, FBC(FB_I1L + 4)), FBC(FB_I1L + 5)), FBC(FB_I1L + 6)), FBC(FB_I1L + 7)),
+                FBC(FB_I1L + 8));
     }
   }
   if (x <= 2.0) {
     const double y = (x * x) * 0.25;
     const double l = fast_log(x * 0.5);
-    if (N0)
-      vk0 = __builtin_fma(-l, vi0, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, __builtin_fma(y, 0.74e-5, 0.10750e-3), 0.262698e-2), 0.3488590e-1), 0.23069756),
-              0.42278420), -0.57721566));
-    if (N1)
-      vk1 = __builtin_fma(l, vi1, fast_rcp(x) * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, __builtin_fma(y, -0.4686e-4, -0.110404e-2), -0.1919402e-1), -0.18156897),
-              -0.67278579), 0.15443144), 1.0));
+    if (N0) vk0 = __builtin_fma(-l, vi0, fb_poly<7>(y, FB_K0S));
+    if (N1) vk1 = __builtin_fma(l, vi1, fast_rcp(x) * fb_poly<7>(y, FB_K1S));
   } else {
     const double y = 2.0 * fast_rcp(x);
     const double e = fast_rcp(ex) * rsx;
-    if (N0)
-      vk0 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, 0.53208e-3, -0.251540e-2), 0.587872e-2), -0.1062446e-1), 0.2189568e-1), -0.7832358e-1),
-              1.25331414);
-    if (N1)
-      vk1 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-              __builtin_fma(y, -0.68245e-3, 0.325614e-2), -0.780353e-2), 0.1504268e-1), -0.3655620e-1), 0.23498619),
-              1.25331414);
+    if (N0) vk0 = e * fb_poly<7>(y, FB_K0L);
+    if (N1) vk1 = e * fb_poly<7>(y, FB_K1L);
   }
   bool ok = true;
   if (N0) { ok = ok && fast_certain(vi0) && fast_certain(vk0); *i0 = (float)vi0; *k0 = (float)vk0; }
@@ -1350,7 +1371,8 @@ struct Gfn {
     A0 = m[0]; A1 = m[1]; B0 = m[2]; B1 = m[3];
   }
 
-  __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust) {
+  // fast: the certified fast Bessels (bessel_ik_fast; the caller's kernel staged s_fbc)
+  __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust, bool fast = false) {
     for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
     R = RR; r = 0.0f;
     if (!yukawa) return;
@@ -1361,7 +1383,7 @@ struct Gfn {
       return;
     }
     if constexpr (DIM == 2) {
-      if (WOS_FAST_BESSEL) {
+      if (WOS_FAST_BESSEL && fast) {
         float fi0 = 0.0f, fk0 = 0.0f, fi1 = 0.0f, fk1 = 0.0f;
         const bool ok = muR >= kFastBesselLo && muR <= kFastBesselHi &&
                         bessel_ik_fast<true, true>((double)muR, &fi0, &fk0, &fi1, &fk1);
@@ -1503,7 +1525,7 @@ struct Gfn {
     }
   }
 
-  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y) const {
+  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y, bool fast = false) const {
     if (!yukawa) return 1.0f;
     float d[DIM];
     for (int k = 0; k < DIM; k++) d[k] = y[k] - c[k];
@@ -1517,7 +1539,7 @@ struct Gfn {
         // the ball update already evaluated -- the same double values, rounded the same
         K1mur = B0;
         I1mur = B1;
-      } else if (WOS_FAST_BESSEL) {
+      } else if (WOS_FAST_BESSEL && WOS_FAST_BESSEL_PK && fast) {
         const bool ok = mur >= kFastBesselLo && mur <= kFastBesselHi &&
                         bessel_ik_fast<false, true>((double)mur, nullptr, nullptr, &I1mur, &K1mur);
         if (!ok) {
@@ -2487,7 +2509,7 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
     starRadius = starQ;
     if (prm.min_star_radius <= dirichletDist) starRadius = smax(0.99f * starRadius, prm.min_star_radius);
   }
-  g.update_ball(st.pt, starRadius, prm.robust != 0);
+  g.update_ball(st.pt, starRadius, prm.robust != 0, true);
   (*steps)++;
   float u[2];
   u[0] = smp.nextf();
@@ -2558,7 +2580,7 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
   st.prevDist = ip.d;
   for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
   st.onNeumann = hit;
-  st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
+  st.throughput *= g.dir_sampled_poisson_kernel(st.pt, true);
   if (st.throughput < prm.rr_threshold) {
     float survival = st.throughput / prm.rr_threshold;
     if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
@@ -4045,6 +4067,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const int lane = threadIdx.x & (kWave - 1);
   stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
+  if (WOS_FAST_BESSEL && DIM == 2) stage_fast_bessel();
   // per-wave scratch shared by the star and ray queries (used one after the other)
   const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // wave-uniform: SGPR address
   char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();

@@ -992,7 +992,8 @@ __device__ __forceinline__ void offset_point(const float* p, const float* n, flo
 // the walk step a second time on opaque copies of its inputs, results sunk -- the walks are
 // unchanged, so the kernel's SQ_INSTS_VALU and time minus the base build's are that piece's
 // dynamic instruction count and cost.  1: update_ball's Bessels (2D), 2: the direction-
-// sampled Poisson kernel's Bessels (2D), 4: a cooperative rejection item (draws + fast test).
+// sampled Poisson kernel's Bessels (2D), 4: a cooperative rejection item (draws + fast test),
+// 8: the star-radius query, 16: the ray query, 32: the whole source sample (sample_volume_wave).
 #ifndef WOS_PROBE
 #define WOS_PROBE 0
 #endif
@@ -1094,7 +1095,10 @@ __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x)
 // is monotone, so its float equals ours.  Uncertain lanes (P ~ 1e-5 per value) and
 // arguments outside [1e-6, 80] take the exact bessel_ik.  Results are bit-identical.
 #ifndef WOS_FAST_BESSEL
-#define WOS_FAST_BESSEL 1
+#define WOS_FAST_BESSEL 0
+#endif
+#ifndef WOS_FAST_BESSEL_FB
+#define WOS_FAST_BESSEL_FB 0  // 1: also the 2D first balls' source-sample pdf and gradient norm
 #endif
 #ifndef WOS_FAST_BESSEL_PK
 #define WOS_FAST_BESSEL_PK 1  // also the direction-sampled Poisson kernel's K1, I1
@@ -1242,8 +1246,15 @@ __device__ __forceinline__ bool bessel_ik_fast(double x, float* i0, float* k0, f
 // the exact evaluation (bessel_ik) rounded to float, for the lanes the fast path cannot certify:
 // out of line, so the throughput path keeps its registers
 struct F4 { float i0, k0, i1, k1; };
+#ifndef WOS_FB_EXACT_NOINLINE
+#define WOS_FB_EXACT_NOINLINE 1
+#endif
 template <bool N0, bool N1>
+#if WOS_FB_EXACT_NOINLINE
 __device__ __attribute__((noinline)) F4 bessel_ik_exact_f(double x) {
+#else
+__device__ __forceinline__ F4 bessel_ik_exact_f(double x) {
+#endif
   double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
   bessel_ik<N0, N1>(x, N0 ? &a : nullptr, N0 ? &b : nullptr, N1 ? &c : nullptr, N1 ? &d : nullptr);
   return F4{(float)a, (float)b, (float)c, (float)d};
@@ -1446,6 +1457,14 @@ struct Gfn {
   __device__ __forceinline__ float evaluate_k0i0(double k0, double i0) const {
     const float K0mur = (float)k0, I0mur = (float)i0;
     return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
+  }
+  // the same from the float-rounded values (certified fast path: bessel_ik_fast)
+  __device__ __forceinline__ float evaluate_k0i0f(float K0mur, float I0mur) const {
+    return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
+  }
+  __device__ __forceinline__ float gradient_norm_k1i1f(float K1mur, float I1mur) const {
+    const float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
+    return (float)((double)Qr / (kTwoPi * (double)r));
   }
   __device__ __forceinline__ float gradient_norm_k1i1(double k1, double i1) const {
     const float K1mur = (float)k1, I1mur = (float)i1;
@@ -3133,8 +3152,10 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
 //   3. wos_fold_kernel        -- one lane per point: the statistics in walk order
 //      (Welford means with sequential control variates, walk_on_stars.h:500-506,
 //      583-614, 744-877) and the masked outputs (grid.h:155-179, 207-237).
-// The three stages touch HBM only for the task records (~48 B per walk in 2D),
-// which is negligible next to the walk arithmetic.
+// The three stages touch HBM only for the task hand-off (~48 B per walk in 2D).  It is most of
+// the walk kernel's traffic -- karman: 134 MB of start-state reads and 99 MB of record write-backs
+// per launch, DESIGN.md "HBM bytes of the walk kernel" -- but 2 % of HBM bandwidth over the
+// kernel's time: the walk arithmetic, not the hand-off, sets the time.
 
 // stratifiedSample (sampling.h:435-457) on the per-point stream, drawn in parallel:
 // draw k of the stream is pcg_output(A_k * s0 + C_k).  Diagonal draws k < n*sd;
@@ -3371,7 +3392,19 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
           }
 #endif
           const float nrm = g.norm();
-          if (rpre == g.r) {
+          if (rpre == g.r && WOS_FAST_BESSEL && WOS_FAST_BESSEL_FB) {
+            // certified fast Bessels (s_fbc staged by the first-ball kernel), exact fallback
+            const double xr = (double)(g.r * g.sqrtLambda);
+            float fi0 = 0.0f, fk0 = 0.0f, fi1 = 0.0f, fk1 = 0.0f;
+            const bool ok = xr >= kFastBesselLo && xr <= kFastBesselHi &&
+                            bessel_ik_fast<true, true>(xr, &fi0, &fk0, &fi1, &fk1);
+            if (!ok) {
+              const F4 e = bessel_ik_exact_f<true, true>(xr);
+              fi0 = e.i0; fk0 = e.k0; fi1 = e.i1; fk1 = e.k1;
+            }
+            sourcePdf = g.evaluate_k0i0f(fk0, fi0) / nrm;
+            gn_a = g.gradient_norm_k1i1f(fk1, fi1);
+          } else if (rpre == g.r) {
             double i0, k0, i1, k1;
             bessel_ik<true, true>((double)(g.r * g.sqrtLambda), &i0, &k0, &i1, &k1);
             sourcePdf = g.evaluate_k0i0(k0, i0) / nrm;
@@ -3707,6 +3740,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   stage_rej_jump(prm);
+  if (WOS_FAST_BESSEL && WOS_FAST_BESSEL_FB && DIM == 2) stage_fast_bessel();
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -3898,6 +3932,12 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   if (active) code = walk_step_begin<DIM>(sc, prm, ddist, st, &flip, &query, BSTART ? firstR : 0.0f);
   DIAG_T0(t_star);
   const float starQ = star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, st.pt, ddist, flip, starL, lane);
+  if (WOS_PROBE & 8) {
+    float px[DIM];
+    for (int k = 0; k < DIM; k++) px[k] = probe_opaque(st.pt[k]);
+    probe_sink(star_radius_wave<DIM, GG>(G, sc, prm, active && code < 0 && query, px, probe_opaque(ddist), flip, starL,
+                                         lane));
+  }
   DIAG_ADD_LONE(D_STAR, D_L_STAR, t_star, lone);
   const bool live = active && code < 0;
   float dir[DIM], org[DIM], starR = 0.0f;
@@ -3908,6 +3948,12 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   Hit ip;
   DIAG_T0(t_ray);
   const bool hit = ray_hit_wave<DIM, GG>(G, sc, live, org, dir, starR, &ip, rayL, lane);
+  if (WOS_PROBE & 16) {
+    Hit ip2;
+    float po[DIM];
+    for (int k = 0; k < DIM; k++) po[k] = probe_opaque(org[k]);
+    probe_sink(ray_hit_wave<DIM, GG>(G, sc, live, po, dir, probe_opaque(starR), &ip2, rayL, lane) ? ip2.d : 0.0f);
+  }
   DIAG_ADD_LONE(D_RAY, D_L_RAY, t_ray, lone);
   DIAG_T0(t_end);
   if (live) walk_step_end<DIM, RB, NEU>(sc, prm, G, ws, g, st, starR, dir, org, hit, ip, flip);
@@ -3915,6 +3961,15 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   float sp[DIM], pdf_unused;
   for (int k = 0; k < DIM; k++) sp[k] = 0.0f;
   DIAG_T0(t_smp);
+  if ((WOS_PROBE & 32) && !prm.ignore_source) {
+    Gfn<DIM, RB> g2 = g;
+    Pcg32 ws2 = ws;
+    ws2.state = probe_opaque(ws2.state);
+    float sp2[DIM], pdf2;
+    uint32_t it2 = 0;
+    sample_volume_wave<DIM>(prm, live, g2, dir, ws2, &pdf2, sp2, &it2, false, rejL, lane);
+    probe_sink(sp2[0]);
+  }
   if (!prm.ignore_source) sample_volume_wave<DIM>(prm, live, g, dir, ws, &pdf_unused, sp, c_iters, false, rejL, lane);
   DIAG_ADD_LONE(D_SAMPLE, D_L_SAMPLE, t_smp, lone);
   DIAG_T0(t_tail);

@@ -1871,83 +1871,6 @@ __device__ __forceinline__ void sample_volume(const DevParams& prm, Gfn<DIM, RB>
   for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
 }
 
-// The sequential loop above, kFbSpec iterations per trip (2D Yukawa fast path, mu R < 80): the
-// draws, certain-reject bounds and float fast tests of iterations j .. j + kFbSpec - 1 are
-// evaluated together (independent, so their latencies overlap), then decided in order -- the
-// first accept wins, an undecided iteration before it takes the exact double test -- so the
-// accepted radius, the iteration count and the stream position are the sequential loop's.  A
-// lane's loop is a chain of dependent trips whose length is set by the slowest lane of the
-// wave (the 64 pairs of a first ball: ~14 iterations against a mean of ~3.4, karman), so
-// fewer, wider trips shorten it.  First-ball kernel (2D) only.
-#ifndef WOS_FB_SPEC
-#define WOS_FB_SPEC 4
-#endif
-constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
-constexpr int kFbSpec = WOS_FB_SPEC;
-template <int DIM, bool RB>
-__device__ __forceinline__ void sample_volume_spec(const DevParams& prm, Gfn<DIM, RB>& g, const float* dir, Pcg32& s,
-                                                   float* pdf, float* out, uint32_t* iters, bool need_pdf,
-                                                   float* r_pre) {
-  const float R = g.R;
-  const float a = 2.2f, b = 0.6f;
-  const float lam = g.lambda, sl = g.sqrtLambda;
-  const float bound = R <= lam ? smax(smax(a / R, a / lam), smax(b * __builtin_sqrtf(R), b * sl))
-                               : smax(smin(a / R, a / lam), smin(b * __builtin_sqrtf(R), b * sl));
-  const float nrm = g.norm();
-  const float rho = g.A0 / g.A1;
-  const float invNB = 1.0f / (nrm * bound);
-  const float quick = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB);
-  uint64_t st = s.state;  // the stream before iteration j (draw 2j)
-  int j = 0, jacc = -1;
-  uint64_t st_acc = 0;    // the stream before the accepted (or last) iteration
-  while (jacc < 0) {
-    float uu[kFbSpec], rr[kFbSpec];
-    int dec[kFbSpec];
-    uint64_t sj[kFbSpec];
-    uint64_t cur = st;
-#pragma unroll
-    for (int k = 0; k < kFbSpec; k++) {
-      sj[k] = cur;
-      uu[k] = pcg_float_of(cur);
-      rr[k] = pcg_float_of(cur * kPcgMult + kPcgInc) * R;
-      cur = cur * kPcgMult2 + kPcgInc2;
-      dec[k] = 0;
-      if (!(uu[k] > quick)) {
-        const float mur = rr[k] * sl;
-        float k0, i0v;
-        k0i0_fast(mur, &k0, &i0v);
-        const float ip = i0v * rho;
-        const float c = rr[k] * invNB;
-        const float Tf = (k0 - ip) * c;
-        const float M = 8e-6f * (__builtin_fabsf(k0) + __builtin_fabsf(ip)) * c + 2e-6f * __builtin_fabsf(Tf) + 1e-30f;
-        dec[k] = uu[k] < Tf - M ? 1 : (uu[k] > Tf + M ? 0 : -1);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kFbSpec; k++) {
-      if (jacc >= 0 || j + k >= kRejMax) continue;
-      int d = dec[k];
-      if (d < 0) {  // undecided: the exact test of sample_volume
-        g.r = rr[k];
-        const float p = g.evaluate() / nrm;
-        const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
-        d = uu[k] < pdfRadius / bound ? 1 : 0;
-      }
-      if (d == 1 || j + k == kRejMax - 1) { jacc = j + k; st_acc = sj[k]; }  // accept, or the limit
-    }
-    st = cur;
-    j += kFbSpec;
-  }
-  s.state = st_acc * kPcgMult2 + kPcgInc2;
-  g.r = pcg_float_of(st_acc * kPcgMult + kPcgInc) * R;  // the last iteration's radius
-  if (need_pdf) *pdf = g.evaluate() / nrm;
-  if (r_pre) *r_pre = g.r;
-  *iters += (uint32_t)(jacc + 1);
-  g.r = smax(Gfn<DIM>::rClamp, g.r);
-  if (g.r > R) g.r = R / 2.0f;
-  for (int k = 0; k < DIM; k++) { g.yVol[k] = g.c[k] + g.r * dir[k]; out[k] = g.yVol[k]; }
-}
-
 // ---------------------------------------------------------------------------
 // Wave-cooperative rejection sampling (rejectionSampleGreensFn, distributions.h:
 // 362-383) for the 2D Yukawa fast path.  Iteration j of a lane's loop consumes
@@ -1962,6 +1885,7 @@ __device__ __forceinline__ void sample_volume_spec(const DevParams& prm, Gfn<DIM
 // geometric tail (the wave paid for the longest loop of its lanes).  Lanes off
 // the fast path (3D, harmonic, mu*R >= 80) run the sequential loop.
 // ---------------------------------------------------------------------------
+constexpr int kRejMax = 1000;  // rejectionSampleGreensFn iteration limit
 // minimum iterations per unfinished lane and generation of the cooperative sampler
 // (2D acceptance ~21 %, 3D ~7 % on the shipped scenes)
 // (A/B on MI355X, tools/ab.sh: 2D 3 beats 1 by 2-4 % on karman / C; 3D 8 in the first-ball
@@ -3455,10 +3379,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
 #if WOS_DIAG
           const uint32_t it0 = *iters;
 #endif
-          if (kFbSpec > 1 && g.muR < 80.0f)
-            sample_volume_spec<DIM, RB>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, false, &rpre);
-          else
-            sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, false, &rpre);
+          sample_volume<DIM>(prm, g, dir, fs, &sourcePdf, sourcePt, iters, false, &rpre);
 #if WOS_DIAG
           {
             const uint32_t itn = *iters - it0;

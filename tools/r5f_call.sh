@@ -10,7 +10,3 @@ for v in $VARS; do
   WOS_LIB_PATH=$L/libwos_$v.so timeout -k 10 300 python3 tools/collect_sq.py ${TAG}_$v B > gpurun_out/${TAG}_${v}_sq.log 2>&1 || exit 1
   python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_${v}_walk_sq.json'));c=d['counters'];print('$v VALU %.1fM SALU %.1fM t %.3f ms issue %.3f' % (c['SQ_INSTS_VALU']/1e6, c['SQ_INSTS_SALU']/1e6, d['kernel_s']*1e3, d['valu_issue_frac']))"
 done
-if [ -f $L/libwos_diag.so ]; then
-  WOS_LIB_PATH=$L/libwos_diag.so timeout -k 10 200 python3 tools/time_configs.py B_karman64k > gpurun_out/${TAG}_diag_B.log 2>&1 || exit 1
-  grep "diag" gpurun_out/${TAG}_diag_B.log | head -40
-fi

@@ -1424,6 +1424,12 @@ struct Gfn {
       A0 = expmuR; A1 = sinhmuR;
       B0 = expmuR * (1.0f + 1.0f / muR);
       B1 = coshmuR - sinhmuR / muR;
+      if (WOS_PROBE & 1) {
+        const float m2 = probe_opaque(muR);
+        const float e = fexp(-m2), e2 = e * e;
+        const float ch = (1.0f + e2) / (2.0f * e), sh = (1.0f - e2) / (2.0f * e);
+        probe_sink(e * (1.0f + 1.0f / m2)); probe_sink(ch - sh / m2); probe_sink(sh);
+      }
     }
   }
 
@@ -1586,6 +1592,12 @@ struct Gfn {
       float K32mur = expmur * (1.0f + 1.0f / mur);
       float I32mur = coshmur - sinhmur / mur;
       float Q = K32mur + I32mur * A0 / A1;
+      if (WOS_PROBE & 2) {
+        const float m2 = probe_opaque(mur);
+        const float e = fexp(-m2), e2 = e * e;
+        const float ch = (1.0f + e2) / (2.0f * e), sh = (1.0f - e2) / (2.0f * e);
+        probe_sink(m2 * (e * (1.0f + 1.0f / m2) + (ch - sh / m2) * A0 / A1));
+      }
       return mur * Q;
     }
   }

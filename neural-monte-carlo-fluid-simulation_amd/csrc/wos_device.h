@@ -2662,6 +2662,18 @@ __device__ __forceinline__ void dirichlet_dist_step(const DevScene& sc, const LG
 // the exact test on the winner for the hit record (identical arithmetic).
 // ---------------------------------------------------------------------------
 constexpr int kRayChunk = 16;
+// Scenes with at most this many Neumann primitives (2D segments / 3D triangles) take the per-lane
+// scan of ray_hit_wave when two or more lanes query: every lane tests every primitive
+#ifndef WOS_RAY_SCAN
+#define WOS_RAY_SCAN 1
+#endif
+#ifndef WOS_RAY_SCAN_MAX2
+#define WOS_RAY_SCAN_MAX2 24
+#endif
+#ifndef WOS_RAY_SCAN_MAX3
+#define WOS_RAY_SCAN_MAX3 16
+#endif
+constexpr int kRayScanMax2 = WOS_RAY_SCAN_MAX2, kRayScanMax3 = WOS_RAY_SCAN_MAX3;
 
 template <int DIM>
 struct RayLDS {
@@ -2720,6 +2732,32 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
   for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
   const bool tree = TREE && sc.ptree.levels > 0;
   const uint64_t nmask = __ballot(need);
+  if (WOS_RAY_SCAN && !tree && np <= (DIM == 2 ? kRayScanMax2 : kRayScanMax3) && (nmask & (nmask - 1)) != 0) {
+    // a handful of primitives (config C's box: 4 segments, the cube: 12 triangles): each querying
+    // lane tests every primitive against its own ray with the same pre-filter + exact test as the
+    // cooperative items (each against tmax) and keeps the minimum (d bits, ~index) -- no
+    // compaction, no LDS, no wave syncs; the same winner, rerun exactly for the hit record
+    bool found = false;
+    if (need) {
+      unsigned long long best = ~0ull;
+      for (int p = 0; p < np; p++) {
+        float rt = tmax;
+        Hit hh;
+        if (ray_prim_filtered<DIM>(G.prim + p * PS, o, dir, rt, &hh)) {
+          const unsigned long long key = ((unsigned long long)__float_as_uint(hh.d + 0.0f) << 32) |
+                                         (0xFFFFFFFFu - (uint32_t)p);
+          best = key < best ? key : best;
+        }
+      }
+      if (best != ~0ull) {
+        const int p = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+        float rt = tmax;
+        found = ray_prim_exact<DIM>(G.prim + p * PS, o, dir, rt, h);
+        if (found) normalize_rcp<DIM>(h->n);
+      }
+    }
+    return found;
+  }
   if (WOS_SOLO && !tree && (nmask & (nmask - 1)) == 0) {
     // one querying lane: lane l tests group g0 + l against the owner's ray, then the
     // primitives of the accepted groups, kGroup lanes per group; the minimum key by a

@@ -1924,6 +1924,13 @@ static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 
 #define WOS_REJ_OWN 4
 #endif
 constexpr int kRejOwn = WOS_REJ_OWN;
+// 3D (acceptance ~7 %): iterations of the own generation (WOS_REJ_OWN3, default the 2D count)
+#ifndef WOS_REJ_OWN3
+#define WOS_REJ_OWN3 WOS_REJ_OWN
+#endif
+template <int DIM>
+constexpr int kRejOwnD = DIM == 2 ? WOS_REJ_OWN : WOS_REJ_OWN3;
+static_assert(WOS_REJ_OWN3 >= 0 && WOS_REJ_OWN3 <= 32 && WOS_REJ_OWN3 < 1000, "WOS_REJ_OWN3");
 #ifndef WOS_REJ_OWN_MIN
 #define WOS_REJ_OWN_MIN 40
 #endif
@@ -2159,8 +2166,8 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       const float invNB0 = 1.0f / (nrm * bound);
       const float qb0 = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB0);
       uint32_t acc = 0u, und = 0u;
-#pragma unroll
-      for (int b = 0; b < kRejOwn; b++) {
+#pragma unroll 4
+      for (int b = 0; b < kRejOwnD<DIM>; b++) {
         const uint64_t st = rej_state(prm, s0, b);
         const float u = draw_float(st);
         int dcs = 0;
@@ -2190,7 +2197,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         if (u < pdfRadius / bound) { jacc = b; done = true; break; }
       }
     }
-    j0 = own ? kRejOwn : 0;
+    j0 = own ? kRejOwnD<DIM> : 0;
 #endif
     if (!done) {
       L->s0[lane] = s0;

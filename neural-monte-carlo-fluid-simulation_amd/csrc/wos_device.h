@@ -1924,13 +1924,19 @@ static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 
 #define WOS_REJ_OWN 4
 #endif
 constexpr int kRejOwn = WOS_REJ_OWN;
-// 3D (acceptance ~7 %): iterations of the own generation (WOS_REJ_OWN3, default the 2D count)
+// 3D (acceptance ~7 %): iterations of the own generation -- the walk kernel's 16 (a lane accepts
+// within them with P ~ 0.69; walk kernel on the cube 22.1 -> 20.8 ms at 128^3, against 4), the
+// first-ball kernel's 4 (its 64 lanes hold 2 points' pairs; 16 made first balls +6 %):
+// profiles/r5k_ab_own3.log
 #ifndef WOS_REJ_OWN3
-#define WOS_REJ_OWN3 WOS_REJ_OWN
+#define WOS_REJ_OWN3 16
 #endif
-template <int DIM>
-constexpr int kRejOwnD = DIM == 2 ? WOS_REJ_OWN : WOS_REJ_OWN3;
-static_assert(WOS_REJ_OWN3 >= 0 && WOS_REJ_OWN3 <= 32 && WOS_REJ_OWN3 < 1000, "WOS_REJ_OWN3");
+#ifndef WOS_REJ_OWN3_FB
+#define WOS_REJ_OWN3_FB WOS_REJ_OWN
+#endif
+template <int DIM, bool FB>
+constexpr int kRejOwnD = DIM == 2 ? WOS_REJ_OWN : (FB ? WOS_REJ_OWN3_FB : WOS_REJ_OWN3);
+static_assert(WOS_REJ_OWN3 >= 0 && WOS_REJ_OWN3 <= 32 && WOS_REJ_OWN3_FB >= 0 && WOS_REJ_OWN3_FB <= 32, "own");
 #ifndef WOS_REJ_OWN_MIN
 #define WOS_REJ_OWN_MIN 40
 #endif
@@ -2167,7 +2173,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       const float qb0 = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB0);
       uint32_t acc = 0u, und = 0u;
 #pragma unroll 4
-      for (int b = 0; b < kRejOwnD<DIM>; b++) {
+      for (int b = 0; b < kRejOwnD<DIM, FB>; b++) {
         const uint64_t st = rej_state(prm, s0, b);
         const float u = draw_float(st);
         int dcs = 0;
@@ -2197,7 +2203,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         if (u < pdfRadius / bound) { jacc = b; done = true; break; }
       }
     }
-    j0 = own ? kRejOwnD<DIM> : 0;
+    j0 = own ? kRejOwnD<DIM, FB> : 0;
 #endif
     if (!done) {
       L->s0[lane] = s0;

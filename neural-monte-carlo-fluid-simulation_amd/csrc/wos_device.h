@@ -3326,27 +3326,6 @@ __host__ __device__ constexpr int fb_points_per_wave(int n_pairs) {
              : 1;
 }
 
-// The LHS draws' jump constants k < kLhsJumpLds, staged in LDS by the first-ball kernel when the
-// per-point draws fit (2 n_pairs (DIM - 1) diagonal + as many shuffle draws): karman and the
-// cube read them from LDS instead of a global round trip per draw
-#ifndef WOS_LHS_JUMP_LDS
-#define WOS_LHS_JUMP_LDS 256
-#endif
-constexpr int kLhsJumpLds = WOS_LHS_JUMP_LDS > 0 ? WOS_LHS_JUMP_LDS : 1;
-static __shared__ unsigned long long s_lhs_jump[2 * kLhsJumpLds];
-__device__ __forceinline__ bool lhs_jump_staged(const DevParams& prm) {
-  return WOS_LHS_JUMP_LDS > 0 && 2 * (2 * prm.n_pairs) <= kLhsJumpLds;  // DIM - 1 <= 2 draws per stratum
-}
-__device__ __forceinline__ void stage_lhs_jump(const DevParams& prm) {
-  if (!lhs_jump_staged(prm)) return;
-  const int nk = prm.n_jump < kLhsJumpLds ? prm.n_jump : kLhsJumpLds;
-  for (int i = threadIdx.x; i < 2 * nk; i += blockDim.x) s_lhs_jump[i] = prm.jump[i];
-}
-__device__ __forceinline__ uint64_t lhs_jump_state(const DevParams& prm, uint64_t s0, int k, bool staged) {
-  if (staged && k < kLhsJumpLds) return s_lhs_jump[2 * k] * s0 + s_lhs_jump[2 * k + 1];
-  return jump_state(prm, s0, k);
-}
-
 template <int DIM>
 __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
                                           char* scratch, int lane) {
@@ -3358,10 +3337,9 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   const uint64_t s0 = ps.state;
   const float ome = 1.0f - kFltEps;
   const float inv = 1.0f / (float)nstrat;
-  const bool staged = 2 * nd <= kLhsJumpLds && lhs_jump_staged(prm);
   for (int idx = lane; idx < nd; idx += kWave) {
     const int i = sd == 1 ? idx : idx / sd;
-    const uint32_t r = pcg_output(lhs_jump_state(prm, s0, idx, staged));
+    const uint32_t r = pcg_output(jump_state(prm, s0, idx));
     const float u = bits_to_float((r >> 9) | 0x3f800000u) - 1.0f;
     strat[idx] = smin(((float)i + u) * inv, ome);
   }
@@ -3369,7 +3347,7 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   for (int idx = lane; idx < nd; idx += kWave) {
     const int j = sd == 1 ? idx : idx % nstrat;
     const uint32_t bound = (uint32_t)(nstrat - j);
-    const uint32_t r = pcg_output(lhs_jump_state(prm, s0, nd + idx, staged));
+    const uint32_t r = pcg_output(jump_state(prm, s0, nd + idx));
     // PCG's rejection threshold th = 2^32 mod bound < bound: only r < bound can fall below it
     if (r < bound) rej |= r < (~bound + 1u) % bound;
     partner[idx] = j + (int)(r % bound);
@@ -3825,7 +3803,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   stage_rej_jump(prm);
-  stage_lhs_jump(prm);
   if (WOS_FAST_BESSEL && WOS_FAST_BESSEL_FB && DIM == 2) stage_fast_bessel();
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;

@@ -4455,7 +4455,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #ifndef WOS_FOLD_UNROLL3
 #define WOS_FOLD_UNROLL3 4
 #endif
+// records staged per point and round: 2D 16; 3D (nine fields per record) WOS_FOLD_CHUNK3
+#ifndef WOS_FOLD_CHUNK3
+#define WOS_FOLD_CHUNK3 WOS_FOLD_CHUNK
+#endif
 constexpr int kFoldPoints = WOS_FOLD_POINTS, kFoldChunk = WOS_FOLD_CHUNK;
+template <int DIM>
+constexpr int kFoldChunkD = DIM == 2 ? WOS_FOLD_CHUNK : WOS_FOLD_CHUNK3;
 template <int DIM>
 constexpr int kFoldUnroll = DIM == 2 ? WOS_FOLD_UNROLL2 : WOS_FOLD_UNROLL3;
 
@@ -4466,7 +4472,7 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
                                                                int32_t* __restrict__ nest_out,
                                                                int32_t* __restrict__ steps_out) {
   constexpr int NF = 3 + 2 * DIM;  // code | total | first | bdir[DIM] | sdir[DIM]
-  constexpr int LD = kFoldChunk + 1;
+  constexpr int LD = kFoldChunkD<DIM> + 1;
   wave_priority(prm.wave_prio);
   __shared__ float lds[NF][kFoldPoints][LD];
   const int tid = threadIdx.x;
@@ -4487,17 +4493,17 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   for (int k = 0; k < DIM; k++) dn[k] = k == 0 ? 1.0f : 0.0f;
   if (tk.deriv && tk.ddir && tid < nb)
     for (int k = 0; k < DIM; k++) dn[k] = tk.ddir[i * DIM + k];
-  for (int c0 = 0; c0 < wpp; c0 += kFoldChunk) {
-    const int cnt = (wpp - c0) < kFoldChunk ? (wpp - c0) : kFoldChunk;
+  for (int c0 = 0; c0 < wpp; c0 += kFoldChunkD<DIM>) {
+    const int cnt = (wpp - c0) < kFoldChunkD<DIM> ? (wpp - c0) : kFoldChunkD<DIM>;
     // kFoldUnroll<DIM> staging slots in flight per thread: all their loads are issued
     // before the first LDS store (one HBM round trip per kFoldUnroll slots, not per slot)
-    for (int e0 = tid; e0 < nb * kFoldChunk; e0 += kFoldPoints * kFoldUnroll<DIM>) {
+    for (int e0 = tid; e0 < nb * kFoldChunkD<DIM>; e0 += kFoldPoints * kFoldUnroll<DIM>) {
       float v[kFoldUnroll<DIM>][NF];
 #pragma unroll
       for (int u = 0; u < kFoldUnroll<DIM>; u++) {
         const int e = e0 + u * kFoldPoints;
-        const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
-        if (e >= nb * kFoldChunk || j >= cnt) continue;
+        const int pp = e / kFoldChunkD<DIM>, j = e - pp * kFoldChunkD<DIM>;
+        if (e >= nb * kFoldChunkD<DIM> || j >= cnt) continue;
         const int64_t t = (p0 + pp) * wpp + c0 + j;
         v[u][0] = __uint_as_float(tk.code[t]);
         v[u][1] = tk.total[t];
@@ -4511,8 +4517,8 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
 #pragma unroll
       for (int u = 0; u < kFoldUnroll<DIM>; u++) {
         const int e = e0 + u * kFoldPoints;
-        const int pp = e / kFoldChunk, j = e - pp * kFoldChunk;
-        if (e >= nb * kFoldChunk || j >= cnt) continue;
+        const int pp = e / kFoldChunkD<DIM>, j = e - pp * kFoldChunkD<DIM>;
+        if (e >= nb * kFoldChunkD<DIM> || j >= cnt) continue;
 #pragma unroll
         for (int f = 0; f < NF; f++) lds[f][pp][j] = v[u][f];
       }

@@ -4567,4 +4567,107 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
   if (tk.deriv) tk.deriv[i] = sDeriv / (float)(sN > 1 ? sN : 1);  // getEstimatedDerivative (unmasked)
 }
 
+// The same statistics with one lane QUAD per point: quad lane c runs component c's Welford chain
+// (c = 0: the solution, c = 1..DIM: the gradient components; 2D leaves lane 3 idle), operation for
+// operation as wos_fold_kernel's mean[c]; the control variate cvb -- the solution mean at a pair's
+// start -- comes from quad lane 0 by a DPP quad broadcast, and the walk count and first-source sum
+// (cvs) are kept by every lane.  Four chains in flight per point instead of one, and a quarter of
+// the LDS per point, so four times the waves: the fold was latency-bound on one thread's chain of
+// IEEE divisions per point (round 4, DESIGN).  Not for the derivative output (BVC's Dirichlet
+// samples, DevTasks::deriv): wos_fold_kernel keeps that.
+#ifndef WOS_FOLD4
+#define WOS_FOLD4 1
+#endif
+constexpr int kFold4Points = 64;  // points per 256-thread block
+template <int DIM>
+__global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevParams prm, const DevTasks tk, int64_t n,
+                                                                     float* __restrict__ p_out,
+                                                                     float* __restrict__ g_out,
+                                                                     int32_t* __restrict__ nest_out,
+                                                                     int32_t* __restrict__ steps_out) {
+  constexpr int NF = 3 + 2 * DIM;  // code | total | first | bdir[DIM] | sdir[DIM]
+  constexpr int CH = kFoldChunkD<DIM>;
+  constexpr int LD = CH + 1;
+  constexpr int NT = 4 * kFold4Points;
+  wave_priority(prm.wave_prio);
+  __shared__ float lds[NF][kFold4Points][LD];
+  const int tid = threadIdx.x;
+  const int c = tid & 3, pp = tid >> 2;
+  const int64_t p0 = (int64_t)blockIdx.x * kFold4Points;
+  const int nb = (int)((n - p0) < kFold4Points ? (n - p0) : kFold4Points);
+  const int64_t i = p0 + pp;
+  const int64_t T = tk.T;
+  const int wpp = tk.wpp;
+  const int ps = pp < nb ? tk.pstate[i] : 0;
+  const bool estimate = (ps & kPtEstimate) != 0;
+  const bool comp = c <= DIM;
+  const int fb = c >= 1 && comp ? 3 + (c - 1) : 3, fs = c >= 1 && comp ? 3 + DIM + (c - 1) : 3;
+  float mean = 0.0f, sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
+  int sN = 0;
+  uint32_t steps = 0;
+  for (int c0 = 0; c0 < wpp; c0 += CH) {
+    const int cnt = (wpp - c0) < CH ? (wpp - c0) : CH;
+    for (int e0 = tid; e0 < nb * CH; e0 += NT * kFoldUnroll<DIM>) {
+      float v[kFoldUnroll<DIM>][NF];
+#pragma unroll
+      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
+        const int e = e0 + u * NT;
+        const int q = e / CH, j = e - q * CH;
+        if (e >= nb * CH || j >= cnt) continue;
+        const int64_t t = (p0 + q) * wpp + c0 + j;
+        v[u][0] = __uint_as_float(tk.code[t]);
+        v[u][1] = tk.total[t];
+        v[u][2] = tk.first[t];
+#pragma unroll
+        for (int k = 0; k < DIM; k++) {
+          v[u][3 + k] = tk.bdir[k * T + t];
+          v[u][3 + DIM + k] = tk.sdir[k * T + t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
+        const int e = e0 + u * NT;
+        const int q = e / CH, j = e - q * CH;
+        if (e >= nb * CH || j >= cnt) continue;
+#pragma unroll
+        for (int f = 0; f < NF; f++) lds[f][q][j] = v[u][f];
+      }
+    }
+    __syncthreads();
+    if (estimate) {
+      for (int j = 0; j < cnt; j++) {
+        const int r = c0 + j;
+        if (r % prm.n_anti == 0) {  // a new antithetic pair: control variates from the walks before it
+          // quad lane 0's solution mean (DPP quad_perm [0,0,0,0])
+          cvb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mean), 0x00, 0xF, 0xF, false));
+          cvs = sFirst / (float)(sN > 1 ? sN : 1);
+          if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
+        }
+        const uint32_t code = __float_as_uint(lds[0][pp][j]);
+        steps += code >> 1;
+        if (!(code & 1u)) continue;
+        const float total = lds[1][pp][j];
+        const float first = lds[2][pp][j];
+        sN += 1;
+        const float fN = (float)sN;
+        const float be = (total - first - cvb) * lds[fb][pp][j];
+        const float se = (first - cvs) * lds[fs][pp][j];
+        const float val = c == 0 ? total : be + se;
+        const float delta = val - mean;
+        mean += delta / fN;
+        sFirst += first;
+      }
+    }
+    __syncthreads();
+  }
+  if (pp >= nb || !comp) return;
+  if (c == 0) {
+    p_out[i] = (ps & kPtMaskP) ? 0.0f : mean;
+    if (nest_out) nest_out[i] = sN;
+    if (steps_out) steps_out[i] = (int32_t)steps;
+  } else {
+    g_out[i * DIM + (c - 1)] = (ps & kPtMaskG) ? 0.0f : mean;
+  }
+}
+
 }  // namespace wos

@@ -4574,7 +4574,8 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
 // (cvs) are kept by every lane.  Four chains in flight per point instead of one, and a quarter of
 // the LDS per point, so four times the waves: the fold was latency-bound on one thread's chain of
 // IEEE divisions per point (round 4, DESIGN).  Not for the derivative output (BVC's Dirichlet
-// samples, DevTasks::deriv): wos_fold_kernel keeps that.
+// samples, DevTasks::deriv): wos_fold_kernel keeps that.  Launched for 3D only (launch_fold): 2D's
+// five-float records fold faster one thread per point.
 #ifndef WOS_FOLD4
 #define WOS_FOLD4 1
 #endif
@@ -4590,7 +4591,10 @@ __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevPa
   constexpr int LD = CH + 1;
   constexpr int NT = 4 * kFold4Points;
   wave_priority(prm.wave_prio);
-  __shared__ float lds[NF][kFold4Points][LD];
+  // one plane per field, planes FS words apart: FS = 1 (mod 64) puts the four lanes of a quad, which
+  // read different planes at the same (point, walk), in different LDS banks
+  constexpr int FS = kFold4Points * LD + 1;
+  __shared__ float lds[NF * FS];
   const int tid = threadIdx.x;
   const int c = tid & 3, pp = tid >> 2;
   const int64_t p0 = (int64_t)blockIdx.x * kFold4Points;
@@ -4630,7 +4634,7 @@ __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevPa
         const int q = e / CH, j = e - q * CH;
         if (e >= nb * CH || j >= cnt) continue;
 #pragma unroll
-        for (int f = 0; f < NF; f++) lds[f][q][j] = v[u][f];
+        for (int f = 0; f < NF; f++) lds[f * FS + q * LD + j] = v[u][f];
       }
     }
     __syncthreads();
@@ -4643,15 +4647,15 @@ __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevPa
           cvs = sFirst / (float)(sN > 1 ? sN : 1);
           if (!prm.use_cv) { cvb = 0.0f; cvs = 0.0f; }
         }
-        const uint32_t code = __float_as_uint(lds[0][pp][j]);
+        const uint32_t code = __float_as_uint(lds[pp * LD + j]);
         steps += code >> 1;
         if (!(code & 1u)) continue;
-        const float total = lds[1][pp][j];
-        const float first = lds[2][pp][j];
+        const float total = lds[FS + pp * LD + j];
+        const float first = lds[2 * FS + pp * LD + j];
         sN += 1;
         const float fN = (float)sN;
-        const float be = (total - first - cvb) * lds[fb][pp][j];
-        const float se = (first - cvs) * lds[fs][pp][j];
+        const float be = (total - first - cvb) * lds[fb * FS + pp * LD + j];
+        const float se = (first - cvs) * lds[fs * FS + pp * LD + j];
         const float val = c == 0 ? total : be + se;
         const float delta = val - mean;
         mean += delta / fN;

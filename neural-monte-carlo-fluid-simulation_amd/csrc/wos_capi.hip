@@ -106,7 +106,9 @@ struct DevCtx {
   int64_t task_cap = 0;
   int32_t* d_pstate = nullptr; // per-point state + queue permutation of one batch, then bucket counters
   int64_t pstate_cap = 0;
-  unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counters
+  unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counters (kMainCounterSlots)
+  uint32_t* d_gmail = nullptr; // grid-wide tail spreading: kGsMailWords per wave of the walk grid (lazy)
+  int gmail_waves = 0;
   StatSlot slot[kStatSlots];   // ring indexed by ticket % kStatSlots
   uint64_t next_ticket = 1;
   hipEvent_t done = nullptr;   // end of the last enqueued solve
@@ -126,7 +128,10 @@ DevCtx g_ctx[kMaxDevices];  // never destroyed: the HIP runtime may be gone at p
 void ctx_free(DevCtx& c) {
   hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
   hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters); hipFree(c.d_rejtab);
+  hipFree(c.d_gmail);
   c.d_rejtab = nullptr;
+  c.d_gmail = nullptr;
+  c.gmail_waves = 0;
   for (StatSlot& q : c.slot) {
     if (q.ev0) hipEventDestroy(q.ev0);
     if (q.ev1) hipEventDestroy(q.ev1);
@@ -180,7 +185,7 @@ int ctx_ready(DevCtx& c, int device) {
     HIP_TRY(hipMemcpy(c.d_rejtab, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
   }
   HIP_TRY(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, device));
-  HIP_TRY(hipMalloc((void**)&c.d_counters, wos::kNumCounterSlots * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc((void**)&c.d_counters, wos::kMainCounterSlots * sizeof(unsigned long long)));
   for (StatSlot& q : c.slot) {
     HIP_TRY(hipHostMalloc((void**)&q.h_cnt, wos::kNumCounters * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&q.ev0));
@@ -1041,6 +1046,21 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     HIP_TRY(wos::occupancy_walk_blocks_per_cu(dim, dsc.geom_global != 0, dp, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
+  // Walks handed to idle waves anywhere in the grid, not only to siblings (device-scope
+  // mailboxes; wos_device.h "tail spreading across the grid")
+  const int gs_waves = grid_walk * wos::kWavesPerBlockHost;
+  if (dp.tail_spread && WOS_GRID_SPREAD && !(prm->schedule & WOS_SCHED_NO_GRID_SPREAD) && gs_waves > 0 &&
+      gs_waves <= wos::kGsMaxWaves) {
+    if (c.gmail_waves < gs_waves) {
+      hipFree(c.d_gmail);
+      c.d_gmail = nullptr;
+      c.gmail_waves = 0;
+      HIP_TRY(hipMalloc((void**)&c.d_gmail, (size_t)gs_waves * wos::kGsMailWords * sizeof(uint32_t)));
+      c.gmail_waves = gs_waves;
+    }
+    dp.gspread = reinterpret_cast<uint32_t*>(c.d_counters + wos::kGsSlot0);
+    dp.gspread_mail = c.d_gmail;
+  }
   const uint64_t ticket = c.next_ticket++;
   StatSlot& q = c.slot[ticket % kStatSlots];
   while ((int64_t)q.bev.size() < 4 * n_chunks) {
@@ -1057,7 +1077,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   q.geom_global = dsc.geom_global;
   q.dir_grid = dsc.dgrid != nullptr;
   HIP_TRY(hipEventRecord(q.ev0, st));
-  if (n_chunks == 0) HIP_TRY(wos::launch_zero(c.d_counters, wos::kNumCounterSlots, nullptr, 0, st));
+  if (n_chunks == 0) HIP_TRY(wos::launch_zero(c.d_counters, wos::kMainCounterSlots, nullptr, 0, st));
   for (int64_t k = 0; k < n_chunks; k++) {
     const int64_t b0 = k * chunk;
     hipEvent_t* ev = &q.bev[4 * k];
@@ -1069,18 +1089,21 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     unsigned long long* qslot = c.d_counters + wos::kNumCounters;
     unsigned int* q_points = (unsigned int*)qslot;
     unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
-    // one launch zeroes the counters (first chunk: all of them; later chunks: the queues)
-    // and the bucket histogram -- instead of two or three memset dispatches
+    const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
+    // one launch zeroes the counters (first chunk: all of them; later chunks: the queues and
+    // the spreading control words of this chunk's walk grid) and the bucket histogram --
+    // instead of two or three memset dispatches
+    const int gs_slots = dp.gspread ? wos::gs_ctrl_words(walk_grid * wos::kWavesPerBlockHost) / 2 : 0;
     HIP_TRY(wos::launch_zero(k == 0 ? c.d_counters : qslot,
-                             k == 0 ? wos::kNumCounterSlots : wos::kNumCounterSlots - wos::kNumCounters, tk.hist,
-                             2 * wos::kCostBuckets, st));
+                             (k == 0 ? wos::kNumCounterSlots : wos::kNumCounterSlots - wos::kNumCounters) + gs_slots,
+                             tk.hist, 2 * wos::kCostBuckets, st));
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, st));
     HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
                                     q_points, grid_fb, shmem_fb, lhs_floats, st));
     HIP_TRY(hipEventRecord(ev[1], st));
-    const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
+    dp.gspread_waves = walk_grid * wos::kWavesPerBlockHost;
     HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
                               shmem_walk, geom_floats_walk, st));
     HIP_TRY(hipEventRecord(ev[2], st));

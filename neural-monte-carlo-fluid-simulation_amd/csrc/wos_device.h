@@ -4121,12 +4121,17 @@ static_assert(sizeof(WalkState<2>) == 4 * (3 * 2 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)
 static_assert(sizeof(WalkState<3>) == 4 * (3 * 3 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<3> members");
 static_assert(sizeof(Gfn<2, false>) == 4 * (1 + 3 * 2 + 9) && sizeof(Gfn<3, true>) == 4 * (1 + 3 * 3 + 9), "Gfn members");
 static_assert(sizeof(Pcg32) == 8, "Pcg32 state");
-// one walk's state into / out of mailbox slot `slot` (word-major, kSpreadMax slots per word)
-template <int DIM, bool RB>
+// one walk's state into / out of mailbox slot `slot` (word-major, kSpreadMax slots per word);
+// AT: a global mailbox of another wave, through device-scope (sc1) stores and loads
+template <int DIM, bool RB, bool AT = false>
 __device__ __forceinline__ void spread_put(uint32_t* mb, int slot, const WalkState<DIM>& st, const Gfn<DIM, RB>& g,
                                            const Pcg32& ws, float ddist, float firstR, uint32_t wsteps, uint32_t t) {
   int q = 0;
-  auto put = [&](uint32_t v) { mb[(q++) * kSpreadMax + slot] = v; };
+  auto put = [&](uint32_t v) {
+    uint32_t* a = mb + (q++) * kSpreadMax + slot;
+    if (AT) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *a = v;
+  };
   auto putf = [&](float v) { put(__float_as_uint(v)); };
   for (int k = 0; k < DIM; k++) { putf(st.pt[k]); putf(st.n[k]); putf(st.prevDir[k]); }
   putf(st.prevDist); putf(st.throughput); put(st.onNeumann ? 1u : 0u); put((uint32_t)st.walkLength);
@@ -4139,11 +4144,14 @@ __device__ __forceinline__ void spread_put(uint32_t* mb, int slot, const WalkSta
   (void)firstR;  // 0 after every step (a boundary-start walk's first-sphere radius is used once)
   putf(ddist); put(wsteps); put(t);
 }
-template <int DIM, bool RB>
+template <int DIM, bool RB, bool AT = false>
 __device__ __forceinline__ void spread_get(const uint32_t* mb, int slot, WalkState<DIM>& st, Gfn<DIM, RB>& g,
                                            Pcg32& ws, float& ddist, float& firstR, uint32_t& wsteps, int64_t& t) {
   int q = 0;
-  auto get = [&]() { return mb[(q++) * kSpreadMax + slot]; };
+  auto get = [&]() {
+    const uint32_t* a = mb + (q++) * kSpreadMax + slot;
+    return AT ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *a;
+  };
   auto getf = [&]() { return __uint_as_float(get()); };
   for (int k = 0; k < DIM; k++) { st.pt[k] = getf(); st.n[k] = getf(); st.prevDir[k] = getf(); }
   st.prevDist = getf(); st.throughput = getf(); st.onNeumann = get() != 0u; st.walkLength = (int)get();
@@ -4160,6 +4168,63 @@ struct SpreadLDS {
   uint32_t busy, idle;
   uint32_t mbox[kBlock / kWave];
 };
+
+// ---- tail spreading across the grid (DevParams::gspread) ------------------------
+// The same hand-over between any two waves of the grid, pulled by the idle waves: an idle
+// wave probes other waves' request words (a sibling of its workgroup and a random wave of
+// the grid per poll, backing off while it finds none); a wave holding >= 2 walks once the
+// queue is dry keeps its request word open (1); a prober takes it with a compare-and-swap
+// (1 -> 2 + its index) and waits on its own response word; the holder sees the request at
+// the end of its step (the word is read during the step), hands over the upper half of its
+// walks (into the prober's LDS scratch when it is a sibling, else into its global mailbox),
+// then writes the response kGsFull | n (n may be 0 when its walks have ended meanwhile) and
+// reopens or closes its word.  A wave answers any request before it goes idle, so no prober
+// waits for nobody.
+// Termination: g_idle counts idle waves; a holder that gives walks takes their new owner
+// out of g_idle before the response is visible and stays busy itself, so g_idle reaches W
+// only when no walk is left anywhere: the wave whose announcement makes it W raises the done
+// flag (kGsDoneN replicas on separate lines) and every idle wave leaves when it sees it, or
+// after kGsMaxPolls polls (a grid whose waves are not all resident at once still drains; a
+// prober that is not waiting for a response holds nothing).
+// Only relaxed device-scope atomics (sc1 loads / stores, no cache write-back or invalidate
+// fences), ordered by waiting for the wave's outstanding memory operations (s_waitcnt).
+// Control words (zeroed per launch, gs_ctrl_words): [0] g_idle, done replica i at
+// kGsDone0 + 32 i, busy waves per SIMD from kGsSimd0, then per wave w [kGsRec0 + 4 w] response,
+// [+1] request.
+constexpr uint32_t kGsOpen = 1u, kGsFull = 0x100u, kGsLds = 0x200u;
+constexpr int kGsDone0 = 32, kGsDoneN = 64, kGsSimd0 = kGsDone0 + 32 * kGsDoneN;
+constexpr int kGsSimdSlots = 8 * 8 * 2 * 16 * 4;
+constexpr int kGsRec0 = kGsSimd0 + kGsSimdSlots;
+constexpr int kGsMaxPolls = 1 << 15;
+static_assert(kGsRec0 == kGsRecHost, "control layout (wos_scene.h gs_ctrl_words)");
+static_assert(kGsMailWords >= kSpreadMax * 32 && walk_pack_words<2>() <= 32 && walk_pack_words<3>() <= 32,
+              "global mailbox holds kSpreadMax walks");
+__device__ __forceinline__ uint32_t gs_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gs_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool gs_cas(uint32_t* p, uint32_t expect, uint32_t v) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+// every memory operation of the wave issued so far has completed (stores acknowledged)
+__device__ __forceinline__ void gs_wait_all() { __builtin_amdgcn_s_waitcnt(0); }
+// Probers only where the SIMD has at most WOS_GS_SIMD_MAX busy waves (-1: everywhere): a walk
+// handed to a wave whose SIMD is busy with other walks runs no faster, and the hand-over splits
+// one wave's cooperative queries into two.  Busy waves per SIMD are counted in
+// [kGsSimd0, kGsSimd0 + kGsSimdSlots), indexed by the wave's hardware slot (XCC, SE, SH, CU,
+// SIMD from HW_ID / XCC_ID; a heuristic: a wrong index costs speed, never correctness).
+#ifndef WOS_GS_SIMD_MAX
+#define WOS_GS_SIMD_MAX 1
+#endif
+__device__ __forceinline__ int gs_simd_slot() {
+  const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+  const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID [3:0]
+  const uint32_t simd = (hw >> 4) & 3u, cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
+  return (int)(((((xcc & 7u) * 8u + se) * 2u + sh) * 16u + cu) * 4u + simd) & (kGsSimdSlots - 1);
+}
 
 #ifndef WOS_WALK_WAVES_PER_EU
 #define WOS_WALK_WAVES_PER_EU 4
@@ -4195,6 +4260,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
   if (threadIdx.x == 0) { s_spread.busy = blockDim.x / kWave; s_spread.idle = 0u; }
   if (threadIdx.x < kBlock / kWave) s_spread.mbox[threadIdx.x] = 0u;
+  // grid-wide spreading (DevParams::gspread): its pointers are re-read from the kernel arguments
+  // where used (the per-iteration view), so that nothing of it is live across a step
+#define WOS_GS_VIEW()                                                                                    \
+  const int gW = (int)gridDim.x * (kBlock / kWave);                                                      \
+  uint32_t* const gs = (WOS_GRID_SPREAD && kSpread && prm.gspread != nullptr && prm.gspread_waves == gW) ? prm.gspread \
+                                                                                                        : nullptr; \
+  uint32_t* const gmail = prm.gspread_mail;                                                              \
+  const int gw = (int)blockIdx.x * (kBlock / kWave) + wave_u;                                            \
+  (void)gmail;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -4284,6 +4358,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   float ddist = 0.0f;
   uint32_t wsteps = 0;
   float firstR = 0.0f;  // BSTART: first sphere radius of the lane's walk, 0 after its first step
+  bool gopen = false;   // grid-wide spreading: this wave's request word is open (wave-uniform)
+  if (WOS_GRID_SPREAD && WOS_GS_SIMD_MAX >= 0 && kSpread && prm_arg.gspread != nullptr && lane == 0)  // busy on its SIMD
+    __hip_atomic_fetch_add(prm_arg.gspread + kGsSimd0 + gs_simd_slot(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   for (;;) {
     DIAG_T0(t_loop);
@@ -4335,6 +4412,76 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     if (__ballot(t >= 0) == 0) {
       if (S == 0 && exhausted) {  // queue drained and every lane idle
         if (!kSpread) break;
+        WOS_GS_VIEW();
+        if (gs != nullptr) {
+          uint32_t* const myreq = gs + kGsRec0 + 4 * gw + 1;
+          uint32_t* const myresp = gs + kGsRec0 + 4 * gw;
+          // close the request word; a request that came meanwhile is answered with nothing
+          if (gopen) {
+            if (lane == 0 && !gs_cas(myreq, kGsOpen, 0u)) {
+              const uint32_t rq = gs_ld(myreq);
+              gs_st(gs + kGsRec0 + 4 * ((int)rq - 2), kGsFull);
+              gs_st(myreq, 0u);
+            }
+            gopen = false;
+          }
+          // announce; the wave whose announcement makes every wave idle raises the done flag
+          uint32_t old = 0u;
+          uint32_t* const mysimd = gs + kGsSimd0 + gs_simd_slot();
+          if (lane == 0) {
+            if (WOS_GS_SIMD_MAX >= 0) __hip_atomic_fetch_sub(mysimd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            old = __hip_atomic_fetch_add(gs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (__builtin_amdgcn_readfirstlane((int)old) == gW - 1) {
+            static_assert(kGsDoneN == kWave, "one done replica per lane");
+            gs_st(gs + kGsDone0 + 32 * lane, 1u);
+            break;
+          }
+          int nsl = 1, got = 0;
+          uint32_t rsp = 0u;
+          for (int polls = 0; polls < kGsMaxPolls && !got; polls++) {
+            // probe two request words: lane 0 a sibling's, lane 1 a random wave's
+            const uint32_t h = (uint32_t)gw * 0x9E3779B1u ^ (uint32_t)polls * 0x85EBCA77u;
+            const int vic = lane == 0 ? (gw & ~3) | ((wave_u + 1 + polls) & 3) : (int)((h ^ (h >> 15)) % (uint32_t)gW);
+            const uint32_t x = lane < 2 ? gs_ld(gs + kGsRec0 + 4 * vic + 1) : 0u;
+            const uint32_t dn = lane == 0 ? gs_ld(gs + kGsDone0 + 32 * (gw & (kGsDoneN - 1))) : 0u;
+            const uint32_t sb = (WOS_GS_SIMD_MAX >= 0 && lane == 0) ? gs_ld(mysimd) : 0u;
+            if (__builtin_amdgcn_readfirstlane((int)dn) != 0) break;
+            // (a SIMD busy with other waves: no probe this round)
+            const bool quiet = WOS_GS_SIMD_MAX < 0 || __builtin_amdgcn_readfirstlane((int)sb) <= WOS_GS_SIMD_MAX;
+            const uint64_t open = __ballot(quiet && lane < 2 && x == kGsOpen && vic != gw);
+            if (open != 0) {
+              const int src = __builtin_ctzll(open);
+              int ok = 0;
+              if (lane == src) ok = gs_cas(gs + kGsRec0 + 4 * vic + 1, kGsOpen, 2u + (uint32_t)gw);
+              if (__builtin_amdgcn_readlane(ok, src)) {
+                // the holder answers at the end of its step, or before it goes idle
+                for (;;) {
+                  rsp = (uint32_t)__builtin_amdgcn_readfirstlane((int)gs_ld(myresp));
+                  if (rsp != 0u) break;
+                  __builtin_amdgcn_s_sleep(4);
+                }
+                if (lane == 0) gs_st(myresp, 0u);
+                got = (rsp & 0xFFu) != 0u;
+              }
+              nsl = 1;
+            } else if (nsl < 128) {
+              nsl *= 2;
+            }
+            if (!got)
+              for (int z = 0; z < nsl; z++) __builtin_amdgcn_s_sleep(2);
+          }
+          if (!got) break;  // done, or the poll budget spent: this wave holds and awaits nothing
+          if (WOS_GS_SIMD_MAX >= 0 && lane == 0)
+            __hip_atomic_fetch_add(mysimd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t n = rsp & 0xFFu;
+          if ((uint32_t)lane < n && (rsp & kGsLds))
+            spread_get<DIM, RB>(reinterpret_cast<const uint32_t*>(wscratch), lane, st, g, ws, ddist, firstR, wsteps, t);
+          else if ((uint32_t)lane < n)
+            spread_get<DIM, RB, true>(gmail + (size_t)gw * kGsMailWords, lane, st, g, ws, ddist, firstR, wsteps, t);
+          wave_sync();
+          continue;
+        }
         // idle: announce, then take a sibling's hand-over or leave once no wave holds walks
         if (lane == 0) {
           __hip_atomic_fetch_or(&s_spread.idle, 1u << wave_u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4367,13 +4514,62 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     const bool lone_it = __popcll(__ballot(t >= 0)) <= 2;
     if (lone_it) DIAG_COUNT(D_L_ITERS, 1);
 #endif
+    // grid-wide spreading: this wave's request word, read during the step
+    uint32_t greq = 0u;
+    if (WOS_GRID_SPREAD && gopen && lane == 0) greq = gs_ld(prm.gspread + kGsRec0 + 4 * ((int)blockIdx.x * (kBlock / kWave) + wave_u) + 1);
     const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;
     }
-    if (kSpread && exhausted && S == 0) {
+    WOS_GS_VIEW();
+    if (kSpread && exhausted && S == 0 && gs != nullptr) {
+      const uint64_t live = __ballot(t >= 0);
+      const int k = __popcll(live);
+      uint32_t* const myreq = gs + kGsRec0 + 4 * gw + 1;
+      if (gopen) {
+        const uint32_t rq = (uint32_t)__builtin_amdgcn_readfirstlane((int)greq);
+        if (rq >= 2u) {
+          // a prober's request: the upper half of the live walks (by lane rank, at most
+          // kSpreadMax; none when fewer than 2 are left)
+          const int r = (int)rq - 2;
+          const int kd = k >= 2 ? ((k / 2) < kSpreadMax ? (k / 2) : kSpreadMax) : 0;
+          const bool sib = (r & ~3) == (gw & ~3);
+          static_assert(kBlock / kWave == 4, "siblings: the waves 4 w .. 4 w + 3");
+          if (kd > 0) {
+            // the prober leaves g_idle before the answer is visible (this wave stays busy meanwhile)
+            if (lane == 0) __hip_atomic_fetch_sub(gs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+            const bool give = t >= 0 && rank >= k - kd;
+            if (give && sib)
+              spread_put<DIM, RB>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem + geom_floats) +
+                                                              (r & 3) * walk_scratch_bytes<DIM>()),
+                                  rank - (k - kd), st, g, ws, ddist, firstR, wsteps, (uint32_t)t);
+            else if (give)
+              spread_put<DIM, RB, true>(gmail + (size_t)r * kGsMailWords, rank - (k - kd), st, g, ws, ddist, firstR,
+                                        wsteps, (uint32_t)t);
+            if (give) t = -1;
+          }
+          gs_wait_all();
+          wave_sync();
+          if (lane == 0) {
+            gs_st(gs + kGsRec0 + 4 * r, kGsFull | (sib ? kGsLds : 0u) | (uint32_t)kd);
+            gs_st(myreq, k - kd >= 2 ? kGsOpen : 0u);  // a taken word is written by its holder alone
+          }
+          gopen = k - kd >= 2;
+        } else if (k < 2) {
+          int ok = 0;
+          if (lane == 0) ok = gs_cas(myreq, kGsOpen, 0u);
+          // (failed: a request came meanwhile -- answered after the next step, or on going idle)
+          if (__builtin_amdgcn_readfirstlane(ok)) gopen = false;
+        }
+      } else if (k >= 2) {
+        if (lane == 0) gs_st(myreq, kGsOpen);
+        gopen = true;
+      }
+    } else if (kSpread && exhausted && S == 0) {
       const uint64_t live = __ballot(t >= 0);
       const int k = __popcll(live);
       if (k >= 2 && __builtin_amdgcn_readfirstlane(
@@ -4425,6 +4621,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     }
 #endif
   }
+#undef WOS_GS_VIEW
   DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
   flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();

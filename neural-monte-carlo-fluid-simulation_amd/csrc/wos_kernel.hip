@@ -5,6 +5,7 @@
 // wos_first_ball_kernel, the persistent wos_walk_kernel and wos_fold_kernel (statistics
 // + masked outputs), all on the caller's stream.
 #include "wos_device.h"
+#include <algorithm>
 #include "wos_launch.h"
 
 namespace wos {
@@ -140,12 +141,15 @@ hipError_t launch_point_setup(int dim, const DevScene& sc, const DevParams& prm,
 }
 
 __global__ __launch_bounds__(256) void wos_zero_kernel(unsigned long long* a, int n64, uint32_t* b, int n32) {
-  for (int i = threadIdx.x; i < n64; i += blockDim.x) a[i] = 0ull;
-  for (int i = threadIdx.x; i < n32; i += blockDim.x) b[i] = 0u;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x, di = gridDim.x * blockDim.x;
+  for (int i = i0; i < n64; i += di) a[i] = 0ull;
+  for (int i = i0; i < n32; i += di) b[i] = 0u;
 }
 
 hipError_t launch_zero(unsigned long long* a, int n64, uint32_t* b, int n32, hipStream_t s) {
-  hipLaunchKernelGGL(wos_zero_kernel, dim3(1), dim3(256), 0, s, a, n64, b, n32);
+  // one block per 1024 u64 (the grid-wide spreading control words can be ~10^4)
+  const int grid = std::max(1, std::min(32, (std::max(n64, n32 / 2) + 1023) / 1024));
+  hipLaunchKernelGGL(wos_zero_kernel, dim3(grid), dim3(256), 0, s, a, n64, b, n32);
   return hipGetLastError();
 }
 

@@ -97,7 +97,7 @@ def test_schedule_bits_match_header():
     txt = open(HEADER).read()
     bits = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define WOS_(SCHED_\w+)\s+0x([0-9a-fA-F]+)u", txt)}
     assert set(bits) == {"SCHED_GEOM_GLOBAL", "SCHED_FULL_NEUMANN", "SCHED_NO_STAR_GRID", "SCHED_NO_DIR_GRID",
-                         "SCHED_NO_TAIL_SPREAD"}
+                         "SCHED_NO_TAIL_SPREAD", "SCHED_NO_GRID_SPREAD"}
     for name, v in bits.items():
         assert getattr(_lib, name) == v, name
     assert len(set(bits.values())) == len(bits) and all(v & (v - 1) == 0 for v in bits.values())

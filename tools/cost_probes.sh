@@ -2,7 +2,7 @@
 # Round-5 cost probes (GPU box, repo root): the fast-Bessel build against its exact-only twin
 # (solution hashes on B and D must match), then timings of those and of the WOS_PROBE
 # duplication builds, their SQ_INSTS_VALU (issue pass per variant), and the HBM-accounting
-# builds' FETCH_SIZE / WRITE_SIZE passes (config B).       tools/r5d_call.sh TAG
+# builds' FETCH_SIZE / WRITE_SIZE passes (config B).       tools/cost_probes.sh TAG
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
 TAG=$1
 L=$PWD/neural-monte-carlo-fluid-simulation_amd/lib/var

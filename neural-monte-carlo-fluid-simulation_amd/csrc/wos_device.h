@@ -1924,12 +1924,13 @@ static_assert(WOS_REJ_BMIN2 <= 16 && WOS_REJ_BMIN3 <= 16 && WOS_REJ_BMIN3_FB <= 
 #define WOS_REJ_OWN 4
 #endif
 constexpr int kRejOwn = WOS_REJ_OWN;
-// 3D (acceptance ~7 %): iterations of the own generation -- the walk kernel's 24 (a lane accepts
-// within them with P ~ 0.83; walk kernel on the cube at 128^3: 22.1 ms with 4, 20.8 with 16, 20.7
-// with 24), the first-ball kernel's 4 (16 made first balls +6 %): profiles/r5k_ab_own3.log,
-// r5l_ab_own3.log
+// 3D (acceptance ~7 %): iterations of the own generation -- the walk kernel's 32 (a lane accepts
+// within them with P ~ 0.9; walk kernel on the cube at 128^3: 22.1 ms with 4, 20.8 with 16, 20.7
+// with 24; with the radius-dependent screen (rej_xreject3) 19.4 ms with 24, 19.1 with 32), the
+// first-ball kernel's 4 (16 made first balls +6 %; the screen there +1-4 %): profiles/r5k_ab_own3.log,
+// r5l_ab_own3.log, r5zb_ab_xbound3.log, r5zc_ab_xbound3.log
 #ifndef WOS_REJ_OWN3
-#define WOS_REJ_OWN3 24
+#define WOS_REJ_OWN3 32
 #endif
 #ifndef WOS_REJ_OWN3_FB
 #define WOS_REJ_OWN3_FB WOS_REJ_OWN
@@ -2039,6 +2040,28 @@ __device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, f
   const float M = (2e-6f * e + ar * (3e-7f * ie + 2e-6f * e + 4e-6f * __builtin_fabsf(sh))) * c +
                   4e-6f * __builtin_fabsf(Tf) + 1e-30f;
   return u < Tf - M ? 1 : (u > Tf + M ? 0 : -1);
+}
+
+// Radius-dependent certain reject (3D Yukawa): the threshold
+//   T(r) = r (e^{-mu r} - rho sinh(mu r)) invNB <= r e^{-mu r} invNB,
+// rho = A0/A1 >= 0 and sinh >= 0 (the exact path's float subtraction of a non-negative term
+// cannot exceed e^{-mu r} either).  The bound carries a 0.1 % relative margin (hardware exp2,
+// the rounding of mu r and of the exact path's divisions: ~1e-5) plus 1e-6 R invNB absolute,
+// so u above it is the exact test's reject.  r = 0 and mu r >= 80 are left to the tests.
+// Round 2 measured the screen alone (every iteration still paid for the fast test whenever a
+// lane of its wave needed it); the own generation now screens its whole block first and runs
+// the fast test on the survivors only (tests/test_rejection_bounds.py checks the bound).
+#ifndef WOS_REJ_XB3
+#define WOS_REJ_XB3 1
+#endif
+#ifndef WOS_REJ_XB3_FB
+#define WOS_REJ_XB3_FB 0  // the first-ball kernel's own generation (4 iterations)
+#endif
+__device__ __forceinline__ bool rej_xreject3(float u, float r, float sqrtL, float invNB, float xabs) {
+  const float z = r * sqrtL;
+  if (!(r > 0.0f) || !(z < 80.0f)) return false;
+  const float e = __builtin_amdgcn_exp2f(z * -1.44269502f);
+  return u > (r * e * invNB) * 1.001f + xabs;
 }
 
 // exact 3D Yukawa test of one iteration with an owner's ball constants: the same
@@ -2172,6 +2195,31 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       const float invNB0 = 1.0f / (nrm * bound);
       const float qb0 = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB0);
       uint32_t acc = 0u, und = 0u;
+      if constexpr (DIM == 3 && (FB ? WOS_REJ_XB3_FB : WOS_REJ_XB3)) {
+        // phase A: every iteration of the block through the two certain-reject screens (the
+        // ball's bound on u, then the radius-dependent bound); phase B: the survivors in
+        // order through the fast and the exact test, the first accept wins.  The wave pays
+        // phase B's tests once per survivor round, not once per iteration.
+        const float rho0 = g.A0 / g.A1, xabs = 1e-6f * g.R * invNB0;
+        uint32_t surv = 0u;
+#pragma unroll 4
+        for (int b = 0; b < kRejOwnD<DIM, FB>; b++) {
+          const uint64_t st = rej_state(prm, s0, b);
+          const float u = draw_float(st);
+          DIAG_LANE(D_RITEMS);
+          if (!(u > qb0) && !rej_xreject3(u, draw_float(st * kPcgMult + kPcgInc) * g.R, g.sqrtLambda, invNB0, xabs))
+            surv |= 1u << b;
+        }
+        for (uint32_t m = surv; m != 0u; m &= m - 1u) {
+          const int b = __builtin_ctz(m);
+          float u, x;
+          rej_draws(prm, s0, b, &u, &x);
+          const float rr = x * g.R;
+          int dcs = rej_fast_decide3(u, rr, g.sqrtLambda, rho0, invNB0);
+          if (dcs < 0) dcs = rej_exact_decide3(u, rr, g.R, g.sqrtLambda, g.A0, g.A1, nrm, bound);
+          if (dcs == 1) { jacc = b; done = true; break; }
+        }
+      } else {
 #pragma unroll 4
       for (int b = 0; b < kRejOwnD<DIM, FB>; b++) {
         const uint64_t st = rej_state(prm, s0, b);
@@ -2201,6 +2249,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         const float p = g.evaluate() / nrm;
         const float pdfRadius = p / pdf_sphere_uniform<DIM>(g.r);
         if (u < pdfRadius / bound) { jacc = b; done = true; break; }
+      }
       }
     }
     j0 = own ? kRejOwnD<DIM, FB> : 0;

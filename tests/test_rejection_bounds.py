@@ -160,3 +160,41 @@ def test_tabulated_bound_dominates_exact_threshold(rej_table, dim, lam):
     # the subtracted term); near the closed form for large mu R, where the kernel
     # keeps the smaller of the two
     assert tighter and min(tighter) < 0.01
+
+
+def _xbound3(R, lam, xs, inv_nb):
+    """rej_xreject3's bound r e^{-mu r} invNB * 1.001 + 1e-6 R invNB (exp in double here; the
+    kernel's hardware exp2 is within a few ulp of it, far inside the 0.1 % margin)"""
+    sl = f32(np.sqrt(f32(lam)))
+    r = (xs * R).astype(np.float32)
+    z = (r * sl).astype(np.float32)
+    e = np.exp(-z.astype(np.float64))
+    return (r * e * float(inv_nb)) * 1.001 + 1e-6 * float(R) * float(inv_nb)
+
+
+@pytest.mark.parametrize("lam", [50.0, 350.0, 2000.0])
+def test_radius_bound_3d_dominates_exact_threshold(lam):
+    """the radius-dependent certain reject of the 3D own generation (rej_xreject3) is above the
+    exact threshold at every radius draw, and rejects most of what the exact test rejects"""
+    rng = np.random.default_rng(23)
+    radii = np.concatenate([np.exp(rng.uniform(np.log(1e-4), np.log(3.0), 40)), [1e-3, 0.02, 0.05, 0.5, 2.0]])
+    mu = np.sqrt(lam)
+    caught = []
+    for R in radii.astype(np.float32):
+        peak = min(1.0, 1.0 / (mu * float(R)))
+        xs = np.unique(np.concatenate([np.linspace(1e-5, 1.0, 600), rng.uniform(0, 1, 300),
+                                       peak * np.linspace(0.3, 1.7, 141)]))
+        xs = xs[(xs > 0) & (xs <= 1.0)].astype(np.float32)
+        T, q, (muR, inv_nb) = _thresholds_3d(f32(R), f32(lam), xs)
+        if not (inv_nb > 0 and np.isfinite(inv_nb)):
+            continue
+        z = (xs * R).astype(np.float32) * f32(np.sqrt(f32(lam)))
+        B = _xbound3(f32(R), lam, xs, inv_nb)
+        ok = np.isfinite(T) & (z < 80)
+        assert (T[ok] <= B[ok]).all(), (lam, float(R), float((T - B)[ok].max()))
+        # share of the reject interval (T, min(q, 1)) of u that the screen resolves
+        top = min(float(q), 1.0)
+        Tc, Bc = np.clip(T[ok], 0, top), np.clip(B[ok], 0, top)
+        if top - Tc.mean() > 0 and muR > 2.0:
+            caught.append(float(np.mean(top - Bc) / np.mean(top - Tc)))
+    assert caught and np.mean(caught) > 0.6, caught

@@ -3390,9 +3390,147 @@ __host__ __device__ constexpr int fb_points_per_wave(int n_pairs) {
              : 1;
 }
 
+// lhs_permute for the M = P * sd independent shuffles of a wave's P point slots (slot s at
+// wbase + 2 s lhs_floats: samples, then partners) in one pass: the same arithmetic per
+// shuffle, one set of wave syncs and LDS round trips for all of them (M * ceil(nstrat / 64)
+// <= 4 elements per lane).  Scratch: 7 words per element (fb_union_bytes(P * lhs_floats)).
+// Out of line: inlined, its element arrays pushed the first-ball kernels into spills.
+template <int SD, int R>
+__device__ __attribute__((noinline)) void lhs_permute_all_r(float* wbase, int lhs_floats, int P, int nstrat, char* scratch,
+                                                  int lane) {
+  constexpr int C = 4;  // elements per lane: shuffle m = c / R, step j = 64 (c % R) + lane
+  const int M = P * SD, N = M * nstrat;
+  int* link = reinterpret_cast<int*>(scratch);
+  int* val = link + N;
+  int* last = val + N;
+  int* perm = last + N;
+  int* tmp = perm + N;
+  unsigned long long* cmask = reinterpret_cast<unsigned long long*>(tmp + N + (N & 1));
+  int jj[C], bb[C];
+  const int* pd[C];
+  bool ok[C];
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    const int m = c / R;
+    jj[c] = (c % R) * kWave + lane;
+    ok[c] = m < M && jj[c] < nstrat;
+    bb[c] = m * nstrat;
+    pd[c] = reinterpret_cast<const int*>(wbase + 2 * (m / SD) * lhs_floats + lhs_floats) + (m % SD) * nstrat;
+  }
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (ok[c]) { link[bb[c] + jj[c]] = -1; last[bb[c] + jj[c]] = -1; cmask[bb[c] + jj[c]] = 0ull; }
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (ok[c]) {
+      const int q = pd[c][jj[c]];
+      if (q != jj[c]) atomicMax(&link[bb[c] + q], jj[c]);
+    }
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (ok[c]) val[bb[c] + jj[c]] = jj[c];
+  wave_sync();
+  for (;;) {
+    bool pending = false;
+    int nl[C], nv[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      nl[c] = -1;
+      nv[c] = 0;
+      if (ok[c]) {
+        const int p = link[bb[c] + jj[c]];
+        nl[c] = p;
+        nv[c] = val[bb[c] + jj[c]];
+        if (p >= 0) {
+          const int pp = link[bb[c] + p];
+          if (pp < 0) { nv[c] = val[bb[c] + p]; nl[c] = -1; } else { nl[c] = pp; pending = true; }
+        }
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      if (ok[c]) { link[bb[c] + jj[c]] = nl[c]; val[bb[c] + jj[c]] = nv[c]; }
+    wave_sync();
+    if (!__any(pending)) break;
+  }
+  // predecessor among steps with the same target, 64 steps (one round r) at a time
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+#pragma unroll
+    for (int c = r; c < C; c += R)
+      if (ok[c]) {
+        const int q = pd[c][jj[c]];
+        if (q != jj[c]) atomicOr(&cmask[bb[c] + q], 1ull << lane);
+      }
+    wave_sync();
+#pragma unroll
+    for (int c = r; c < C; c += R)
+      if (ok[c]) {
+        const int q = pd[c][jj[c]];
+        int Pv;
+        if (q == jj[c]) {
+          Pv = val[bb[c] + jj[c]];
+        } else {
+          const unsigned long long below = cmask[bb[c] + q] & ((1ull << lane) - 1ull);
+          const int pred = below ? r * kWave + 63 - __builtin_clzll(below) : last[bb[c] + q];
+          Pv = pred >= 0 ? val[bb[c] + pred] : q;
+        }
+        perm[bb[c] + jj[c]] = Pv;
+      }
+    wave_sync();
+#pragma unroll
+    for (int c = r; c < C; c += R)
+      if (ok[c]) {
+        const int q = pd[c][jj[c]];
+        if (q != jj[c]) { atomicMax(&last[bb[c] + q], jj[c]); cmask[bb[c] + q] = 0ull; }
+      }
+    wave_sync();
+  }
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (ok[c]) {
+      const int m = c / R;
+      const float* st = wbase + 2 * (m / SD) * lhs_floats;
+      tmp[bb[c] + jj[c]] = __float_as_int(st[SD * perm[bb[c] + jj[c]] + (m % SD)]);
+    }
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    if (ok[c]) {
+      const int m = c / R;
+      float* st = wbase + 2 * (m / SD) * lhs_floats;
+      st[SD * jj[c] + (m % SD)] = __int_as_float(tmp[bb[c] + jj[c]]);
+    }
+  wave_sync();
+}
+
+template <int DIM>
+__device__ __forceinline__ void lhs_permute_all(float* wbase, int lhs_floats, int P, int nstrat, char* scratch,
+                                                int lane) {
+  const int R = (nstrat + kWave - 1) / kWave;  // lhs_all_fits: P (DIM - 1) R <= 4
+  if (R == 1) lhs_permute_all_r<DIM - 1, 1>(wbase, lhs_floats, P, nstrat, scratch, lane);
+  else if (R == 2) lhs_permute_all_r<DIM - 1, 2>(wbase, lhs_floats, P, nstrat, scratch, lane);
+  else lhs_permute_all_r<DIM - 1, 4>(wbase, lhs_floats, P, nstrat, scratch, lane);
+}
+
+// 1: a wave's stratified samples (every point slot, every dimension) are shuffled in one
+// lhs_permute_all pass when they fit its registers, instead of one lhs_permute per slot and dimension
+#ifndef WOS_LHS_ALL
+#define WOS_LHS_ALL 1
+#endif
+__host__ __device__ constexpr bool lhs_all_fits(int n_pairs, int dim, int P) {
+  // 3D only: a 2D wave with one point has one shuffle, and the out-of-line pass costs the 2D
+  // first-ball kernel spills
+  return WOS_LHS_ALL && dim == 3 &&
+         P * (dim - 1) * ((2 * n_pairs + kWave - 1) / kWave == 3 ? 4 : (2 * n_pairs + kWave - 1) / kWave) <= 4;
+}
+
 template <int DIM>
 __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
-                                          char* scratch, int lane) {
+                                          char* scratch, int lane, bool permute = true) {
   constexpr int sd = DIM - 1;
   const int nstrat = 2 * prm.n_pairs;
   const int nd = nstrat * sd;
@@ -3427,6 +3565,7 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
     }
     wave_sync();
   }
+  if (!permute) return;  // the caller shuffles (lhs_permute_all)
   if (nstrat <= 4 * kWave) {
     for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);
     return;
@@ -3877,7 +4016,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // shuffle partners at wbase + 2 s lhs_floats; the rejection sampler's / shuffle's
   // scratch follows the P slots
   const int P = fb_points_per_wave(npairs);
-  float* wbase = smem + wave * (2 * P * lhs_floats + (int)(fb_union_bytes(lhs_floats) / sizeof(float)));
+  float* wbase = smem + wave * (2 * P * lhs_floats + (int)(fb_union_bytes(P * lhs_floats) / sizeof(float)));
   RejLDS* rejL = reinterpret_cast<RejLDS*>(wbase + 2 * P * lhs_floats);
   // this lane's point slot and pair (P == 1: all lanes serve the one point, pairs w0 + lane);
   // span = lanes per slot, so lane s * span is slot s's first lane (wave-uniform)
@@ -3953,12 +4092,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     DIAG_ADD(D_FB_SETUP, t_fb0);
     DIAG_COUNT(D_FB_PTS, __popcll(em));
     DIAG_T0(t_fb1);
+    const bool all = lhs_all_fits(npairs, DIM, P);
     for (int s = 0; s < P; s++) {
-      if (!((em >> (s * span)) & 1ull)) continue;
+      if (!all && !((em >> (s * span)) & 1ull)) continue;
       float* strat_s = wbase + 2 * s * lhs_floats;
       build_lhs<DIM>(prm, base + (int64_t)(idx + (unsigned int)s) * stride, strat_s,
-                     reinterpret_cast<int*>(strat_s + lhs_floats), reinterpret_cast<char*>(rejL), lane);
+                     reinterpret_cast<int*>(strat_s + lhs_floats), reinterpret_cast<char*>(rejL), lane, !all);
     }
+    if constexpr (DIM == 3)
+      if (all) lhs_permute_all<DIM>(wbase, lhs_floats, P, 2 * npairs, reinterpret_cast<char*>(rejL), lane);
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
     // lanes without a point of their own (an unestimated slot, or beyond P slots) run the

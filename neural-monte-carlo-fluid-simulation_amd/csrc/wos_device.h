@@ -102,6 +102,20 @@ static __shared__ unsigned long long s_diag[D_NUM];
 #define DIAG_MAX(slot, v)
 #endif
 
+// Timeline build only (-DWOS_TIMELINE=1, never shipped): the walk kernel's live lanes over
+// time.  Bins of 2^kTlShift ticks of the 100 MHz constant clock (s_memrealtime) from the
+// launch's first wave (g_tl[0]); per bin the wave-ticks of iterations with a live lane
+// (attributed to the bin the iteration starts in), the lane-ticks (live lanes x ticks), the
+// tasks handed out and the walks finished.  Printed and reset by diag_print.
+#ifndef WOS_TIMELINE
+#define WOS_TIMELINE 0
+#endif
+constexpr int kTlBins = 384, kTlShift = 10;
+enum { TL_WAVE = 0, TL_LANE, TL_START, TL_FIN, TL_NUM };
+#if WOS_TIMELINE
+static __device__ unsigned long long g_tl[1 + TL_NUM * kTlBins];
+#endif
+
 template <int DIM>
 __device__ __forceinline__ float dotv(const float* a, const float* b) {
   float s = a[0] * b[0] + a[1] * b[1];
@@ -4488,6 +4502,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const bool yuk0 = sc.absorption > 0.0f && prm.steps_before_tikhonov == 0;
   uint32_t c_iters = 0;
   wave_priority(prm.wave_prio);
+#if WOS_TIMELINE
+  uint64_t tl_t0 = 0;
+  if (lane == 0) {
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long old = atomicCAS(&g_tl[0], 0ull, now);
+    tl_t0 = old == 0ull ? now : old;
+  }
+  tl_t0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(tl_t0 >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)tl_t0);
+  auto tl_bin = [&](uint64_t ts) -> int {
+    const uint64_t b = ts > tl_t0 ? (ts - tl_t0) >> kTlShift : 0;
+    return b < (uint64_t)kTlBins ? (int)b : kTlBins - 1;
+  };
+#endif
 
   DIAG_T0(t_wave);
   // ---- task supply: a window [wq, we) of the global queue (wave-uniform; lane i
@@ -4570,6 +4598,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 
   for (;;) {
     DIAG_T0(t_loop);
+#if WOS_TIMELINE
+    const uint64_t tl_a = __builtin_amdgcn_s_memrealtime();
+#endif
     // per-iteration views of the kernel parameters and of the staged geometry (see kview)
     KernArgsPtr ka = kernargs_opaque();
     const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
@@ -4613,6 +4644,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
         }
         head = (head + take) & (kWave - 1);
         S -= take;
+#if WOS_TIMELINE
+        if (lane == 0) atomicAdd(&g_tl[1 + TL_START * kTlBins + tl_bin(tl_a)], (unsigned long long)take);
+#endif
       }
     }
     if (__ballot(t >= 0) == 0) {
@@ -4725,6 +4759,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     if (WOS_GRID_SPREAD && gopen && lane == 0) greq = gs_ld(prm.gspread + kGsRec0 + 4 * ((int)blockIdx.x * (kBlock / kWave) + wave_u) + 1);
     const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
+#if WOS_TIMELINE
+    {
+      const unsigned long long nlive = (unsigned long long)__popcll(__ballot(t >= 0));
+      const unsigned long long nfin = (unsigned long long)__popcll(__ballot(t >= 0 && code >= 0));
+      const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - tl_a;
+      if (lane == 0) {
+        const int b = tl_bin(tl_a);
+        atomicAdd(&g_tl[1 + TL_WAVE * kTlBins + b], dt);
+        atomicAdd(&g_tl[1 + TL_LANE * kTlBins + b], dt * nlive);
+        if (nfin) atomicAdd(&g_tl[1 + TL_FIN * kTlBins + b], nfin);
+      }
+    }
+#endif
     if (t >= 0 && code >= 0) {
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;

@@ -251,7 +251,27 @@ hipError_t occupancy_walk_blocks_per_cu(int dim, bool geom_global, const DevPara
 #undef WOS_OCC
 }
 
-void diag_dump(const char* tag) { diag_print(tag, HIP_SYMBOL(g_diag)); }
+void diag_dump(const char* tag) {
+  diag_print(tag, HIP_SYMBOL(g_diag));
+#if WOS_TIMELINE
+  // the walk kernel's live lanes over time (bins of 2^kTlShift ticks of the 100 MHz clock)
+  static unsigned long long tl[1 + TL_NUM * kTlBins];
+  hipMemcpyFromSymbol(tl, HIP_SYMBOL(g_tl), sizeof(tl));
+  const double bt = (double)(1u << kTlShift);
+  int last = 0;
+  for (int b = 0; b < kTlBins; b++)
+    if (tl[1 + TL_WAVE * kTlBins + b]) last = b;
+  fprintf(stderr, "[timeline %s] bin_us %.2f (bin: busy waves, live lanes, lanes/busy wave, tasks handed out, walks finished)\n",
+          tag, bt / 100.0);
+  for (int b = 0; b <= last; b++) {
+    const double w = tl[1 + TL_WAVE * kTlBins + b] / bt, l = tl[1 + TL_LANE * kTlBins + b] / bt;
+    fprintf(stderr, "[timeline %s] %3d %8.1f %9.1f %6.2f %9llu %9llu\n", tag, b, w, l, w > 0 ? l / w : 0.0,
+            tl[1 + TL_START * kTlBins + b], tl[1 + TL_FIN * kTlBins + b]);
+  }
+  static unsigned long long z[1 + TL_NUM * kTlBins];
+  hipMemcpyToSymbol(HIP_SYMBOL(g_tl), z, sizeof(z));
+#endif
+}
 
 // g_diag is per translation unit: `sym` is the calling unit's copy
 void diag_print(const char* tag, const void* sym) {

@@ -4301,8 +4301,10 @@ constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from th
 #define WOS_TASK_QUEUES 8
 #endif
 constexpr unsigned int kTaskQueues = WOS_TASK_QUEUES;
+// head windows of 16 tasks (32 before round 5): karman -1 %, stride-8 shard -1.5 %, the hardest point alone -6 to -8 %,
+// C and D unchanged (profiles/r5zi_ab_fb_order_head16.log, r5zj_ab_queue_knobs.log; 8 slowed the hardest point)
 #ifndef WOS_TASK_GRAB_HEAD
-#define WOS_TASK_GRAB_HEAD 32
+#define WOS_TASK_GRAB_HEAD 16
 #endif
 #ifndef WOS_TASK_HEAD
 #define WOS_TASK_HEAD 1

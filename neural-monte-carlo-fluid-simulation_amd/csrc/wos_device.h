@@ -5061,35 +5061,43 @@ __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevPa
   float mean = 0.0f, sFirst = 0.0f, cvb = 0.0f, cvs = 0.0f;
   int sN = 0;
   uint32_t steps = 0;
-  for (int c0 = 0; c0 < wpp; c0 += CH) {
-    const int cnt = (wpp - c0) < CH ? (wpp - c0) : CH;
-    for (int e0 = tid; e0 < nb * CH; e0 += NT * kFoldUnroll<DIM>) {
-      float v[kFoldUnroll<DIM>][NF];
+  // software pipeline: the block's next chunk of records is loaded into registers (UE slots per
+  // thread) while the current one is folded from LDS, so the HBM latency of the staging overlaps
+  // the Welford chains (D fold 1.84 -> 1.44 ms, E at 96^3 1.53 -> 1.29 ms; the 2D fold, one
+  // thread per point, measured 1-3 % slower with it: profiles/r5zm_ab_fold_pipe.log)
+  constexpr int UE = (kFold4Points * CH + NT - 1) / NT;
+  float w[UE][NF];
+  auto load_next = [&](int c0n) {
+    const int cntn = (wpp - c0n) < CH ? (wpp - c0n) : CH;
 #pragma unroll
-      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
-        const int e = e0 + u * NT;
-        const int q = e / CH, j = e - q * CH;
-        if (e >= nb * CH || j >= cnt) continue;
-        const int64_t t = (p0 + q) * wpp + c0 + j;
-        v[u][0] = __uint_as_float(tk.code[t]);
-        v[u][1] = tk.total[t];
-        v[u][2] = tk.first[t];
+    for (int u = 0; u < UE; u++) {
+      const int e = tid + u * NT;
+      const int q = e / CH, j = e - q * CH;
+      if (e >= nb * CH || j >= cntn) continue;
+      const int64_t t = (p0 + q) * wpp + c0n + j;
+      w[u][0] = __uint_as_float(tk.code[t]);
+      w[u][1] = tk.total[t];
+      w[u][2] = tk.first[t];
 #pragma unroll
-        for (int k = 0; k < DIM; k++) {
-          v[u][3 + k] = tk.bdir[k * T + t];
-          v[u][3 + DIM + k] = tk.sdir[k * T + t];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kFoldUnroll<DIM>; u++) {
-        const int e = e0 + u * NT;
-        const int q = e / CH, j = e - q * CH;
-        if (e >= nb * CH || j >= cnt) continue;
-#pragma unroll
-        for (int f = 0; f < NF; f++) lds[f * FS + q * LD + j] = v[u][f];
+      for (int k = 0; k < DIM; k++) {
+        w[u][3 + k] = tk.bdir[k * T + t];
+        w[u][3 + DIM + k] = tk.sdir[k * T + t];
       }
     }
+  };
+  load_next(0);
+  for (int c0 = 0; c0 < wpp; c0 += CH) {
+    const int cnt = (wpp - c0) < CH ? (wpp - c0) : CH;
+#pragma unroll
+    for (int u = 0; u < UE; u++) {
+      const int e = tid + u * NT;
+      const int q = e / CH, j = e - q * CH;
+      if (e >= nb * CH || j >= cnt) continue;
+#pragma unroll
+      for (int f = 0; f < NF; f++) lds[f * FS + q * LD + j] = w[u][f];
+    }
     __syncthreads();
+    if (c0 + CH < wpp) load_next(c0 + CH);  // in flight during the fold below
     if (estimate) {
       for (int j = 0; j < cnt; j++) {
         const int r = c0 + j;

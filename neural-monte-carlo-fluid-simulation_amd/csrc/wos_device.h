@@ -5026,8 +5026,8 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
 // (cvs) are kept by every lane.  Four chains in flight per point instead of one, and a quarter of
 // the LDS per point, so four times the waves: the fold was latency-bound on one thread's chain of
 // IEEE divisions per point (round 4, DESIGN).  Not for the derivative output (BVC's Dirichlet
-// samples, DevTasks::deriv): wos_fold_kernel keeps that.  Launched for 3D only (launch_fold): 2D's
-// five-float records fold faster one thread per point.
+// samples, DevTasks::deriv): wos_fold_kernel keeps that.  Both dimensions since its staging is
+// software-pipelined (before that, 2D's five-float records folded faster one thread per point).
 #ifndef WOS_FOLD4
 #define WOS_FOLD4 1
 #endif
@@ -5063,8 +5063,9 @@ __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevPa
   uint32_t steps = 0;
   // software pipeline: the block's next chunk of records is loaded into registers (UE slots per
   // thread) while the current one is folded from LDS, so the HBM latency of the staging overlaps
-  // the Welford chains (D fold 1.84 -> 1.44 ms, E at 96^3 1.53 -> 1.29 ms; the 2D fold, one
-  // thread per point, measured 1-3 % slower with it: profiles/r5zm_ab_fold_pipe.log)
+  // the Welford chains (D fold 1.84 -> 1.44 ms, E at 96^3 1.53 -> 1.29 ms: profiles/r5zm_ab_fold_pipe.log;
+  // with it the quad fold also beats the one-thread 2D fold: karman 0.109 -> 0.084 ms, C 0.81 -> 0.63 ms,
+  // r5zn_ab_fold4_2d.log)
   constexpr int UE = (kFold4Points * CH + NT - 1) / NT;
   float w[UE][NF];
   auto load_next = [&](int c0n) {

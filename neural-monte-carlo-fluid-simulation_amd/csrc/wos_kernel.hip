@@ -73,6 +73,8 @@ template __global__ void wos_fold_kernel<3>(const DevParams, const DevTasks, int
                                             int32_t*);
 template __global__ void wos_fold4_kernel<3>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
                                              int32_t*);
+template __global__ void wos_fold4_kernel<2>(const DevParams, const DevTasks, int64_t, float*, float*, int32_t*,
+                                             int32_t*);
 
 // math self-test kernel (parity of the deterministic math with the CPU oracle)
 __global__ void wos_math_selftest_kernel(int which, const double* x, double* out, int64_t n) {
@@ -195,11 +197,14 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
 
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s) {
-  // 3D only: the quad fold measured -1 % on D/E and +4-5 % on B/C (profiles/r5q_ab_fold4_pad.log)
-  if (WOS_FOLD4 && dim == 3 && tk.deriv == nullptr) {
+  // the quad fold (pipelined staging), both dimensions: profiles/r5zm_ab_fold_pipe.log, r5zn_ab_fold4_2d.log
+  if (WOS_FOLD4 && tk.deriv == nullptr) {
     const int g4 = (int)((n + kFold4Points - 1) / kFold4Points);
     if (g4 < 1) return hipSuccess;
-    hipLaunchKernelGGL(wos_fold4_kernel<3>, dim3(g4), dim3(4 * kFold4Points), 0, s, prm, tk, n, p, g, nest, steps);
+    if (dim == 3)
+      hipLaunchKernelGGL(wos_fold4_kernel<3>, dim3(g4), dim3(4 * kFold4Points), 0, s, prm, tk, n, p, g, nest, steps);
+    else
+      hipLaunchKernelGGL(wos_fold4_kernel<2>, dim3(g4), dim3(4 * kFold4Points), 0, s, prm, tk, n, p, g, nest, steps);
     return hipGetLastError();
   }
   const int grid = (int)((n + kFoldPoints - 1) / kFoldPoints);

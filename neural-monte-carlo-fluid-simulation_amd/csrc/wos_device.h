@@ -4527,7 +4527,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // flight during a whole step and a lane that finishes a walk starts the next one
   // from registers (cross-lane shuffles) instead of a chain of dependent global loads.
   // <= 64 points per window
-  const uint32_t G_win = kTaskGrab < 63u * wpp ? kTaskGrab : 63u * wpp;
+  // 3D: windows of 128 tasks (walk kernel -2 % on D and E, bit-exact: profiles/r5zo_ab_grab3.log; in 2D they
+  // slowed the karman stride-8 shard, r5zl_ab_star_help2_queue.log)
+  constexpr uint32_t kGrabD = DIM == 3 ? 128u : kTaskGrab;
+  const uint32_t G_win = kGrabD < 63u * wpp ? kGrabD : 63u * wpp;
   // the head of the cost order (the hardest points) is dealt in smaller windows, so the
   // long walks of one point spread over more waves: kTaskHead windows of kTaskGrabHead
   // tasks per wave of the grid, then windows of G_win

@@ -10,7 +10,11 @@ RNG is keyed by the global point index so results do not depend on N.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|B_grid|C|D|E|A]
                     [--scaling weak|strong]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (multi-GPU, RCCL)
+    torchrun --nproc-per-node N bench.py --gpus N ...   (same ranks, external launcher)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks
+itself (N child processes, rank r on GPU r, RCCL); under a launcher --gpus must equal
+WORLD_SIZE or it exits non-zero.
 
 Scaling: "weak" (default for B) gives every rank one 64k-point batch of an
 N x 64k projection; "strong" (default for the grid configs C, D, E -- BASELINE's
@@ -49,7 +53,9 @@ LIB = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG, "lib", "libwos_hip.so"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py starts them "
+                         "itself; under torchrun it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="B", help="A, B, B_grid, C, D or E (SURVEY.md section 8(d))")
@@ -68,7 +74,123 @@ def parse():
     ap.add_argument("--blocking", action="store_true",
                     help="wait for every solve before enqueueing the next (default: the next projection is "
                          "enqueued while the previous one runs; its stats are read after)")
+    # test hook for the rank launcher (tests/test_bench_dist.py): a CPU stand-in whose
+    # "solution" is the global point index -- no engine, no GPU, not a measurement
+    ap.add_argument("--standin-scene", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, grace_s=30.0):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of this
+    script (never an exec of this one), rank r on GPU r, rendezvous on 127.0.0.1.  The
+    parent touches no GPU; rank 0's JSON line goes straight to the shared stdout and
+    is the only one.  When a rank fails the others are given `grace_s` to finish and
+    are then terminated (a peer stuck in a collective would never return).  Returns
+    the worst child exit status."""
+    import signal
+    import subprocess
+    import threading
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE, text=True, bufsize=1))
+
+    def relay(r, pipe):
+        # stdout carries rank 0's JSON line only; anything else a rank prints there
+        # (gloo / RCCL chatter) goes to stderr
+        for ln in pipe:
+            out = sys.stdout if (r == 0 and ln.startswith("{")) else sys.stderr
+            out.write(ln)
+            out.flush()
+    relays = [threading.Thread(target=relay, args=(r, p.stdout), daemon=True) for r, p in enumerate(procs)]
+    for t in relays:
+        t.start()
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        failed_at = None
+        while any(p.poll() is None for p in procs):
+            if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+                failed_at = time.monotonic()
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                for p in procs:
+                    try:
+                        p.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                break
+            time.sleep(0.05)
+        for p in procs:
+            p.wait()
+        for t in relays:
+            t.join(timeout=10)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    rcs = [p.returncode for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr, flush=True)
+        # a signal death (negative) maps to 128 + signo, like a shell
+        return max(rc if rc > 0 else 128 - rc for rc in bad)
+    return 0
+
+
+def world_from_env(gpus):
+    """(world, rank, local_rank) of this process; raises SystemExit when --gpus and a
+    launcher's WORLD_SIZE disagree (a mismatched scaling line must never be printed)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    world = int(env_world) if env_world is not None else 1
+    if gpus is not None and gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: run 'bench.py --gpus {gpus}' "
+                         f"without a launcher, or under torchrun with --nproc-per-node {gpus}")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class StandInScene:
+    """--standin-scene: p = global index, grad = (index, -index) [, 0]; three steps per
+    point.  Exercises the launcher, sharding, gather and JSON line without an engine."""
+
+    def __init__(self, dim):
+        self.dim, self.pending, self.next = dim, {}, 0
+
+    def info(self):
+        return {"n_silhouettes": 0, "n_prims": 0}
+
+    def solve(self, x, params, index_base=0, index_stride=1, sync=False):
+        import torch
+        n = int(x.shape[0])
+        p = (index_base + index_stride * torch.arange(n, dtype=torch.float64)).float()
+        g = torch.stack([p, -p] + [torch.zeros_like(p)] * (self.dim - 2), 1)
+        t, self.next = self.next, self.next + 1
+        self.pending[t] = {"walk_steps": 3 * n, "wasted_steps": 0, "rejection_iters": 0, "kernel_ms": 1.0,
+                           "walk_ms": 1.0, "first_ball_ms": 0.0, "fold_ms": 0.0, "walk_launches": 1,
+                           "walks_recorded": n, "walks_escaped": 0, "walks_max_length": 0}
+        return p, g, {"ticket": t}
+
+    def solve_stats(self, ticket):
+        return self.pending.pop(ticket)
+
+    def close(self):
+        pass
 
 
 def lib_sha16():
@@ -271,30 +393,44 @@ def shard_projection(a, scene, params, pts, torch, dev, shards=8):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        # no launcher: this process only starts and waits for the N ranks (no GPU call here)
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    world, rank, local_rank = world_from_env(a.gpus)
     scaling = a.scaling or ("weak" if a.config == "B" else "strong")
     if scaling == "weak" and a.config != "B":
         raise SystemExit("weak scaling is defined for config B (random points per rank); use --scaling strong")
+    if a.standin_scene:
+        a.no_cpu_baseline = a.no_projection_wall = True
     import torch
     import torch.distributed as dist
     from wos_amd import WosScene, solver_params, workloads
-    # one rank per GPU; more ranks than GPUs (the gloo rehearsal on a 1-GPU box) share them
-    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    if a.standin_scene:
+        dev = torch.device("cpu")
+    else:
+        # one rank per GPU; more ranks than GPUs (the gloo rehearsal on a 1-GPU box) share them
+        n_dev = torch.cuda.device_count()
+        if world > 1 and a.dist_backend == "nccl" and n_dev < world:
+            raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {n_dev} visible "
+                             "(--dist-backend gloo lets ranks share a GPU)")
+        dev = torch.device("cuda", local_rank % max(1, n_dev))
     if world > 1:
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-    torch.cuda.set_device(dev)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
 
     cfg = workloads.config_by_name(a.config, n_points=a.points * world if scaling == "weak" else None)
     pts_all = cfg["points"]
     n_all = pts_all.shape[0]
     dim = cfg["dim"]
-    scene = WosScene(cfg["vertices"], cfg["prims"], torch.from_numpy(cfg["source"]).to(dev), cfg["absorption"],
-                     watertight=True, device=dev.index, **cfg["scene_kw"])
+    if a.standin_scene:
+        scene = StandInScene(dim)
+    else:
+        scene = WosScene(cfg["vertices"], cfg["prims"], torch.from_numpy(cfg["source"]).to(dev),
+                         cfg["absorption"], watertight=True, device=dev.index, **cfg["scene_kw"])
     info = scene.info()
     params = solver_params(cfg["solver"], cfg["output"])
 
@@ -391,6 +527,8 @@ def main():
             "kernel_split_ms": {"first_ball": float(np.mean(fb_ms)), "walk": float(np.mean(walk_ms)),
                                 "fold": float(np.mean(fold_ms)), "total": kms},
         }
+        if a.standin_scene:
+            line["engine"] = "stand-in scene (launcher test hook): not a measurement"
         if strong is not None:
             line["strong"] = strong
         if shard is not None:

@@ -40,12 +40,19 @@ def sharded_projection(solve_local, pts, rank, world, dim, group=None, device=No
     p, g = solve_local(local, rank, world)
     p = torch.as_tensor(p, device=device)
     g = torch.as_tensor(g, device=device).reshape(-1, dim)
-    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=device)
-    send[: idx.size, 0] = p
-    send[: idx.size, 1:] = g
-    if world > 1 or force_gather:
-        buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=device)
+    gathered = world > 1 or force_gather
+    # gloo has no device collectives: a gloo group (CPU rehearsal of the N-rank path,
+    # ranks sharing one GPU) stages the shard through host memory
+    staged = gathered and p.device.type != "cpu" and dist.get_backend(group) == "gloo"
+    bdev = torch.device("cpu") if staged else p.device
+    send = torch.zeros(n_pad, 1 + dim, dtype=torch.float32, device=bdev)
+    send[: idx.size, 0] = p.to(bdev)
+    send[: idx.size, 1:] = g.to(bdev)
+    if gathered:
+        buf = torch.empty(world * n_pad, 1 + dim, dtype=torch.float32, device=bdev)
         dist.all_gather_into_tensor(buf, send, group=group)
+        if staged:
+            buf = buf.to(p.device)
     else:
         buf = send
     # (world, n_pad) blocks -> point order r + world * j; the padded rows (j >= count of

@@ -119,9 +119,18 @@ class PressureProjector:
         div = proj.source_from_velocity(u_prev, vis_resolution, scene_size)
         p, grad_p = proj.solve(div)
         loss = proj.projection_loss(u, u_prev, grad_p, n)
+
+    Multi-GPU (one process per GPU): pass the process group
+    (`group=torch.distributed.group.WORLD` after init_process_group("nccl")).  Every
+    rank holds the same pressure samples; rank r solves the stride shard r, r + W, ...
+    keyed by GLOBAL sample index, and ONE all_gather_into_tensor of [p, grad p] (RCCL
+    over xGMI) hands every rank the full field -- bit-identical to a one-GPU solve, so
+    projection_loss draws from it unchanged.  `force_gather` runs the collective even in
+    a world of one.
     """
 
-    def __init__(self, scene_config, solver_config, output_config, pressure_samples, device=None):
+    def __init__(self, scene_config, solver_config, output_config, pressure_samples, device=None,
+                 group=None, force_gather=False):
         import zombie_bindings  # the drop-in shim parses the reference's scene keys
         self.dim = int(pressure_samples.shape[-1])
         self.device = pressure_samples.device if device is None else torch.device(device)
@@ -129,6 +138,7 @@ class PressureProjector:
         self.scene = zombie_bindings.Scene(dict(scene_config), placeholder, device=self.device.index or 0)
         self.params = _engine.solver_params(solver_config, output_config)
         self.samples = pressure_samples.detach().to(self.device, torch.float32).contiguous()
+        self.group, self.force_gather = group, force_gather
         self.last_stats = None
 
     def source_from_velocity(self, velocity_fn, resolution, size):
@@ -140,12 +150,32 @@ class PressureProjector:
         div = divergence(u, grid)
         return (-div[..., 0]).detach().contiguous()
 
-    def solve(self, div):
-        """wost_pressure (model_split.py:185-202) with device tensors in and out."""
+    def _set_source(self, div):
         self.scene._scene.set_source(div)
-        p, g, st = self.scene._scene.solve(self.samples, self.params)
-        self.last_stats = st
-        return p, g
+
+    def _solve_points(self, x, index_base, index_stride):
+        return self.scene._scene.solve(x, self.params, index_base=index_base, index_stride=index_stride)
+
+    def solve(self, div):
+        """wost_pressure (model_split.py:185-202) with device tensors in and out; with a
+        process group, this rank's stride shard + one all-gather (wos_amd.dist)."""
+        self._set_source(div)
+        if self.group is None and not self.force_gather:
+            p, g, st = self._solve_points(self.samples, 0, 1)
+            self.last_stats = st
+            return p, g
+        import torch.distributed as tdist
+        from . import dist as _dist
+        group = self.group if self.group is not None else tdist.group.WORLD
+        rank, world = tdist.get_rank(group), tdist.get_world_size(group)
+
+        def solve_local(local, base, stride):
+            p, g, st = self._solve_points(local.contiguous(), base, stride)
+            self.last_stats = st  # this rank's shard
+            return p, g
+
+        return _dist.sharded_projection(solve_local, self.samples, rank, world, self.dim, group=group,
+                                        device=self.device, force_gather=self.force_gather)
 
     def projection_loss(self, velocity, velocity_prev, grad_p, n_samples, generator=None):
         """_project_velocity (model_split.py:272-283): u <- u_prev - grad p on random

@@ -28,6 +28,8 @@ def main():
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda", 0)
+    if backend == "projector":
+        return projector(rank, world, dev, out_dir)
     if backend == "nccl":
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
@@ -57,6 +59,36 @@ def main():
     dist.barrier()
     dist.destroy_process_group()
     sc.close()
+
+
+def projector(rank, world, dev, out_dir):
+    """BACKEND "projector": the caller-facing PressureProjector over an RCCL group
+    (world 1 on a one-GPU box, collective forced) against the same projector unsharded."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from wos_amd import projection as pj
+    from wos_amd import workloads
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    cfg = workloads.karman_config(n_walks=32, n_points=4096)
+    size = workloads.scene_size(workloads.KARMAN_OBJ)
+    scene_cfg = dict(cfg["scene"], boundary=cfg["obj"])
+    samples = torch.from_numpy(cfg["points"]).to(dev)
+    torch.manual_seed(3)
+    u = pj.Siren(2, 2, 2, 64).to(dev)
+    sharded = pj.PressureProjector(scene_cfg, cfg["solver"], cfg["output"], samples,
+                                   group=dist.group.WORLD, force_gather=True)
+    div = sharded.source_from_velocity(u, 200, size)
+    p, g = sharded.solve(div)
+    assert p.is_cuda and g.is_cuda and dist.get_backend() == "nccl"
+    plain = pj.PressureProjector(scene_cfg, cfg["solver"], cfg["output"], samples)
+    p1, g1 = plain.solve(div)
+    print(f"rank {rank}: PressureProjector over RCCL, world {world}, {samples.shape[0]} samples", flush=True)
+    np.savez(os.path.join(out_dir, f"proj{rank}.npz"), p=p.cpu().numpy(), g=g.cpu().numpy(),
+             p1=p1.cpu().numpy(), g1=g1.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

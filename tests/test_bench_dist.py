@@ -92,6 +92,64 @@ def test_bench_gather_and_strong_line(tmp_path, world):
         assert s["value"] > 0 and s["ms_per_step"] > 0
 
 
+def _bench(args, env_extra=None, timeout=120):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, cwd=REPO,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_gpus_flag_launches_ranks(world):
+    """`bench.py --gpus N` with no launcher starts N ranks itself (the driver's form of
+    the scaling run): exactly one JSON line, n_gpus == N, the strong line's step count
+    covering the fixed point set once (3 stand-in steps per point, summed over ranks)."""
+    r = _bench(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--dist-backend", "gloo",
+                "--points", "4096", "--standin-scene"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["steps"] == 3 and line["scaling"] == "weak"
+    assert line["walk_steps_per_projection"] == 3 * line["config"]["points"]
+    assert line["config"]["points"] > 0.9 * 4096 * world
+    assert line["strong"]["n_gpus"] == world and line["strong"]["walk_steps_per_projection"] == 3 * 65398
+    assert "stand-in" in line["engine"]
+
+
+def test_bench_gpus_mismatch_with_launcher_fails():
+    """Under a launcher, --gpus must equal WORLD_SIZE: no line, non-zero exit."""
+    r = _bench(["--gpus", "8", "--steps", "1", "--standin-scene"],
+               {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_failed_rank_fails_the_job():
+    """A rank that dies (here: an unknown config, before the rendezvous) makes the
+    launcher exit non-zero within its grace period instead of hanging on the peers."""
+    r = _bench(["--gpus", "2", "--config", "nope", "--scaling", "strong", "--dist-backend", "gloo",
+                "--standin-scene"], timeout=100)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_gloo_hip_engine():
+    """`bench.py --gpus 2 --dist-backend gloo` on the GPU box, no torchrun: two ranks on
+    GPU 0 through the HIP engine, one line with n_gpus 2."""
+    r = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--points", "8192", "--dist-backend", "gloo",
+                "--no-cpu-baseline"], timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["strong"]["n_gpus"] == 2 and "engine" not in line
+    assert line["value"] > 0 and line["lib_sha16"]
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_gloo_hip_engine(tmp_path, gpu):
     """bench.py --gpus 2 over gloo with both ranks on GPU 0: one JSON line with the

@@ -182,3 +182,92 @@ def test_sharded_projection_hip_engine(tmp_path, gpu, oracle, world):
         d = np.load(tmp_path / f"rank{r}.npz")
         np.testing.assert_array_equal(d["p"], p1)
         np.testing.assert_array_equal(d["g"], g1)
+
+
+def _oracle_projector(group, force_gather=False):
+    """A PressureProjector whose engine calls are the CPU oracle (test infrastructure):
+    the sharding / gather / loss logic is the product's, unchanged."""
+    import torch
+    import objparse
+    import oracle_lib
+    from wos_amd import projection as pj
+    from wos_amd import workloads
+
+    cfg = workloads.karman_config(n_walks=16)
+    v, ix = objparse.load(cfg["obj"], 2)
+    prm = oracle_lib.make_params(cfg["solver"], cfg["output"], n_threads=2)
+
+    class OracleProjector(pj.PressureProjector):
+        def __init__(self):
+            self.dim, self.device = 2, torch.device("cpu")
+            self.samples = torch.from_numpy(cfg["points"][:257].copy())
+            self.group, self.force_gather, self.last_stats = group, force_gather, None
+
+        def _set_source(self, div):
+            self.osc = oracle_lib.OracleScene(v, ix, div.numpy(), 350.0)
+
+        def _solve_points(self, x, base, stride):
+            p, g, _, _, st = oracle_lib.solve(self.osc, prm, x.numpy(), index_base=base, index_stride=stride)
+            return torch.from_numpy(p), torch.from_numpy(g), st
+
+    return OracleProjector(), torch.from_numpy(cfg["source"])
+
+
+def _projector_worker(rank, world, port, out_dir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "neural-monte-carlo-fluid-simulation_amd")]
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    proj, div = _oracle_projector(dist.group.WORLD)
+    p, g = proj.solve(div)
+    assert proj.last_stats["points_estimated"] <= (257 + world - 1) // world
+    ident = lambda x: x * 0  # noqa: E731
+    loss = proj.projection_loss(ident, ident, g, 64, generator=torch.Generator().manual_seed(5))
+    np.savez(os.path.join(out_dir, f"proj{rank}.npz"), p=p.numpy(), g=g.numpy(), loss=float(loss))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pressure_projector_sharded_matches_single_process(tmp_path, oracle, world):
+    """PressureProjector(group=WORLD): each rank solves its stride shard of the pressure
+    samples, one all-gather hands every rank the full [p, grad p]; bit-identical to the
+    one-process projector, and projection_loss on the gathered field equals it too."""
+    import torch
+    port = _free_port()
+    mp.start_processes(_projector_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    proj, div = _oracle_projector(None)
+    p0, g0 = proj.solve(div)
+    ident = lambda x: x * 0  # noqa: E731
+    loss0 = float(proj.projection_loss(ident, ident, g0, 64, generator=torch.Generator().manual_seed(5)))
+    for r in range(world):
+        d = np.load(tmp_path / f"proj{r}.npz")
+        np.testing.assert_array_equal(d["p"], p0.numpy())
+        np.testing.assert_array_equal(d["g"], g0.numpy())
+        assert float(d["loss"]) == loss0
+
+
+@pytest.mark.gpu
+def test_pressure_projector_rccl_world1(tmp_path, gpu):
+    """PressureProjector(group=WORLD, force_gather=True) on a world-1 RCCL group: the
+    shard + all_gather_into_tensor path on MI355X equals the unsharded projector bit
+    for bit (device tensors throughout)."""
+    import subprocess
+    import sys
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_engine_worker.py")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, worker, "0", "1", str(port), str(tmp_path), "projector"], env=env,
+                       capture_output=True, text=True, timeout=150)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "PressureProjector over RCCL" in r.stdout
+    d = np.load(tmp_path / "proj0.npz")
+    assert d["p"].shape[0] > 3000
+    np.testing.assert_array_equal(d["p"].view(np.uint32), d["p1"].view(np.uint32))
+    np.testing.assert_array_equal(d["g"].view(np.uint32), d["g1"].view(np.uint32))

@@ -538,8 +538,16 @@ def main():
                                         note=f"rank 0's share of an 8-GPU strong-scaled config {a.config} "
                                              "projection, timed alone on this GPU (all-gather excluded)")
         if sq:
-            line["valu_issue"] = {"kernel": sq["kernel"], "frac": sq["valu_issue_frac"],
+            # calibrated: each instruction type at its measured SIMD-cycles (tools/collect_sq.py combine);
+            # older profiles carry only the 4-cycle CDNA3 rule of thumb
+            cal = "valu_issue_frac" in sq and "issue_cycles" in sq
+            line["valu_issue"] = {"kernel": sq["kernel"],
+                                  "frac": sq["valu_issue_frac"] if cal else None,
+                                  "frac_4cyc": sq.get("valu_issue_frac_4cyc", sq.get("valu_issue_frac")),
+                                  "calibrated": cal,
+                                  "parts": sq.get("valu_issue_parts"),
                                   "wait_any_frac": sq["wait_any_frac"], "wait_inst_frac": sq["wait_inst_frac"],
+                                  "active_frac": sq.get("active_frac"),
                                   "source": f"{sq['file']}: {sq['source']}"}
         if world == 1 and a.config == "B" and not a.no_projection_wall:
             # the metric's second half: wall time of one whole projection call as the

@@ -154,7 +154,8 @@ typedef struct wos_solver_params {
 #define WOS_SCHED_NO_STAR_GRID  0x4u  /* no star-radius cell grid: the cooperative group scan alone */
 #define WOS_SCHED_NO_DIR_GRID   0x8u  /* no Dirichlet-distance cell grid (2D): the culled scans alone */
 #define WOS_SCHED_NO_TAIL_SPREAD 0x10u /* no hand-over of walks to idle sibling waves once the queue is dry */
-#define WOS_SCHED_NO_GRID_SPREAD 0x20u /* hand walks over inside a workgroup only, not to idle waves anywhere */
+#define WOS_SCHED_NO_GRID_SPREAD 0x20u /* reserved, no effect: grid-wide hand-over was measured slower than the
+                                          in-workgroup one and removed (ABI 9 keeps the bit so callers still build) */
 
 void wos_default_params(wos_solver_params *p);
 

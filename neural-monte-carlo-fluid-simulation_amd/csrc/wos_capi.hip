@@ -107,8 +107,6 @@ struct DevCtx {
   int32_t* d_pstate = nullptr; // per-point state + queue permutation of one batch, then bucket counters
   int64_t pstate_cap = 0;
   unsigned long long* d_counters = nullptr;  // kNumCounters u64 + work counters (kMainCounterSlots)
-  uint32_t* d_gmail = nullptr; // grid-wide tail spreading: kGsMailWords per wave of the walk grid (lazy)
-  int gmail_waves = 0;
   StatSlot slot[kStatSlots];   // ring indexed by ticket % kStatSlots
   uint64_t next_ticket = 1;
   hipEvent_t done = nullptr;   // end of the last enqueued solve
@@ -128,10 +126,7 @@ DevCtx g_ctx[kMaxDevices];  // never destroyed: the HIP runtime may be gone at p
 void ctx_free(DevCtx& c) {
   hipFree(c.d_pts); hipFree(c.d_p); hipFree(c.d_g); hipFree(c.d_nest); hipFree(c.d_steps);
   hipFree(c.d_jump); hipFree(c.d_tasks); hipFree(c.d_pstate); hipFree(c.d_counters); hipFree(c.d_rejtab);
-  hipFree(c.d_gmail);
   c.d_rejtab = nullptr;
-  c.d_gmail = nullptr;
-  c.gmail_waves = 0;
   for (StatSlot& q : c.slot) {
     if (q.ev0) hipEventDestroy(q.ev0);
     if (q.ev1) hipEventDestroy(q.ev1);
@@ -702,16 +697,10 @@ wos::DevTasks task_view(DevCtx& c, int dim, int64_t T, int32_t wpp) {
 
 // Stream priorities of boundary value caching's walk sets: the Dirichlet samples' solve and
 // the Neumann samples' walks feed the splat (high), the near-boundary walks do not (low).
-#ifndef WOS_BVC_PRIO
-#define WOS_BVC_PRIO 1
-#endif
-#ifndef WOS_BVC_WPRIO
-#define WOS_BVC_WPRIO 1
-#endif
 
 int bvc_priority(bool high) {
   int least = 0, greatest = 0;
-  if (!WOS_BVC_PRIO || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
   return high ? greatest : least;
 }
 
@@ -1046,21 +1035,6 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     HIP_TRY(wos::occupancy_walk_blocks_per_cu(dim, dsc.geom_global != 0, dp, shmem_walk, &bpc_walk));
     grid_walk = std::max(1, bpc_walk) * std::max(1, c.num_cus);
   }
-  // Walks handed to idle waves anywhere in the grid, not only to siblings (device-scope
-  // mailboxes; wos_device.h "tail spreading across the grid")
-  const int gs_waves = grid_walk * wos::kWavesPerBlockHost;
-  if (dp.tail_spread && WOS_GRID_SPREAD && !(prm->schedule & WOS_SCHED_NO_GRID_SPREAD) && gs_waves > 0 &&
-      gs_waves <= wos::kGsMaxWaves) {
-    if (c.gmail_waves < gs_waves) {
-      hipFree(c.d_gmail);
-      c.d_gmail = nullptr;
-      c.gmail_waves = 0;
-      HIP_TRY(hipMalloc((void**)&c.d_gmail, (size_t)gs_waves * wos::kGsMailWords * sizeof(uint32_t)));
-      c.gmail_waves = gs_waves;
-    }
-    dp.gspread = reinterpret_cast<uint32_t*>(c.d_counters + wos::kGsSlot0);
-    dp.gspread_mail = c.d_gmail;
-  }
   const uint64_t ticket = c.next_ticket++;
   StatSlot& q = c.slot[ticket % kStatSlots];
   while ((int64_t)q.bev.size() < 4 * n_chunks) {
@@ -1090,12 +1064,10 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     unsigned int* q_points = (unsigned int*)qslot;
     unsigned int* q_tasks = (unsigned int*)(c.d_counters + wos::kTaskQueueSlot0);
     const int walk_grid = (int)std::min<int64_t>(grid_walk, (tk.T + 63) / 64);
-    // one launch zeroes the counters (first chunk: all of them; later chunks: the queues and
-    // the spreading control words of this chunk's walk grid) and the bucket histogram --
-    // instead of two or three memset dispatches
-    const int gs_slots = dp.gspread ? wos::gs_ctrl_words(walk_grid * wos::kWavesPerBlockHost) / 2 : 0;
+    // one launch zeroes the counters (first chunk: all of them; later chunks: the queues) and
+    // the bucket histogram -- instead of two or three memset dispatches
     HIP_TRY(wos::launch_zero(k == 0 ? c.d_counters : qslot,
-                             (k == 0 ? wos::kNumCounterSlots : wos::kNumCounterSlots - wos::kNumCounters) + gs_slots,
+                             k == 0 ? wos::kNumCounterSlots : wos::kNumCounterSlots - wos::kNumCounters,
                              tk.hist, 2 * wos::kCostBuckets, st));
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, st));
@@ -1103,7 +1075,6 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
                                     q_points, grid_fb, shmem_fb, lhs_floats, st));
     HIP_TRY(hipEventRecord(ev[1], st));
-    dp.gspread_waves = walk_grid * wos::kWavesPerBlockHost;
     HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
                               shmem_walk, geom_floats_walk, st));
     HIP_TRY(hipEventRecord(ev[2], st));
@@ -1458,7 +1429,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
   if (dir_solve) {
     SolveExtra ex;
     ex.force_estimate = true;
-    ex.wave_prio = WOS_BVC_WPRIO ? 2 : 0;
+    ex.wave_prio = 2;
     for (const Run& r : runs) {
       if (!r.dir) continue;
       ex.ddir = d_ddir + 2 * r.b0;
@@ -1486,7 +1457,7 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     dp.rej_tab = c.d_rejtab;
     // the Neumann samples' harmonic walks run longest (reflecting, up to maxWalkLength): top
     // issue priority; the near-boundary walks feed nothing downstream: none
-    dp.wave_prio = WOS_BVC_WPRIO && k == 0 ? 3 : 0;
+    dp.wave_prio = k == 0 ? 3 : 0;
     const int64_t wpp = n_walks;
     wos::DevTasks tk = task_view_in(w.tasks, w.pstate, w.pstate_cap, 2, np_ * wpp, (int32_t)wpp);
     tk.n0 = tk.bdir;

@@ -412,9 +412,6 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // result in lane 63.  A source lane outside the row mask keeps the destination's own
 // value, which leaves a minimum unchanged.  Needs every lane active (the solo query
 // forms are convergent); otherwise the ds_bpermute butterfly above.
-#ifndef WOS_DPP_MIN
-#define WOS_DPP_MIN 1
-#endif
 template <int CTRL, int ROWS = 0xF>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWS, 0xF, false);
@@ -427,7 +424,7 @@ __device__ __forceinline__ void dpp_min_step(uint32_t& hi, uint32_t& lo) {
   lo = take ? nl : lo;
 }
 __device__ __forceinline__ unsigned long long wave_min_u64_solo(unsigned long long v) {
-  if (!WOS_DPP_MIN || __builtin_amdgcn_read_exec() != ~0ull) return wave_min_u64(v);
+  if (__builtin_amdgcn_read_exec() != ~0ull) return wave_min_u64(v);
   uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
   dpp_min_step<0xB1>(hi, lo);        // quad_perm [1, 0, 3, 2]
   dpp_min_step<0x4E>(hi, lo);        // quad_perm [2, 3, 0, 1]
@@ -439,7 +436,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64_solo(unsigned long lo
          (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
 }
 __device__ __forceinline__ uint32_t wave_min_u32_solo(uint32_t v) {
-  if (!WOS_DPP_MIN || __builtin_amdgcn_read_exec() != ~0ull) return wave_min_u32(v);
+  if (__builtin_amdgcn_read_exec() != ~0ull) return wave_min_u32(v);
   v = min(v, dpp_u32<0xB1>(v));
   v = min(v, dpp_u32<0x4E>(v));
   v = min(v, dpp_u32<0x141>(v));
@@ -454,11 +451,8 @@ __device__ __forceinline__ uint32_t wave_min_u32_solo(uint32_t v) {
 // (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3) -- six VALU adds instead
 // of six ds_bpermute round trips (≈ 80 cycles each).  Needs the full exec mask (as the
 // cooperative queries have); otherwise the shuffle form.
-#ifndef WOS_DPP_SCAN
-#define WOS_DPP_SCAN 1
-#endif
 __device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v, int lane) {
-  if (WOS_DPP_SCAN && __builtin_amdgcn_read_exec() == ~0ull) {
+  if (__builtin_amdgcn_read_exec() == ~0ull) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
@@ -618,9 +612,6 @@ __device__ __forceinline__ float dirichlet_dist_grid(const DevScene& sc, const f
 // per group; (fl(d*d), larger index on ties) minima by wave reductions, and the winner's
 // distance from the same cp_prim -- dirichlet_dist_culled's value (a primitive with
 // d^2 <= the bound lies in a group whose bound is <= d^2: never skipped).  Convergent.
-#ifndef WOS_DIR_SOLO
-#define WOS_DIR_SOLO 1
-#endif
 template <int DIM>
 __device__ __forceinline__ float dirichlet_dist_solo(const DevScene& sc, const float* dprim, const float* dgroup,
                                                      const float* xo, int lane) {
@@ -1096,202 +1087,11 @@ __device__ __forceinline__ bool outside_bbox(const DevScene& sc, const float* x)
   return false;
 }
 
-// float Bessel approximations (defined with the certified rejection fast path below)
-// ---- certified fast Bessel members (2D Yukawa) -------------------------------------
-// The reference stores K0, I0, K1, I1 at mu R as floats rounded from its double A&S
-// evaluation (distributions.h:581-588 -> bessel.hpp:373-555).  bessel_ik_fast evaluates the
-// same formulas with cheaper pieces -- FMA Horner, a 13-term Taylor exp after Cody-Waite
-// reduction, fdlibm's log with a Newton reciprocal instead of its division, hardware
-// reciprocal / rsqrt estimates refined by Newton steps, exp(-x) as 1/exp(x) -- accurate
-// to a few 1e-14 of the double value the reference computes (both ~20 roundings, the K
-// sums at x <= 2 conditioned <= 6).  A value is certified when v (1 - tol) and v (1 + tol)
-// round to the same float: the reference's double value lies between them and rounding
-// is monotone, so its float equals ours.  Uncertain lanes (P ~ 1e-5 per value) and
-// arguments outside [1e-6, 80] take the exact bessel_ik.  Results are bit-identical.
-#ifndef WOS_FAST_BESSEL
-#define WOS_FAST_BESSEL 0
-#endif
-#ifndef WOS_FAST_BESSEL_FB
-#define WOS_FAST_BESSEL_FB 0  // 1: also the 2D first balls' source-sample pdf and gradient norm
-#endif
-#ifndef WOS_FAST_BESSEL_PK
-#define WOS_FAST_BESSEL_PK 1  // also the direction-sampled Poisson kernel's K1, I1
-#endif
-constexpr double kFastBesselTol = 1e-13;
-constexpr float kFastBesselLo = 1e-6f, kFastBesselHi = 80.0f;
-
-// The fast path's double constants live in LDS (s_fbc, staged by stage_fast_bessel in the walk
-// kernel, the only caller): as literals each would be two s_mov_b32 into an SGPR pair at its
-// use (VOP3 takes no 64-bit literal), and the walk kernel's SGPRs are already spilled to VGPR
-// lanes -- measured: literals pushed its scratch from 0 to ~500 B per lane.
-enum {
-  FB_EXP = 0,       // 1/12!, 1/11!, ..., 1/2!, 1, 1 (13)
-  FB_LN2HI = 13, FB_LN2LO = 14, FB_INVLN2 = 15,
-  FB_LG = 16,       // Lg1..Lg7
-  FB_I0S = 23,      // I0, x < 3.75: 0.45813e-2 ... 3.5156229, 1 (7, highest first)
-  FB_I1S = 30,      // I1, x < 3.75 (7)
-  FB_I0L = 37,      // I0, x >= 3.75 (9)
-  FB_I1L = 46,      // I1, x >= 3.75: inner 4, outer 6
-  FB_K0S = 56,      // K0, x <= 2 (7)
-  FB_K1S = 63,      // K1, x <= 2 (7)
-  FB_K0L = 70,      // K0, x > 2 (7)
-  FB_K1L = 77,      // K1, x > 2 (7)
-  FB_MISC = 84,     // 1/3.75, 3.75, sqrt(2), 1 - tol, 1 + tol
-  FB_N = 89
-};
-static __shared__ double s_fbc[FB_N];
-__host__ __device__ constexpr double fb_const(int k) {
-  constexpr double t[FB_N] = {
-      2.08767569878680989792e-09, 2.50521083854417187751e-08, 2.75573192239858906526e-07,
-      2.75573192239858906526e-06, 2.48015873015873015873e-05, 1.98412698412698412698e-04,
-      1.38888888888888888889e-03, 8.33333333333333333333e-03, 4.16666666666666666667e-02,
-      1.66666666666666666667e-01, 0.5, 1.0, 1.0,
-      6.93147180369123816490e-01, 1.90821492927058770002e-10, 1.44269504088896338700e+00,
-      6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01, 2.222219843214978396e-01,
-      1.818357216161805012e-01, 1.531383769920937332e-01, 1.479819860511658591e-01,
-      0.45813e-2, 0.360768e-1, 0.2659732, 1.2067492, 3.0899424, 3.5156229, 1.0,
-      0.32411e-3, 0.301532e-2, 0.2658733e-1, 0.15084934, 0.51498869, 0.87890594, 0.5,
-      0.392377e-2, -0.1647633e-1, 0.2635537e-1, -0.2057706e-1, 0.916281e-2, -0.157565e-2, 0.225319e-2,
-      0.1328592e-1, 0.39894228,
-      -0.420059e-2, 0.1787654e-1, -0.2895312e-1, 0.2282967e-1,
-      -0.1031555e-1, 0.163801e-2, -0.362018e-2, -0.3988024e-1, 0.39894228, 0.0,
-      0.74e-5, 0.10750e-3, 0.262698e-2, 0.3488590e-1, 0.23069756, 0.42278420, -0.57721566,
-      -0.4686e-4, -0.110404e-2, -0.1919402e-1, -0.18156897, -0.67278579, 0.15443144, 1.0,
-      0.53208e-3, -0.251540e-2, 0.587872e-2, -0.1062446e-1, 0.2189568e-1, -0.7832358e-1, 1.25331414,
-      -0.68245e-3, 0.325614e-2, -0.780353e-2, 0.1504268e-1, -0.3655620e-1, 0.23498619, 1.25331414,
-      1.0 / 3.75, 3.75, 1.4142135623730951, 1.0 - kFastBesselTol, 1.0 + kFastBesselTol};
-  return t[k];
-}
-__device__ __forceinline__ void stage_fast_bessel() {
-  for (int i = threadIdx.x; i < FB_N; i += blockDim.x) s_fbc[i] = fb_const(i);
-}
-#define FBC(k) s_fbc[k]
-
-__device__ __forceinline__ double fast_rcp(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-x, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-__device__ __forceinline__ double fast_rsqrt(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  for (int i = 0; i < 2; i++) {
-    const double h = (x * y) * y;
-    y = y * __builtin_fma(-0.5, h, 1.5);
-  }
-  return y;
-}
-// Horner from LDS: c[0] x^(n-1) + ... + c[n-1]
-template <int N>
-__device__ __forceinline__ double fb_poly(double x, int base) {
-  double p = FBC(base);
-#pragma unroll
-  for (int k = 1; k < N; k++) p = __builtin_fma(p, x, FBC(base + k));
-  return p;
-}
-// e^x, |x| <= 88 (Cody-Waite reduction, 13-term Taylor: |r| <= 0.347, 2e-16)
-__device__ __forceinline__ double fast_exp(double x) {
-  const double kd = __builtin_rint(x * FBC(FB_INVLN2));
-  double r = __builtin_fma(-kd, FBC(FB_LN2HI), x);
-  r = __builtin_fma(-kd, FBC(FB_LN2LO), r);
-  return __builtin_ldexp(fb_poly<13>(r, FB_EXP), (int)kd);
-}
-// log(x), x a positive normal double: dlog's reduction and polynomial (fdlibm) with
-// f / (2 + f) by a Newton reciprocal
-__device__ __forceinline__ double fast_log(double x) {
-  const uint64_t u = double_to_bits(x);
-  int e = (int)((u >> 52) & 0x7ff) - 1023;
-  double m = bits_to_double((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
-  if (m > FBC(FB_MISC + 2)) { m = m * 0.5; e += 1; }
-  const double f = m - 1.0;
-  const double s = f * fast_rcp(2.0 + f);
-  const double z = s * s, w = z * z;
-  const double t1 = w * __builtin_fma(w, __builtin_fma(w, FBC(FB_LG + 5), FBC(FB_LG + 3)), FBC(FB_LG + 1));
-  const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, FBC(FB_LG + 6), FBC(FB_LG + 4)),
-                                                       FBC(FB_LG + 2)), FBC(FB_LG + 0));
-  const double hfsq = 0.5 * f * f, dk = (double)e;
-  return dk * FBC(FB_LN2HI) - ((hfsq - (s * (hfsq + t1 + t2) + dk * FBC(FB_LN2LO))) - f);
-}
-__device__ __forceinline__ bool fast_certain(double v) {
-  const float f = (float)v;
-  return (float)(v * FBC(FB_MISC + 3)) == f && (float)(v * FBC(FB_MISC + 4)) == f;
-}
-// N0: K0, I0; N1: K1, I1 at x in [kFastBesselLo, kFastBesselHi], rounded to float; false when a
-// value is not certified (then the exact bessel_ik).  Reads s_fbc: walk kernel only.
-template <bool N0, bool N1>
-__device__ __forceinline__ bool bessel_ik_fast(double x, float* i0, float* k0, float* i1, float* k1) {
-  double vi0 = 0.0, vi1 = 0.0, vk0 = 0.0, vk1 = 0.0;
-  double ex = 0.0, rsx = 0.0;  // e^x, 1/sqrt(x) (shared by the two large-x branches)
-  if (x > 2.0) { ex = fast_exp(x); rsx = fast_rsqrt(x); }
-  if (x < 3.75) {
-    double y = x * FBC(FB_MISC + 0);
-    y = y * y;
-    if (N0) vi0 = fb_poly<7>(y, FB_I0S);
-    if (N1) vi1 = x * fb_poly<7>(y, FB_I1S);
-  } else {
-    const double y = FBC(FB_MISC + 1) * fast_rcp(x);
-    const double e = ex * rsx;
-    if (N0) vi0 = e * fb_poly<9>(y, FB_I0L);
-    if (N1) {
-      const double a = fb_poly<4>(y, FB_I1L);
-      vi1 = e * __builtin_fma(y, __builtin_fma(y, __builtin_fma(y, __builtin_fma(y,
-                __builtin_fma(y, a, FBC(FB_I1L + 4)), FBC(FB_I1L + 5)), FBC(FB_I1L + 6)), FBC(FB_I1L + 7)),
-                FBC(FB_I1L + 8));
-    }
-  }
-  if (x <= 2.0) {
-    const double y = (x * x) * 0.25;
-    const double l = fast_log(x * 0.5);
-    if (N0) vk0 = __builtin_fma(-l, vi0, fb_poly<7>(y, FB_K0S));
-    if (N1) vk1 = __builtin_fma(l, vi1, fast_rcp(x) * fb_poly<7>(y, FB_K1S));
-  } else {
-    const double y = 2.0 * fast_rcp(x);
-    const double e = fast_rcp(ex) * rsx;
-    if (N0) vk0 = e * fb_poly<7>(y, FB_K0L);
-    if (N1) vk1 = e * fb_poly<7>(y, FB_K1L);
-  }
-  bool ok = true;
-  if (N0) { ok = ok && fast_certain(vi0) && fast_certain(vk0); *i0 = (float)vi0; *k0 = (float)vk0; }
-  if (N1) { ok = ok && fast_certain(vi1) && fast_certain(vk1); *i1 = (float)vi1; *k1 = (float)vk1; }
-  return ok;
-}
-
-// the exact evaluation (bessel_ik) rounded to float, for the lanes the fast path cannot certify:
-// out of line, so the throughput path keeps its registers
-struct F4 { float i0, k0, i1, k1; };
-#ifndef WOS_FB_EXACT_NOINLINE
-#define WOS_FB_EXACT_NOINLINE 1
-#endif
-template <bool N0, bool N1>
-#if WOS_FB_EXACT_NOINLINE
-__device__ __attribute__((noinline)) F4 bessel_ik_exact_f(double x) {
-#else
-__device__ __forceinline__ F4 bessel_ik_exact_f(double x) {
-#endif
-  double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
-  bessel_ik<N0, N1>(x, N0 ? &a : nullptr, N0 ? &b : nullptr, N1 ? &c : nullptr, N1 ? &d : nullptr);
-  return F4{(float)a, (float)b, (float)c, (float)d};
-}
-
-__device__ __forceinline__ float i0_fast(float x);
-__device__ __forceinline__ float k0_fast(float x);
-__device__ __forceinline__ float i1_fast(float x);
-__device__ __forceinline__ float k1_fast(float x);
-
 // ---------------------------------------------------------------------------
 // Green's functions on balls (distributions.h:273-832)
 // ---------------------------------------------------------------------------
-// 1: the direction-sampled Poisson kernel reuses the ball update's K1(mu R), I1(mu R)
-// when the point's distance from the centre rounds to R (bit-identical values)
-#ifndef WOS_PK_REUSE
-#define WOS_PK_REUSE 0
-#endif
-// 1: a walk step's source texel is consumed at the next step (or when the walk ends),
-// so its global load overlaps the next step's queries instead of stalling the tail
-#ifndef WOS_DEFER_TEXEL
-#define WOS_DEFER_TEXEL 1
-#endif
+// A walk step's source texel is consumed at the next step (or when the walk ends), so its
+// global load overlaps the next step's queries instead of stalling the tail (WalkState::pend)
 // ---------------------------------------------------------------------------
 // Robust float semantics (Gfn::yukawa == kYukScaled): the reference's Yukawa members
 // rewritten with exponentially scaled Bessels (bessel_scaled) and e^{2(mu r - mu R)} <= 1,
@@ -1396,8 +1196,7 @@ struct Gfn {
     A0 = m[0]; A1 = m[1]; B0 = m[2]; B1 = m[3];
   }
 
-  // fast: the certified fast Bessels (bessel_ik_fast; the caller's kernel staged s_fbc)
-  __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust, bool fast = false) {
+  __device__ __forceinline__ void update_ball(const float* cc, float RR, bool robust) {
     for (int k = 0; k < DIM; k++) { c[k] = cc[k]; yVol[k] = 0.0f; ySurf[k] = 0.0f; }
     R = RR; r = 0.0f;
     if (!yukawa) return;
@@ -1408,17 +1207,6 @@ struct Gfn {
       return;
     }
     if constexpr (DIM == 2) {
-      if (WOS_FAST_BESSEL && fast) {
-        float fi0 = 0.0f, fk0 = 0.0f, fi1 = 0.0f, fk1 = 0.0f;
-        const bool ok = muR >= kFastBesselLo && muR <= kFastBesselHi &&
-                        bessel_ik_fast<true, true>((double)muR, &fi0, &fk0, &fi1, &fk1);
-        if (!ok) {
-          const F4 e = bessel_ik_exact_f<true, true>((double)muR);
-          fi0 = e.i0; fk0 = e.k0; fi1 = e.i1; fk1 = e.k1;
-        }
-        A0 = fk0; A1 = fi0; B0 = fk1; B1 = fi1;
-        return;
-      }
       double i0, k0, i1, k1;
       bessel_ik<true, true>((double)muR, &i0, &k0, &i1, &k1);
       if (WOS_PROBE & 1) {
@@ -1477,14 +1265,6 @@ struct Gfn {
   __device__ __forceinline__ float evaluate_k0i0(double k0, double i0) const {
     const float K0mur = (float)k0, I0mur = (float)i0;
     return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
-  }
-  // the same from the float-rounded values (certified fast path: bessel_ik_fast)
-  __device__ __forceinline__ float evaluate_k0i0f(float K0mur, float I0mur) const {
-    return (float)((double)(K0mur - I0mur * A0 / A1) / kTwoPi);
-  }
-  __device__ __forceinline__ float gradient_norm_k1i1f(float K1mur, float I1mur) const {
-    const float Qr = sqrtLambda * (K1mur - I1mur * B0 / B1);
-    return (float)((double)Qr / (kTwoPi * (double)r));
   }
   __device__ __forceinline__ float gradient_norm_k1i1(double k1, double i1) const {
     const float K1mur = (float)k1, I1mur = (float)i1;
@@ -1564,7 +1344,7 @@ struct Gfn {
     }
   }
 
-  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y, bool fast = false) const {
+  __device__ __forceinline__ float dir_sampled_poisson_kernel(const float* y) const {
     if (!yukawa) return 1.0f;
     float d[DIM];
     for (int k = 0; k < DIM; k++) d[k] = y[k] - c[k];
@@ -1572,30 +1352,15 @@ struct Gfn {
     float mur = rr * sqrtLambda;
     if (scaled()) return scaled_dir_poisson_kernel<DIM>(mur, muR, A0, A1);
     if constexpr (DIM == 2) {
-      float K1mur, I1mur;
-      if (WOS_PK_REUSE && rr == R) {
-        // |y - c| rounds to R (about half the sphere points): mu r is mu R, whose K1 and I1
-        // the ball update already evaluated -- the same double values, rounded the same
-        K1mur = B0;
-        I1mur = B1;
-      } else if (WOS_FAST_BESSEL && WOS_FAST_BESSEL_PK && fast) {
-        const bool ok = mur >= kFastBesselLo && mur <= kFastBesselHi &&
-                        bessel_ik_fast<false, true>((double)mur, nullptr, nullptr, &I1mur, &K1mur);
-        if (!ok) {
-          const F4 e = bessel_ik_exact_f<false, true>((double)mur);
-          I1mur = e.i1; K1mur = e.k1;
-        }
-      } else {
-        double i1, k1;
-        bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
-        if (WOS_PROBE & 2) {
-          double p1, p2;
-          bessel_ik<false, true>(probe_opaque((double)mur), nullptr, nullptr, &p1, &p2);
-          probe_sink(p1); probe_sink(p2);
-        }
-        K1mur = (float)k1;
-        I1mur = (float)i1;
+      double i1, k1;
+      bessel_ik<false, true>((double)mur, nullptr, nullptr, &i1, &k1);
+      if (WOS_PROBE & 2) {
+        double p1, p2;
+        bessel_ik<false, true>(probe_opaque((double)mur), nullptr, nullptr, &p1, &p2);
+        probe_sink(p1); probe_sink(p2);
       }
+      const float K1mur = (float)k1;
+      const float I1mur = (float)i1;
       float Q = K1mur + I1mur * A0 / A1;
       return mur * Q;
     } else {
@@ -1740,11 +1505,7 @@ __device__ __forceinline__ float k1_fast(float x) {
 // the divisions by / of x as reciprocal products.  The reciprocals add ~1 ulp to y,
 // far inside the 8e-6 band the decisions are certified with (the GPU self-test checks
 // the <= 2e-6 error against the double-precision A&S functions).
-#ifndef WOS_FUSED_K0I0
-#define WOS_FUSED_K0I0 1
-#endif
 __device__ __forceinline__ void k0i0_fast(float x, float* k0, float* i0) {
-  if (!WOS_FUSED_K0I0) { *k0 = k0_fast(x); *i0 = i0_fast(x); return; }
   const float rs = __builtin_amdgcn_rsqf(x);
   const float rx = __builtin_amdgcn_rcpf(x);
   float iv;
@@ -1787,22 +1548,15 @@ __device__ __forceinline__ void k0i0_fast(float x, float* k0, float* i0) {
 // tabulated by bins of s with a 2 % margin (DevParams::rej_tab, wos_host_scene.h
 // rejection_bound_table) -- the subtracted term is kept, so the bound follows the
 // real peak of the threshold (tests/test_rejection_bounds.py checks both bounds).
-#ifndef WOS_QUICK_REJ
-#define WOS_QUICK_REJ 1
-#endif
 // the rejection bound table (both dimensions) in LDS: read on every sampler call,
-// one global round trip less on a walk step's critical path (WOS_REJ_TAB_LDS)
-#ifndef WOS_REJ_TAB_LDS
-#define WOS_REJ_TAB_LDS 1
-#endif
-static __shared__ float s_rej_tab[WOS_REJ_TAB_LDS ? 2 * kRejTabBins : 1];
+// one global round trip less on a walk step's critical path
+static __shared__ float s_rej_tab[2 * kRejTabBins];
 __device__ __forceinline__ float rej_tab_at(int i, const DevParams& prm) {
-  return WOS_REJ_TAB_LDS ? s_rej_tab[i] : prm.rej_tab[i];
+  return s_rej_tab[i];
 }
 
 template <int DIM>
 __device__ __forceinline__ float rej_quick_bound(const DevParams& prm, float R, float muR, float sqrtL, float invNB) {
-  if (!WOS_QUICK_REJ) return 3.0e38f;
   const float C = DIM == 2 ? 0.4670f : 0.3683f;
   float q = C * invNB / sqrtL;
   if (prm.rej_tab != nullptr && muR >= 0.0f) {
@@ -1975,7 +1729,7 @@ static __shared__ unsigned long long s_rej_jump[2 * kRejJumpLds];
 
 __device__ __forceinline__ void stage_rej_jump(const DevParams& prm) {
   for (int i = threadIdx.x; i < 2 * kRejJumpLds; i += blockDim.x) s_rej_jump[i] = prm.jump[4 * (i >> 1) + (i & 1)];
-  if (WOS_REJ_TAB_LDS && prm.rej_tab != nullptr)
+  if (prm.rej_tab != nullptr)
     for (int i = threadIdx.x; i < 2 * kRejTabBins; i += blockDim.x) s_rej_tab[i] = prm.rej_tab[i];
 }
 
@@ -1988,9 +1742,6 @@ __device__ __forceinline__ uint64_t rej_state(const DevParams& prm, uint64_t s0,
 // floor(item / B) for item < 2048, 1 <= B <= 32, with m = ceil(2^16 / B): writing
 // item = qB + r, item*m/2^16 = q + (r + item*e/2^16)/B with e = mB - 2^16 < B, and
 // item*e < 2^16, so the floor is q.  (A runtime u32 division is ~20 VALU ops per item.)
-#ifndef WOS_FASTDIV
-#define WOS_FASTDIV 1
-#endif
 // The sampler's generation has items = nact * B with B = clamp(64 / nact, kRejBmin, kRejBcap):
 // items <= 64 when B = floor(64 / nact) or B = kRejBcap (then nact < 2), else
 // items = nact * kRejBmin <= 64 * kRejBmin.  rej_div needs items <= 2048 and B <= 32.
@@ -1999,7 +1750,6 @@ static_assert(kRejBcap <= 32, "rej_div: e = m B - 2^16 < B <= 32");
 static_assert(kWave * (WOS_REJ_BMIN2 > WOS_REJ_BMIN3 ? WOS_REJ_BMIN2 : WOS_REJ_BMIN3) <= 2048 && kWave <= 2048,
               "rej_div: item * e < 2^16 needs items <= 2048");
 __device__ __forceinline__ int rej_div(int item, int B, uint32_t mB) {
-  if (!WOS_FASTDIV) return item / B;
   return (int)(((uint32_t)item * mB) >> 16);
 }
 
@@ -2065,12 +1815,6 @@ __device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, f
 // Round 2 measured the screen alone (every iteration still paid for the fast test whenever a
 // lane of its wave needed it); the own generation now screens its whole block first and runs
 // the fast test on the survivors only (tests/test_rejection_bounds.py checks the bound).
-#ifndef WOS_REJ_XB3
-#define WOS_REJ_XB3 1
-#endif
-#ifndef WOS_REJ_XB3_FB
-#define WOS_REJ_XB3_FB 0  // the first-ball kernel's own generation (4 iterations)
-#endif
 __device__ __forceinline__ bool rej_xreject3(float u, float r, float sqrtL, float invNB, float xabs) {
   const float z = r * sqrtL;
   if (!(r > 0.0f) || !(z < 80.0f)) return false;
@@ -2094,12 +1838,9 @@ __device__ __forceinline__ int rej_exact_decide3(float u, float r, float R, floa
   return u < pdfRadius / bound ? 1 : 0;
 }
 
-// 1: queries with exactly one querying lane (a lone walk in its wave) take the
+// Queries with exactly one querying lane (a lone walk in its wave) take the
 // register-only solo forms (sampler, star radius, ray): every lane works on the one
 // owner's items, owner data broadcast with readlane, results by ballot / wave reduction
-#ifndef WOS_SOLO
-#define WOS_SOLO 1
-#endif
 
 // Convergent: every lane calls it.  Inactive lanes do nothing.  2D: certified float
 // decisions by any lane, undecided ones by the owner (exact); 3D: certified float
@@ -2120,7 +1861,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
     coop = true;
   }
   const uint64_t cmask = __ballot(coop);
-  if (WOS_SOLO && cmask != 0 && (cmask & (cmask - 1)) == 0) {
+  if (cmask != 0 && (cmask & (cmask - 1)) == 0) {
     // one sampling lane (a lone walk): lane l evaluates iteration j0 + l of the owner's
     // stream with the owner's constants broadcast from registers; the decisions come
     // back as ballots and are scanned in order -- no LDS, no wave syncs
@@ -2209,7 +1950,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
       const float invNB0 = 1.0f / (nrm * bound);
       const float qb0 = rej_quick_bound<DIM>(prm, g.R, g.muR, g.sqrtLambda, invNB0);
       uint32_t acc = 0u, und = 0u;
-      if constexpr (DIM == 3 && (FB ? WOS_REJ_XB3_FB : WOS_REJ_XB3)) {
+      if constexpr (DIM == 3 && !FB) {  // (the first-ball kernel's own generation of 4: no screen)
         // phase A: every iteration of the block through the two certain-reject screens (the
         // ball's bound on u, then the radius-dependent bound); phase B: the survivors in
         // order through the fast and the exact test, the first accept wins.  The wave pays
@@ -2395,25 +2136,19 @@ struct WalkState {
   bool onNeumann;
   int walkLength;
   float totalNeumann, totalSource;
-#if WOS_DEFER_TEXEL
   // the source contribution of the last step, added once its texel has arrived:
   // totalSource += pThr * (pNrm * pTex) in the reference's order (walk_on_stars.h:270-275)
   float pThr, pNrm, pTex;
   bool pend;
-#endif
 };
 
 // Fold a deferred source contribution into totalSource (a no-op without one)
 template <int DIM>
 __device__ __forceinline__ void flush_source(WalkState<DIM>& st) {
-#if WOS_DEFER_TEXEL
   if (st.pend) {
     st.totalSource += st.pThr * (st.pNrm * st.pTex);
     st.pend = false;
   }
-#else
-  (void)st;
-#endif
 }
 
 template <int DIM>
@@ -2616,7 +2351,7 @@ __device__ __forceinline__ float walk_step_mid(const DevParams& prm, float diric
     starRadius = starQ;
     if (prm.min_star_radius <= dirichletDist) starRadius = smax(0.99f * starRadius, prm.min_star_radius);
   }
-  g.update_ball(st.pt, starRadius, prm.robust != 0, true);
+  g.update_ball(st.pt, starRadius, prm.robust != 0);
   (*steps)++;
   float u[2];
   u[0] = smp.nextf();
@@ -2668,7 +2403,6 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
                                               Pcg32& smp, Gfn<DIM, RB>& g, WalkState<DIM>& st, const float* dir,
                                               bool hit, const Hit& ip, const float* sp) {
   if (!prm.ignore_source) {
-#if WOS_DEFER_TEXEL
     flush_source<DIM>(st);
     if (g.r <= ip.d) {
       st.pNrm = g.norm();
@@ -2676,18 +2410,12 @@ __device__ __forceinline__ int walk_step_tail(const DevScene& sc, const LGeom& G
       st.pTex = source_value<DIM>(sc, sp);
       st.pend = true;
     }
-#else
-    if (g.r <= ip.d) {
-      float contrib = g.norm() * source_value<DIM>(sc, sp);
-      st.totalSource += st.throughput * contrib;
-    }
-#endif
   }
   if (!hit && outside_bbox<DIM>(sc, ip.p)) return WC_ESCAPED;
   st.prevDist = ip.d;
   for (int k = 0; k < DIM; k++) { st.prevDir[k] = dir[k]; st.pt[k] = ip.p[k]; st.n[k] = ip.n[k]; }
   st.onNeumann = hit;
-  st.throughput *= g.dir_sampled_poisson_kernel(st.pt, true);
+  st.throughput *= g.dir_sampled_poisson_kernel(st.pt);
   if (st.throughput < prm.rr_threshold) {
     float survival = st.throughput / prm.rr_threshold;
     if (survival < smp.nextf()) { st.throughput = 0.0f; return WC_RR; }
@@ -2715,7 +2443,7 @@ __device__ __forceinline__ void dirichlet_dist_step(const DevScene& sc, const LG
     return;
   }
   const uint64_t m = __ballot(want && sc.n_dprims > 0);
-  if (WOS_DIR_SOLO && m != 0 && (m & (m - 1)) == 0) {
+  if (m != 0 && (m & (m - 1)) == 0) {
     const int ol = __builtin_ctzll(m);
     float xo[DIM];
     for (int k = 0; k < DIM; k++) xo[k] = lane_bcast(x[k], ol);
@@ -2740,9 +2468,6 @@ __device__ __forceinline__ void dirichlet_dist_step(const DevScene& sc, const LG
 constexpr int kRayChunk = 16;
 // Scenes with at most this many Neumann primitives (2D segments / 3D triangles) take the per-lane
 // scan of ray_hit_wave when two or more lanes query: every lane tests every primitive
-#ifndef WOS_RAY_SCAN
-#define WOS_RAY_SCAN 1
-#endif
 #ifndef WOS_RAY_SCAN_MAX2
 #define WOS_RAY_SCAN_MAX2 24
 #endif
@@ -2815,7 +2540,7 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
   for (int k = 0; k < DIM; k++) inv[k] = __builtin_amdgcn_rcpf(dir[k]);
   const bool tree = TREE && sc.ptree.levels > 0;
   const uint64_t nmask = __ballot(need);
-  if (WOS_RAY_SCAN && !tree && np <= (DIM == 2 ? kRayScanMax2 : kRayScanMax3) && (nmask & (nmask - 1)) != 0) {
+  if (!tree && np <= (DIM == 2 ? kRayScanMax2 : kRayScanMax3) && (nmask & (nmask - 1)) != 0) {
     // a handful of primitives (config C's box: 4 segments, the cube: 12 triangles): each querying
     // lane tests every primitive against its own ray with the same pre-filter + exact test as the
     // cooperative items (each against tmax) and keeps the minimum (d bits, ~index) -- no
@@ -2849,7 +2574,7 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
     }
     return found;
   }
-  if (WOS_SOLO && !tree && (nmask & (nmask - 1)) == 0) {
+  if (!tree && (nmask & (nmask - 1)) == 0) {
     // one querying lane: lane l tests group g0 + l against the owner's ray, then the
     // primitives of the accepted groups, kGroup lanes per group; the minimum key by a
     // wave reduction instead of LDS atomics
@@ -2976,11 +2701,8 @@ __device__ __forceinline__ bool ray_hit_wave(const LGeom& G, const DevScene& sc,
 // union of every lane's groups) become ~(total work)/64 wave iterations.
 // ---------------------------------------------------------------------------
 constexpr int kStarChunk = 16;  // groups per compaction round: at most 64 * 16 list entries
-// 1: the star query's cell lists are copied to the wave list 16 entries per LDS round
-// trip (dword reads + alignbyte) instead of one byte read per entry
-#ifndef WOS_STAR_BATCH
-#define WOS_STAR_BATCH 1
-#endif
+// The star query's cell lists are copied to the wave list 16 entries per LDS round trip
+// (dword reads + alignbyte) instead of one byte read per entry
 
 template <int DIM>
 struct StarLDS {
@@ -3103,7 +2825,7 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
   }
   const uint64_t nmask = __ballot(need);
   if (nmask == 0) return result;
-  if (WOS_SOLO && (nmask & (nmask - 1)) == 0 &&
+  if ((nmask & (nmask - 1)) == 0 &&
       __builtin_amdgcn_readlane((int)use_cell, __builtin_ctzll(nmask)) != 0) {
     // one querying lane inside the cell grid: lane l judges entry l of the owner's cell
     // list (64 at a time) against the owner's query; (d^2, ~index) minimum and the
@@ -3161,7 +2883,6 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
     DIAG_T0(t_s2);
     constexpr uint32_t kWin = kWave * kStarChunk;
     for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
-#if WOS_STAR_BATCH
       // this lane's entries inside the window, 16 at a time: the list bytes of a batch
       // come from five dword reads issued together (one LDS round trip per batch
       // instead of one per entry), realigned with alignbyte; reads are clamped to the
@@ -3185,13 +2906,6 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
             if (i + (uint32_t)j < hi0) L->list[first + i + (uint32_t)j - w0] = tag | ((al[j >> 2] >> (8 * (j & 3))) & 0xFFu);
         }
       }
-#else
-      const uint8_t* lst = reinterpret_cast<const uint8_t*>(G.sgrid + G.sgrid_off_words);
-      for (uint32_t i = 0; i < cnt; i++) {
-        const uint32_t q = first + i;
-        if (q >= w0 && q < w0 + kWin) L->list[q - w0] = ((uint32_t)lane << 26) | (uint32_t)lst[c_beg + i];
-      }
-#endif
       wave_sync();
       DIAG_ADD_IF(D_L_S_BUILD, t_s2, lone);
       const uint32_t items = (total - w0) < kWin ? (total - w0) : kWin;
@@ -3394,12 +3108,9 @@ __host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
 // samples are built in turn into its own LDS slot; seeds stay keyed by the global
 // point index, so results do not depend on the packing.  The cap bounds the
 // sequential stratified-sample builds per wave for tiny n_pairs.
-#ifndef WOS_FB_PACK
-#define WOS_FB_PACK 1
-#endif
 constexpr int kFbMaxPack = 4;
 __host__ __device__ constexpr int fb_points_per_wave(int n_pairs) {
-  return (WOS_FB_PACK && n_pairs > 0 && 2 * n_pairs <= kWave)
+  return (n_pairs > 0 && 2 * n_pairs <= kWave)
              ? (kWave / n_pairs < kFbMaxPack ? kWave / n_pairs : kFbMaxPack)
              : 1;
 }
@@ -3530,15 +3241,12 @@ __device__ __forceinline__ void lhs_permute_all(float* wbase, int lhs_floats, in
   else lhs_permute_all_r<DIM - 1, 4>(wbase, lhs_floats, P, nstrat, scratch, lane);
 }
 
-// 1: a wave's stratified samples (every point slot, every dimension) are shuffled in one
+// A wave's stratified samples (every point slot, every dimension) are shuffled in one
 // lhs_permute_all pass when they fit its registers, instead of one lhs_permute per slot and dimension
-#ifndef WOS_LHS_ALL
-#define WOS_LHS_ALL 1
-#endif
 __host__ __device__ constexpr bool lhs_all_fits(int n_pairs, int dim, int P) {
   // 3D only: a 2D wave with one point has one shuffle, and the out-of-line pass costs the 2D
   // first-ball kernel spills
-  return WOS_LHS_ALL && dim == 3 &&
+  return dim == 3 &&
          P * (dim - 1) * ((2 * n_pairs + kWave - 1) / kWave == 3 ? 4 : (2 * n_pairs + kWave - 1) / kWave) <= 4;
 }
 
@@ -3605,9 +3313,6 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
 // 2D first balls: K0, I0, K1, I1 at the sampled radius from one fused Bessel evaluation
 // (pdf and gradient norm), and the second member reuses the first's gradient norm when its
 // radius is the same float -- identical values, fewer double-precision exp / sqrt / divisions
-#ifndef WOS_FB_FUSED_BESSEL
-#define WOS_FB_FUSED_BESSEL 1
-#endif
 template <int DIM, bool RB>
 __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams& prm, const DevTasks& tk,
                                             const float* x, float firstR, const float* strat, int64_t gidx,
@@ -3652,7 +3357,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
         sample_unit_sphere<DIM>(&strat[sd * (2 * w + 0)], dir);
         if constexpr (DIM == 3) {
           sample_volume_wave<DIM, RB, true>(prm, active, g, dir, fs, &sourcePdf, sourcePt, iters, true, rejL, lane);
-        } else if (WOS_FB_FUSED_BESSEL && g.yukawa == 1) {
+        } else if (g.yukawa == 1) {
           // the pdf (K0, I0 at the sampled mu r, before the clamps) and the gradient norm
           // (K1, I1 at the clamped mu r) from one fused evaluation when the clamps kept r
           float rpre;
@@ -3672,19 +3377,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
           }
 #endif
           const float nrm = g.norm();
-          if (rpre == g.r && WOS_FAST_BESSEL && WOS_FAST_BESSEL_FB) {
-            // certified fast Bessels (s_fbc staged by the first-ball kernel), exact fallback
-            const double xr = (double)(g.r * g.sqrtLambda);
-            float fi0 = 0.0f, fk0 = 0.0f, fi1 = 0.0f, fk1 = 0.0f;
-            const bool ok = xr >= kFastBesselLo && xr <= kFastBesselHi &&
-                            bessel_ik_fast<true, true>(xr, &fi0, &fk0, &fi1, &fk1);
-            if (!ok) {
-              const F4 e = bessel_ik_exact_f<true, true>(xr);
-              fi0 = e.i0; fk0 = e.k0; fi1 = e.i1; fk1 = e.k1;
-            }
-            sourcePdf = g.evaluate_k0i0f(fk0, fi0) / nrm;
-            gn_a = g.gradient_norm_k1i1f(fk1, fi1);
-          } else if (rpre == g.r) {
+          if (rpre == g.r) {
             double i0, k0, i1, k1;
             bessel_ik<true, true>((double)(g.r * g.sqrtLambda), &i0, &k0, &i1, &k1);
             sourcePdf = g.evaluate_k0i0(k0, i0) / nrm;
@@ -3712,7 +3405,7 @@ __device__ __forceinline__ void first_balls(const DevScene& sc, const DevParams&
       totalSource += throughput * contrib;
       firstSource = contrib;
       float gr[DIM];
-      if (WOS_FB_FUSED_BESSEL && DIM == 2 && g.yukawa == 1 && g.r == r_a) {
+      if (DIM == 2 && g.yukawa == 1 && g.r == r_a) {
         // gradient() with the norm of member a's identical radius (same value)
         for (int k = 0; k < DIM; k++) gr[k] = (g.yVol[k] - g.c[k]) * gn_a;
       } else {
@@ -3858,9 +3551,6 @@ __device__ __forceinline__ LGeom stage_geometry(const DevScene& sc, float* smem,
 // walk kernel's loop-invariant scene / parameter / task fields and the constants
 // hoisted next to them otherwise overflow the SGPR file, whose spills into VGPR
 // lanes then push the VGPRs into scratch.
-#ifndef WOS_KVIEW
-#define WOS_KVIEW 1
-#endif
 // The walk kernel's parameters as they lie in the kernarg segment (the ABI lays the
 // arguments out like the members of this struct: declaration order, natural alignment).
 struct WalkKernArgs {
@@ -3871,7 +3561,7 @@ struct WalkKernArgs {
 using KernArgsPtr = const __attribute__((address_space(4))) WalkKernArgs*;
 __device__ __forceinline__ KernArgsPtr kernargs_opaque() {
   KernArgsPtr q = (KernArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
-  if (WOS_KVIEW) asm volatile("" : "+s"(q));
+  asm volatile("" : "+s"(q));
   return q;
 }
 
@@ -4020,7 +3710,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   stage_rej_jump(prm);
-  if (WOS_FAST_BESSEL && WOS_FAST_BESSEL_FB && DIM == 2) stage_fast_bessel();
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -4179,9 +3868,7 @@ __device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& 
   st.walkLength = 0;
   st.totalNeumann = 0.0f;
   st.totalSource = v_tsrc;
-#if WOS_DEFER_TEXEL
   st.pend = false;
-#endif
   ddist = v_dd;
   g.init(yuk0, sc.absorption);
   if constexpr (BSTART) {
@@ -4205,10 +3892,16 @@ __device__ __forceinline__ void walk_start(const DevScene& sc, const DevParams& 
 // termination code (>= 0) or -1 while the walk continues.
 template <int DIM, bool GG, bool BSTART, bool RB, bool NEU = true>
 __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParams& prm, const LGeom& G, bool active,
-                                              WalkState<DIM>& st, Gfn<DIM, RB>& g, Pcg32& ws, float& ddist,
+                                              WalkState<DIM>& st, Gfn<DIM, RB>& gc, Pcg32& ws, float& ddist,
                                               uint32_t& wsteps, float& firstR, StarLDS<DIM>* starL,
                                               RayLDS<DIM>* rayL, RejLDS* rejL, uint32_t* c_iters, int lane) {
   DIAG_T0(t_step);
+  // This step's ball: only the Green's function's kind carries over from step to step (its
+  // absorption is the scene's -- every Gfn::init takes sc.absorption -- and update_ball rebuilds
+  // the ball before any use), so the ball's members are locals of the iteration instead of
+  // loop-carried registers of the persistent loop (3D walk kernel scratch 108 -> 40 B/lane)
+  Gfn<DIM, RB> g;
+  g.yukawa = gc.yukawa; g.lambda = sc.absorption; g.sqrtLambda = __builtin_sqrtf(sc.absorption);
   int code = -1;
   DIAG_LONE(lone, active);
   bool flip = false, query = false;
@@ -4261,6 +3954,7 @@ __device__ __forceinline__ int walk_iteration(const DevScene& sc, const DevParam
   if (BSTART) firstR = 0.0f;  // firstStep = false (walk_on_stars.h:325)
   DIAG_ADD_LONE(D_TAIL, D_L_TAIL, t_tail, lone);
   DIAG_ADD_LONE(D_STEP, D_L_STEP, t_step, lone);
+  if (live) gc.yukawa = g.yukawa;
   return code;
 }
 
@@ -4327,61 +4021,47 @@ static_assert((kTaskQueues & (kTaskQueues - 1)) == 0 && kTaskQueues <= (unsigned
 // The kernels with SPR = true hand over (2D, LDS geometry; chosen per solve,
 // DevParams::tail_spread); 3D keeps SPR = false (its extra live state costs the throughput
 // path scratch that its short tails do not return).  Only the loop-carried state moves.
-// WOS_TAIL_SPREAD=2 (A/B builds only) turns it on in every instantiation.
-#ifndef WOS_TAIL_SPREAD
-#define WOS_TAIL_SPREAD 0
-#endif
 constexpr int kSpreadMax = 32;  // walks per hand-over
-// words of one walk's state between two steps: WalkState, the Green's function's kind and
-// absorption (its ball -- c, R, r, y*, muR and the Bessel members -- is rebuilt by update_ball
-// before any use in the next step, so it is not loop-carried and not moved), the PCG32 state,
-// ddist, wsteps, task
+// words of one walk's state between two steps: WalkState, the Green's function's kind (its
+// absorption is the scene's, and its ball -- c, R, r, y*, muR and the Bessel members -- is rebuilt
+// by update_ball before any use in the next step: walk_iteration), the PCG32 state, ddist,
+// wsteps, task
 template <int DIM>
-constexpr int walk_pack_words() { return (3 * DIM + 6 + (WOS_DEFER_TEXEL ? 4 : 0)) + 3 + 2 + 3; }
+constexpr int walk_pack_words() { return (3 * DIM + 6 + 4) + 1 + 2 + 3; }
 // every member is moved (the struct sizes, bools padded to a word, match the counts)
-static_assert(sizeof(WalkState<2>) == 4 * (3 * 2 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<2> members");
-static_assert(sizeof(WalkState<3>) == 4 * (3 * 3 + 6 + (WOS_DEFER_TEXEL ? 4 : 0)), "WalkState<3> members");
+static_assert(sizeof(WalkState<2>) == 4 * (3 * 2 + 6 + 4), "WalkState<2> members");
+static_assert(sizeof(WalkState<3>) == 4 * (3 * 3 + 6 + 4), "WalkState<3> members");
 static_assert(sizeof(Gfn<2, false>) == 4 * (1 + 3 * 2 + 9) && sizeof(Gfn<3, true>) == 4 * (1 + 3 * 3 + 9), "Gfn members");
 static_assert(sizeof(Pcg32) == 8, "Pcg32 state");
-// one walk's state into / out of mailbox slot `slot` (word-major, kSpreadMax slots per word);
-// AT: a global mailbox of another wave, through device-scope (sc1) stores and loads
-template <int DIM, bool RB, bool AT = false>
+// one walk's state into / out of mailbox slot `slot` (word-major, kSpreadMax slots per word)
+template <int DIM, bool RB>
 __device__ __forceinline__ void spread_put(uint32_t* mb, int slot, const WalkState<DIM>& st, const Gfn<DIM, RB>& g,
                                            const Pcg32& ws, float ddist, float firstR, uint32_t wsteps, uint32_t t) {
   int q = 0;
   auto put = [&](uint32_t v) {
-    uint32_t* a = mb + (q++) * kSpreadMax + slot;
-    if (AT) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *a = v;
+    mb[(q++) * kSpreadMax + slot] = v;
   };
   auto putf = [&](float v) { put(__float_as_uint(v)); };
   for (int k = 0; k < DIM; k++) { putf(st.pt[k]); putf(st.n[k]); putf(st.prevDir[k]); }
   putf(st.prevDist); putf(st.throughput); put(st.onNeumann ? 1u : 0u); put((uint32_t)st.walkLength);
   putf(st.totalNeumann); putf(st.totalSource);
-#if WOS_DEFER_TEXEL
   putf(st.pThr); putf(st.pNrm); putf(st.pTex); put(st.pend ? 1u : 0u);
-#endif
-  put((uint32_t)g.yukawa); putf(g.lambda); putf(g.sqrtLambda);
+  put((uint32_t)g.yukawa);
   put((uint32_t)ws.state); put((uint32_t)(ws.state >> 32));
   (void)firstR;  // 0 after every step (a boundary-start walk's first-sphere radius is used once)
   putf(ddist); put(wsteps); put(t);
 }
-template <int DIM, bool RB, bool AT = false>
+template <int DIM, bool RB>
 __device__ __forceinline__ void spread_get(const uint32_t* mb, int slot, WalkState<DIM>& st, Gfn<DIM, RB>& g,
                                            Pcg32& ws, float& ddist, float& firstR, uint32_t& wsteps, int64_t& t) {
   int q = 0;
-  auto get = [&]() {
-    const uint32_t* a = mb + (q++) * kSpreadMax + slot;
-    return AT ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *a;
-  };
+  auto get = [&]() { return mb[(q++) * kSpreadMax + slot]; };
   auto getf = [&]() { return __uint_as_float(get()); };
   for (int k = 0; k < DIM; k++) { st.pt[k] = getf(); st.n[k] = getf(); st.prevDir[k] = getf(); }
   st.prevDist = getf(); st.throughput = getf(); st.onNeumann = get() != 0u; st.walkLength = (int)get();
   st.totalNeumann = getf(); st.totalSource = getf();
-#if WOS_DEFER_TEXEL
   st.pThr = getf(); st.pNrm = getf(); st.pTex = getf(); st.pend = get() != 0u;
-#endif
-  g.yukawa = (int)get(); g.lambda = getf(); g.sqrtLambda = getf();
+  g.yukawa = (int)get();
   const uint32_t lo = get(), hi = get();
   ws.state = ((uint64_t)hi << 32) | lo;
   ddist = getf(); firstR = 0.0f; wsteps = get(); t = (int64_t)get();
@@ -4390,63 +4070,6 @@ struct SpreadLDS {
   uint32_t busy, idle;
   uint32_t mbox[kBlock / kWave];
 };
-
-// ---- tail spreading across the grid (DevParams::gspread) ------------------------
-// The same hand-over between any two waves of the grid, pulled by the idle waves: an idle
-// wave probes other waves' request words (a sibling of its workgroup and a random wave of
-// the grid per poll, backing off while it finds none); a wave holding >= 2 walks once the
-// queue is dry keeps its request word open (1); a prober takes it with a compare-and-swap
-// (1 -> 2 + its index) and waits on its own response word; the holder sees the request at
-// the end of its step (the word is read during the step), hands over the upper half of its
-// walks (into the prober's LDS scratch when it is a sibling, else into its global mailbox),
-// then writes the response kGsFull | n (n may be 0 when its walks have ended meanwhile) and
-// reopens or closes its word.  A wave answers any request before it goes idle, so no prober
-// waits for nobody.
-// Termination: g_idle counts idle waves; a holder that gives walks takes their new owner
-// out of g_idle before the response is visible and stays busy itself, so g_idle reaches W
-// only when no walk is left anywhere: the wave whose announcement makes it W raises the done
-// flag (kGsDoneN replicas on separate lines) and every idle wave leaves when it sees it, or
-// after kGsMaxPolls polls (a grid whose waves are not all resident at once still drains; a
-// prober that is not waiting for a response holds nothing).
-// Only relaxed device-scope atomics (sc1 loads / stores, no cache write-back or invalidate
-// fences), ordered by waiting for the wave's outstanding memory operations (s_waitcnt).
-// Control words (zeroed per launch, gs_ctrl_words): [0] g_idle, done replica i at
-// kGsDone0 + 32 i, busy waves per SIMD from kGsSimd0, then per wave w [kGsRec0 + 4 w] response,
-// [+1] request.
-constexpr uint32_t kGsOpen = 1u, kGsFull = 0x100u, kGsLds = 0x200u;
-constexpr int kGsDone0 = 32, kGsDoneN = 64, kGsSimd0 = kGsDone0 + 32 * kGsDoneN;
-constexpr int kGsSimdSlots = 8 * 8 * 2 * 16 * 4;
-constexpr int kGsRec0 = kGsSimd0 + kGsSimdSlots;
-constexpr int kGsMaxPolls = 1 << 15;
-static_assert(kGsRec0 == kGsRecHost, "control layout (wos_scene.h gs_ctrl_words)");
-static_assert(kGsMailWords >= kSpreadMax * 32 && walk_pack_words<2>() <= 32 && walk_pack_words<3>() <= 32,
-              "global mailbox holds kSpreadMax walks");
-__device__ __forceinline__ uint32_t gs_ld(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gs_st(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool gs_cas(uint32_t* p, uint32_t expect, uint32_t v) {
-  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-}
-// every memory operation of the wave issued so far has completed (stores acknowledged)
-__device__ __forceinline__ void gs_wait_all() { __builtin_amdgcn_s_waitcnt(0); }
-// Probers only where the SIMD has at most WOS_GS_SIMD_MAX busy waves (-1: everywhere): a walk
-// handed to a wave whose SIMD is busy with other walks runs no faster, and the hand-over splits
-// one wave's cooperative queries into two.  Busy waves per SIMD are counted in
-// [kGsSimd0, kGsSimd0 + kGsSimdSlots), indexed by the wave's hardware slot (XCC, SE, SH, CU,
-// SIMD from HW_ID / XCC_ID; a heuristic: a wrong index costs speed, never correctness).
-#ifndef WOS_GS_SIMD_MAX
-#define WOS_GS_SIMD_MAX 1
-#endif
-__device__ __forceinline__ int gs_simd_slot() {
-  const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
-  const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID [3:0]
-  const uint32_t simd = (hw >> 4) & 3u, cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
-  return (int)(((((xcc & 7u) * 8u + se) * 2u + sh) * 16u + cu) * 4u + simd) & (kGsSimdSlots - 1);
-}
 
 #ifndef WOS_WALK_WAVES_PER_EU
 #define WOS_WALK_WAVES_PER_EU 4
@@ -4468,11 +4091,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   const DevParams& prm = prm_arg;
   const DevTasks& tk = tk_arg;
   static_assert(walk_pack_words<DIM>() * kSpreadMax * 4 <= (int)walk_scratch_bytes<DIM>(), "mailbox fits the scratch");
-  constexpr bool kSpread = SPR || WOS_TAIL_SPREAD == 2;
+  constexpr bool kSpread = SPR;
   const int lane = threadIdx.x & (kWave - 1);
   stage_geometry<DIM, GG>(sc, smem, true);
   stage_rej_jump(prm);
-  if (WOS_FAST_BESSEL && DIM == 2) stage_fast_bessel();
   // per-wave scratch shared by the star and ray queries (used one after the other)
   const int wave_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // wave-uniform: SGPR address
   char* wscratch = reinterpret_cast<char*>(smem + geom_floats) + wave_u * walk_scratch_bytes<DIM>();
@@ -4482,15 +4104,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   if (threadIdx.x < C_NUM) s_ctr[threadIdx.x] = 0u;
   if (threadIdx.x == 0) { s_spread.busy = blockDim.x / kWave; s_spread.idle = 0u; }
   if (threadIdx.x < kBlock / kWave) s_spread.mbox[threadIdx.x] = 0u;
-  // grid-wide spreading (DevParams::gspread): its pointers are re-read from the kernel arguments
-  // where used (the per-iteration view), so that nothing of it is live across a step
-#define WOS_GS_VIEW()                                                                                    \
-  const int gW = (int)gridDim.x * (kBlock / kWave);                                                      \
-  uint32_t* const gs = (WOS_GRID_SPREAD && kSpread && prm.gspread != nullptr && prm.gspread_waves == gW) ? prm.gspread \
-                                                                                                        : nullptr; \
-  uint32_t* const gmail = prm.gspread_mail;                                                              \
-  const int gw = (int)blockIdx.x * (kBlock / kWave) + wave_u;                                            \
-  (void)gmail;
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
@@ -4597,9 +4210,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   float ddist = 0.0f;
   uint32_t wsteps = 0;
   float firstR = 0.0f;  // BSTART: first sphere radius of the lane's walk, 0 after its first step
-  bool gopen = false;   // grid-wide spreading: this wave's request word is open (wave-uniform)
-  if (WOS_GRID_SPREAD && WOS_GS_SIMD_MAX >= 0 && kSpread && prm_arg.gspread != nullptr && lane == 0)  // busy on its SIMD
-    __hip_atomic_fetch_add(prm_arg.gspread + kGsSimd0 + gs_simd_slot(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   for (;;) {
     DIAG_T0(t_loop);
@@ -4608,9 +4218,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
 #endif
     // per-iteration views of the kernel parameters and of the staged geometry (see kview)
     KernArgsPtr ka = kernargs_opaque();
-    const DevScene& sc = WOS_KVIEW ? (const DevScene&)ka->sc : sc_arg;
-    const DevParams& prm = WOS_KVIEW ? (const DevParams&)ka->prm : prm_arg;
-    const DevTasks& tk = WOS_KVIEW ? (const DevTasks&)ka->tk : tk_arg;
+    const DevScene& sc = (const DevScene&)ka->sc;
+    const DevParams& prm = (const DevParams&)ka->prm;
+    const DevTasks& tk = (const DevTasks&)ka->tk;
     const LGeom G = geometry_view<DIM, GG>(sc, smem, true, false);
     // ---- hand staged tasks to idle lanes (uniform control flow)
     {
@@ -4657,76 +4267,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     if (__ballot(t >= 0) == 0) {
       if (S == 0 && exhausted) {  // queue drained and every lane idle
         if (!kSpread) break;
-        WOS_GS_VIEW();
-        if (gs != nullptr) {
-          uint32_t* const myreq = gs + kGsRec0 + 4 * gw + 1;
-          uint32_t* const myresp = gs + kGsRec0 + 4 * gw;
-          // close the request word; a request that came meanwhile is answered with nothing
-          if (gopen) {
-            if (lane == 0 && !gs_cas(myreq, kGsOpen, 0u)) {
-              const uint32_t rq = gs_ld(myreq);
-              gs_st(gs + kGsRec0 + 4 * ((int)rq - 2), kGsFull);
-              gs_st(myreq, 0u);
-            }
-            gopen = false;
-          }
-          // announce; the wave whose announcement makes every wave idle raises the done flag
-          uint32_t old = 0u;
-          uint32_t* const mysimd = gs + kGsSimd0 + gs_simd_slot();
-          if (lane == 0) {
-            if (WOS_GS_SIMD_MAX >= 0) __hip_atomic_fetch_sub(mysimd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            old = __hip_atomic_fetch_add(gs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          if (__builtin_amdgcn_readfirstlane((int)old) == gW - 1) {
-            static_assert(kGsDoneN == kWave, "one done replica per lane");
-            gs_st(gs + kGsDone0 + 32 * lane, 1u);
-            break;
-          }
-          int nsl = 1, got = 0;
-          uint32_t rsp = 0u;
-          for (int polls = 0; polls < kGsMaxPolls && !got; polls++) {
-            // probe two request words: lane 0 a sibling's, lane 1 a random wave's
-            const uint32_t h = (uint32_t)gw * 0x9E3779B1u ^ (uint32_t)polls * 0x85EBCA77u;
-            const int vic = lane == 0 ? (gw & ~3) | ((wave_u + 1 + polls) & 3) : (int)((h ^ (h >> 15)) % (uint32_t)gW);
-            const uint32_t x = lane < 2 ? gs_ld(gs + kGsRec0 + 4 * vic + 1) : 0u;
-            const uint32_t dn = lane == 0 ? gs_ld(gs + kGsDone0 + 32 * (gw & (kGsDoneN - 1))) : 0u;
-            const uint32_t sb = (WOS_GS_SIMD_MAX >= 0 && lane == 0) ? gs_ld(mysimd) : 0u;
-            if (__builtin_amdgcn_readfirstlane((int)dn) != 0) break;
-            // (a SIMD busy with other waves: no probe this round)
-            const bool quiet = WOS_GS_SIMD_MAX < 0 || __builtin_amdgcn_readfirstlane((int)sb) <= WOS_GS_SIMD_MAX;
-            const uint64_t open = __ballot(quiet && lane < 2 && x == kGsOpen && vic != gw);
-            if (open != 0) {
-              const int src = __builtin_ctzll(open);
-              int ok = 0;
-              if (lane == src) ok = gs_cas(gs + kGsRec0 + 4 * vic + 1, kGsOpen, 2u + (uint32_t)gw);
-              if (__builtin_amdgcn_readlane(ok, src)) {
-                // the holder answers at the end of its step, or before it goes idle
-                for (;;) {
-                  rsp = (uint32_t)__builtin_amdgcn_readfirstlane((int)gs_ld(myresp));
-                  if (rsp != 0u) break;
-                  __builtin_amdgcn_s_sleep(4);
-                }
-                if (lane == 0) gs_st(myresp, 0u);
-                got = (rsp & 0xFFu) != 0u;
-              }
-              nsl = 1;
-            } else if (nsl < 128) {
-              nsl *= 2;
-            }
-            if (!got)
-              for (int z = 0; z < nsl; z++) __builtin_amdgcn_s_sleep(2);
-          }
-          if (!got) break;  // done, or the poll budget spent: this wave holds and awaits nothing
-          if (WOS_GS_SIMD_MAX >= 0 && lane == 0)
-            __hip_atomic_fetch_add(mysimd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t n = rsp & 0xFFu;
-          if ((uint32_t)lane < n && (rsp & kGsLds))
-            spread_get<DIM, RB>(reinterpret_cast<const uint32_t*>(wscratch), lane, st, g, ws, ddist, firstR, wsteps, t);
-          else if ((uint32_t)lane < n)
-            spread_get<DIM, RB, true>(gmail + (size_t)gw * kGsMailWords, lane, st, g, ws, ddist, firstR, wsteps, t);
-          wave_sync();
-          continue;
-        }
         // idle: announce, then take a sibling's hand-over or leave once no wave holds walks
         if (lane == 0) {
           __hip_atomic_fetch_or(&s_spread.idle, 1u << wave_u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4759,9 +4299,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     const bool lone_it = __popcll(__ballot(t >= 0)) <= 2;
     if (lone_it) DIAG_COUNT(D_L_ITERS, 1);
 #endif
-    // grid-wide spreading: this wave's request word, read during the step
-    uint32_t greq = 0u;
-    if (WOS_GRID_SPREAD && gopen && lane == 0) greq = gs_ld(prm.gspread + kGsRec0 + 4 * ((int)blockIdx.x * (kBlock / kWave) + wave_u) + 1);
     const int code = walk_iteration<DIM, GG, BSTART, RB, NEU>(sc, prm, G, t >= 0, st, g, ws, ddist, wsteps, firstR, starL,
                                                          rayL, rejL, &c_iters, lane);
 #if WOS_TIMELINE
@@ -4781,53 +4318,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
       walk_finish<DIM>(sc, prm, tk, t, code, st, wsteps, s_ctr);
       t = -1;
     }
-    WOS_GS_VIEW();
-    if (kSpread && exhausted && S == 0 && gs != nullptr) {
-      const uint64_t live = __ballot(t >= 0);
-      const int k = __popcll(live);
-      uint32_t* const myreq = gs + kGsRec0 + 4 * gw + 1;
-      if (gopen) {
-        const uint32_t rq = (uint32_t)__builtin_amdgcn_readfirstlane((int)greq);
-        if (rq >= 2u) {
-          // a prober's request: the upper half of the live walks (by lane rank, at most
-          // kSpreadMax; none when fewer than 2 are left)
-          const int r = (int)rq - 2;
-          const int kd = k >= 2 ? ((k / 2) < kSpreadMax ? (k / 2) : kSpreadMax) : 0;
-          const bool sib = (r & ~3) == (gw & ~3);
-          static_assert(kBlock / kWave == 4, "siblings: the waves 4 w .. 4 w + 3");
-          if (kd > 0) {
-            // the prober leaves g_idle before the answer is visible (this wave stays busy meanwhile)
-            if (lane == 0) __hip_atomic_fetch_sub(gs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-            const bool give = t >= 0 && rank >= k - kd;
-            if (give && sib)
-              spread_put<DIM, RB>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem + geom_floats) +
-                                                              (r & 3) * walk_scratch_bytes<DIM>()),
-                                  rank - (k - kd), st, g, ws, ddist, firstR, wsteps, (uint32_t)t);
-            else if (give)
-              spread_put<DIM, RB, true>(gmail + (size_t)r * kGsMailWords, rank - (k - kd), st, g, ws, ddist, firstR,
-                                        wsteps, (uint32_t)t);
-            if (give) t = -1;
-          }
-          gs_wait_all();
-          wave_sync();
-          if (lane == 0) {
-            gs_st(gs + kGsRec0 + 4 * r, kGsFull | (sib ? kGsLds : 0u) | (uint32_t)kd);
-            gs_st(myreq, k - kd >= 2 ? kGsOpen : 0u);  // a taken word is written by its holder alone
-          }
-          gopen = k - kd >= 2;
-        } else if (k < 2) {
-          int ok = 0;
-          if (lane == 0) ok = gs_cas(myreq, kGsOpen, 0u);
-          // (failed: a request came meanwhile -- answered after the next step, or on going idle)
-          if (__builtin_amdgcn_readfirstlane(ok)) gopen = false;
-        }
-      } else if (k >= 2) {
-        if (lane == 0) gs_st(myreq, kGsOpen);
-        gopen = true;
-      }
-    } else if (kSpread && exhausted && S == 0) {
+    if (kSpread && exhausted && S == 0) {
       const uint64_t live = __ballot(t >= 0);
       const int k = __popcll(live);
       if (k >= 2 && __builtin_amdgcn_readfirstlane(
@@ -4879,7 +4370,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     }
 #endif
   }
-#undef WOS_GS_VIEW
   DIAG_MAX(D_WAVEMAX, __builtin_amdgcn_s_memtime() - t_wave);
   flush_counter(counters, C_ITERS, c_iters, lane);
   __syncthreads();
@@ -5031,9 +4521,6 @@ __global__ __launch_bounds__(kFoldPoints) void wos_fold_kernel(const DevParams p
 // IEEE divisions per point (round 4, DESIGN).  Not for the derivative output (BVC's Dirichlet
 // samples, DevTasks::deriv): wos_fold_kernel keeps that.  Both dimensions since its staging is
 // software-pipelined (before that, 2D's five-float records folded faster one thread per point).
-#ifndef WOS_FOLD4
-#define WOS_FOLD4 1
-#endif
 constexpr int kFold4Points = 64;  // points per 256-thread block
 template <int DIM>
 __global__ __launch_bounds__(4 * kFold4Points) void wos_fold4_kernel(const DevParams prm, const DevTasks tk, int64_t n,

@@ -198,7 +198,7 @@ hipError_t launch_walks(int dim, const DevScene& sc, const DevParams& prm, const
 hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_t n, float* p, float* g,
                        int32_t* nest, int32_t* steps, hipStream_t s) {
   // the quad fold (pipelined staging), both dimensions: profiles/r5zm_ab_fold_pipe.log, r5zn_ab_fold4_2d.log
-  if (WOS_FOLD4 && tk.deriv == nullptr) {
+  if (tk.deriv == nullptr) {
     const int g4 = (int)((n + kFold4Points - 1) / kFold4Points);
     if (g4 < 1) return hipSuccess;
     if (dim == 3)

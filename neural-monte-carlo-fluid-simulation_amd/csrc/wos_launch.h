@@ -11,10 +11,7 @@ constexpr int kNumCounters = 9;
 // task queues from slot kNumCounters + 8 on, one per 64-byte line (wos_walk_kernel)
 constexpr int kTaskQueueSlot0 = kNumCounters + 8;
 constexpr int kNumCounterSlots = kTaskQueueSlot0 + kMaxTaskQueues * 8;
-// the main solve's counter buffer continues with the grid-wide spreading control words
-// (DevParams::gspread, gs_ctrl_words(W) u32 for W waves), zeroed with the queues
-constexpr int kGsSlot0 = kNumCounterSlots;
-constexpr int kMainCounterSlots = kGsSlot0 + gs_ctrl_words(kGsMaxWaves) / 2;
+constexpr int kMainCounterSlots = kNumCounterSlots;  // the main solve's counter buffer
 
 // the first balls of every estimated point (after launch_point_setup)
 hipError_t launch_first_balls(int dim, const DevScene& sc, const DevParams& prm, const float* pts, int64_t n,

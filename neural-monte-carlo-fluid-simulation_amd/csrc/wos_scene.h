@@ -129,12 +129,6 @@ struct DevParams {
   int32_t force_estimate;   // 1: estimate every point, inside the domain or not (BVC's Dirichlet samples:
                             // BoundarySampler::computeEstimates solves at every sample, boundary_sampler.h:125-166)
   int32_t tail_spread;      // 1: the walk kernel instantiation that hands walks to idle sibling waves
-  // tail spreading across the grid (tail_spread only; nullptr: inside the workgroup): the control
-  // words of gspread_waves waves (gs_ctrl_words, zeroed per launch) and kGsMailWords u32 of
-  // mailbox per wave
-  uint32_t* gspread;
-  uint32_t* gspread_mail;
-  int32_t gspread_waves;
   int32_t wave_prio;        // 0..3: the walk / fold kernels' waves issue at this priority (s_setprio) --
                             // boundary value caching's concurrent walk sets, longest chain highest
   uint64_t seed;
@@ -153,18 +147,6 @@ struct DevParams {
 // kMaxTaskQueues, kTaskQueueStride u32 words (64 B) apart
 constexpr int kMaxTaskQueues = 32;
 constexpr unsigned int kTaskQueueStride = 16;
-// grid-wide tail spreading (DevParams::gspread): at most kGsMaxWaves waves; control words
-// gs_ctrl_words(W) (a multiple of 16) after the counters (wos_launch.h kGsSlot0), and a
-// mailbox of kGsMailWords u32 per wave
-constexpr int kGsMaxWaves = 8192;
-// 1: the walk kernel carries the grid-wide hand-over and solves enable it (A/B builds); 0 (shipped):
-// compiled out -- measured slower than spreading inside the workgroup (DESIGN, round 5)
-#ifndef WOS_GRID_SPREAD
-#define WOS_GRID_SPREAD 0
-#endif
-constexpr int kGsMailWords = 1024;
-constexpr int kGsRecHost = 32 + 32 * 64 + 8192;  // wos_device.h kGsRec0: g_idle, done replicas, SIMD counts; then 4 words per wave
-constexpr int gs_ctrl_words(int waves) { return (kGsRecHost + 4 * waves + 15) / 16 * 16; }
 constexpr int kRejTabBins = 96;
 constexpr float kRejTabScale = 8.0f;
 

@@ -71,7 +71,7 @@ SCHED_FULL_NEUMANN = 0x2
 SCHED_NO_STAR_GRID = 0x4
 SCHED_NO_DIR_GRID = 0x8
 SCHED_NO_TAIL_SPREAD = 0x10
-SCHED_NO_GRID_SPREAD = 0x20
+SCHED_NO_GRID_SPREAD = 0x20  # reserved: no effect (include/wos.h)
 
 
 class BvcParams(C.Structure):

@@ -24,6 +24,7 @@ Neumann data h as an image over the scene's bounding box (default h = 0, as the
 reference's pde.neumann).
 """
 import os
+import warnings
 
 import numpy as np
 
@@ -40,7 +41,7 @@ def _required(d, key):
     return d[key]
 
 
-# Parsed boundary meshes by (path, size, mtime, dim, flip, normalize): the time-stepper builds
+# Parsed boundary meshes by (real path, inode, size, mtime, dim, flip, normalize): the time-stepper builds
 # a new Scene(sceneConfig, div) every projection (model_split.py:191) on the same OBJ, whose
 # parse would otherwise be repeated each time (the geometry's prepared device records are
 # cached by content in the library, wos_capi.hip geom_get)
@@ -49,8 +50,9 @@ _obj_cache = {}
 
 def _load_boundary(path, dim, flip, normalize):
     try:
-        st = os.stat(path)
-        key = (os.fspath(path), st.st_size, st.st_mtime_ns, dim, flip, normalize)
+        real = os.path.realpath(path)  # a relative path stays right after a chdir
+        st = os.stat(real)
+        key = (real, st.st_ino, st.st_size, st.st_mtime_ns, dim, flip, normalize)
     except OSError:
         key = None  # let the parser report the missing file
     hit = _obj_cache.get(key) if key is not None else None
@@ -63,6 +65,28 @@ def _load_boundary(path, dim, flip, normalize):
                 _obj_cache.pop(next(iter(_obj_cache)))
             _obj_cache[key] = hit
     return hit
+
+
+def _junction_near_misses(v, dv, rel=1e-6):
+    """Dirichlet vertices within rel x (scene extent) of a Neumann vertex but not bit-equal to
+    one.  Boundary value caching welds the two parts' normals at junction vertices by exact
+    position (as the reference's one-mesh computeNormals shares them); two OBJ files whose shared
+    corner differs in the last bits would silently not weld -- this makes such a mesh visible."""
+    v = np.asarray(v, np.float32)
+    dv = np.asarray(dv, np.float32)
+    if v.size == 0 or dv.size == 0:
+        return 0
+    allv = np.concatenate([v, dv])
+    tol = rel * float(np.max(allv.max(0) - allv.min(0)))
+    exact = {tuple(p) for p in (v + np.float32(0.0)).tolist()}  # +0 == -0
+    n = 0
+    for s in range(0, dv.shape[0], 1024):
+        blk = dv[s:s + 1024]
+        d = np.abs(blk[:, None, :].astype(np.float64) - v[None, :, :]).max(-1).min(1)
+        for p, dd in zip((blk + np.float32(0.0)).tolist(), d):
+            if dd <= tol and tuple(p) not in exact:
+                n += 1
+    return n
 
 
 def _read_pfm(path):
@@ -100,8 +124,14 @@ class Scene:
             flip, normalize = False, False
         v, ix = _load_boundary(boundary, dim, flip, normalize)
         dv = dix = None
+        self.junction_near_misses = 0
         if config.get("dirichletBoundary"):
             dv, dix = _load_boundary(config["dirichletBoundary"], dim, flip, normalize)
+            self.junction_near_misses = _junction_near_misses(v, dv)
+            if self.junction_near_misses:
+                warnings.warn(f"{self.junction_near_misses} Dirichlet vertices lie within 1e-6 of the scene extent of "
+                              "a Neumann vertex without being equal to it: those junctions are not welded (boundary "
+                              "value caching's Dirichlet normals, wos_bvc_host.cpp dirichlet_normals)", stacklevel=2)
         nkw = {}
         if config.get("neumannBoundaryValue"):
             if dim != 2:

@@ -11,10 +11,9 @@ wos_solver_params.schedule (include/wos.h WOS_SCHED_*) selects, per solve:
 * WOS_SCHED_NO_DIR_GRID  the culled Dirichlet-distance scans alone, without the
                          Dirichlet cell grid (2D scenes with Dirichlet segments);
 * WOS_SCHED_NO_TAIL_SPREAD the walk kernel without the hand-over of walks to idle sibling
-                         waves (2D scenes with LDS geometry use it by default);
-* WOS_SCHED_NO_GRID_SPREAD hand-overs inside a workgroup only (by default a wave hands walks
-                         to idle waves anywhere in the grid, device-scope mailboxes).
-One process solves the same points under all 64 combinations of the bits and compares p, grad p,
+                         waves (2D scenes with LDS geometry use it by default).
+(WOS_SCHED_NO_GRID_SPREAD is reserved and has no effect: the grid-wide hand-over was removed.)
+One process solves the same points under all 32 combinations of the five bits and compares p, grad p,
 the per-point walk counts and step counts bit for bit with the default (schedule 0), which
 itself is compared with the CPU oracle.
 Karman (2D, no Dirichlet geometry: the walk kernel recomputes the start distance), the
@@ -25,13 +24,12 @@ import pytest
 import objparse
 from wos_amd import WosScene, solver_params, workloads
 from wos_amd._lib import (SCHED_FULL_NEUMANN, SCHED_GEOM_GLOBAL, SCHED_NO_DIR_GRID, SCHED_NO_STAR_GRID,
-                          SCHED_NO_GRID_SPREAD, SCHED_NO_TAIL_SPREAD)
+                          SCHED_NO_TAIL_SPREAD)
 
 pytestmark = pytest.mark.gpu
 
-SETTINGS = list(range(64))  # every combination of the six bits
-assert (SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID | SCHED_NO_DIR_GRID | SCHED_NO_TAIL_SPREAD
-        | SCHED_NO_GRID_SPREAD) == 63
+SETTINGS = list(range(32))  # every combination of the five bits
+assert (SCHED_GEOM_GLOBAL | SCHED_FULL_NEUMANN | SCHED_NO_STAR_GRID | SCHED_NO_DIR_GRID | SCHED_NO_TAIL_SPREAD) == 31
 
 
 def _scenes():

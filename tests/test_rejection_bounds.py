@@ -172,18 +172,22 @@ def _xbound3(R, lam, xs, inv_nb):
     return (r * e * float(inv_nb)) * 1.001 + 1e-6 * float(R) * float(inv_nb)
 
 
-@pytest.mark.parametrize("lam", [50.0, 350.0, 2000.0])
+@pytest.mark.parametrize("lam", [1e-2, 50.0, 350.0, 2000.0, 1e4])
 def test_radius_bound_3d_dominates_exact_threshold(lam):
     """the radius-dependent certain reject of the 3D own generation (rej_xreject3) is above the
-    exact threshold at every radius draw, and rejects most of what the exact test rejects"""
+    exact threshold at every radius draw, and rejects most of what the exact test rejects.
+    The kernel applies it to every 3D Yukawa ball with mu R < 80: the sweep covers small and
+    large lambda, balls up to mu R = 79.9, and radius draws r -> R, where the exact path's
+    float subtraction e^{-mu r} - A0 sinh(mu r) / A1 cancels"""
     rng = np.random.default_rng(23)
-    radii = np.concatenate([np.exp(rng.uniform(np.log(1e-4), np.log(3.0), 40)), [1e-3, 0.02, 0.05, 0.5, 2.0]])
     mu = np.sqrt(lam)
+    radii = np.concatenate([np.exp(rng.uniform(np.log(1e-4), np.log(3.0), 40)), [1e-3, 0.02, 0.05, 0.5, 2.0],
+                            np.array([0.5, 2.5, 10.0, 40.0, 70.0, 79.0, 79.9]) / mu])
     caught = []
     for R in radii.astype(np.float32):
         peak = min(1.0, 1.0 / (mu * float(R)))
         xs = np.unique(np.concatenate([np.linspace(1e-5, 1.0, 600), rng.uniform(0, 1, 300),
-                                       peak * np.linspace(0.3, 1.7, 141)]))
+                                       peak * np.linspace(0.3, 1.7, 141), 1.0 - np.logspace(-7.5, -2, 60)]))
         xs = xs[(xs > 0) & (xs <= 1.0)].astype(np.float32)
         T, q, (muR, inv_nb) = _thresholds_3d(f32(R), f32(lam), xs)
         if not (inv_nb > 0 and np.isfinite(inv_nb)):

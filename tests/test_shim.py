@@ -182,3 +182,41 @@ def test_wost_torch_device_points(gpu):
     _, p2, g2 = zombie_bindings.wost(scene, solver, output, pts.cpu().numpy(), return_numpy=True)
     np.testing.assert_array_equal(p.cpu().numpy(), p2)
     np.testing.assert_array_equal(g.cpu().numpy(), g2)
+
+
+def test_obj_cache_follows_real_path_and_inode(tmp_path, monkeypatch):
+    """The parsed-OBJ cache is keyed by the resolved path and the file's inode:
+    a relative path after a chdir, or a file replaced by one of the same size, is re-parsed."""
+    import zombie_bindings as zb
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir(); b.mkdir()
+    tri = "v 0 0\nv 1 0\nv 0 1\nl 1 2\nl 2 3\nl 3 1\n"
+    (a / "m.obj").write_text(tri)
+    (b / "m.obj").write_text(tri.replace("v 1 0", "v 2 0"))
+    zb._obj_cache.clear()
+    monkeypatch.chdir(a)
+    va, _ = zb._load_boundary("m.obj", 2, False, False)
+    monkeypatch.chdir(b)
+    vb, _ = zb._load_boundary("m.obj", 2, False, False)
+    assert va[1, 0] == 1.0 and vb[1, 0] == 2.0
+    # same size, same mtime, new inode (atomic replace): re-parsed
+    st = os.stat(b / "m.obj")
+    new = tmp_path / "n.obj"
+    new.write_text(tri.replace("v 1 0", "v 3 0"))
+    os.utime(new, ns=(st.st_atime_ns, st.st_mtime_ns))
+    os.replace(new, b / "m.obj")
+    vc, _ = zb._load_boundary("m.obj", 2, False, False)
+    assert vc[1, 0] == 3.0
+    assert zb._load_boundary(str(b / "m.obj"), 2, False, False)[0] is vc  # same file by absolute path: cached
+
+
+def test_junction_near_misses_are_counted():
+    """A Dirichlet vertex a few ulp away from a Neumann vertex (two OBJ exports that do not
+    share the corner bit for bit) is reported; exact junctions and distant vertices are not."""
+    import zombie_bindings as zb
+    v = np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32)
+    dv = np.array([[1, 1], [0.5, 0.5], [np.nextafter(np.float32(0), np.float32(1)), 1], [-0.0, 0]], np.float32)
+    assert zb._junction_near_misses(v, dv) == 1  # (denormal, 1) vs (0, 1); (-0, 0) equals (0, 0)
+    assert zb._junction_near_misses(v, dv[:2]) == 0
+    dv2 = np.array([[np.nextafter(np.float32(1), np.float32(2)), 1]], np.float32)
+    assert zb._junction_near_misses(v, dv2) == 1

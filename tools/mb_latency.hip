@@ -1,4 +1,5 @@
-// microbenchmarks of a lone wave's latencies (gfx950): s_memtime deltas
+// microbenchmarks (gfx950): a lone wave's latencies (s_memtime deltas; no argument), conflicting
+// LDS atomics (argument "atomics"), VALU issue cost per instruction type (argument "issue")
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -175,4 +176,93 @@ int main2() {
   hipLaunchKernelGGL(k_wavemin, 1, 64, 0, 0, d, N); rep("wave_min_u64 (shfl_xor)", 64);
   return 0;
 }
-int main(int argc, char** argv) { if (argc > 1) return main2(); return main1(); }
+// ---- VALU issue cost per wave64 instruction type (the calibration of tools/collect_sq.py)
+// One workgroup per CU (the LDS request admits one), W waves per SIMD (4 W waves per workgroup,
+// dealt one per SIMD in turn), every wave issuing 16 independent chains of one instruction type
+// for `n` rounds: SIMD-cycles per wave-instruction = elapsed x 2.4 GHz / (instructions per SIMD),
+// the same nominal clock the counter passes divide by.
+constexpr int kIssueChains = 16;
+template <int OP>
+__global__ void k_issue(float* out, int n, float seed) {
+  extern __shared__ float big[];
+  float a[kIssueChains];
+  double d[kIssueChains];
+  unsigned u[kIssueChains];
+  unsigned long long q[kIssueChains];
+  for (int c = 0; c < kIssueChains; c++) {
+    a[c] = seed + c + threadIdx.x;
+    d[c] = (double)a[c];
+    u[c] = (unsigned)c * 977u + threadIdx.x;
+    q[c] = (unsigned long long)u[c] * 3u;
+  }
+  const float fb = seed * 0.5f, fc = seed * 0.25f;
+  const double db = (double)fb, dc = (double)fc;
+  const unsigned ub = (unsigned)threadIdx.x + 3u;
+  for (int i = 0; i < n; i++) {
+#pragma unroll
+    for (int c = 0; c < kIssueChains; c++) {
+      if (OP == 0) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[c]) : "v"(fb), "v"(fc));
+      if (OP == 1) asm volatile("v_add_u32 %0, %1, %0" : "+v"(u[c]) : "v"(ub));
+      if (OP == 2) asm volatile("v_cndmask_b32 %0, %1, %0, vcc" : "+v"(u[c]) : "v"(ub) : "vcc");  // any mask
+      if (OP == 3) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d[c]) : "v"(db), "v"(dc));
+      if (OP == 4) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[c]));
+      if (OP == 5) asm volatile("v_exp_f32 %0, %0" : "+v"(a[c]));
+      if (OP == 6) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(u[c]) : "v"(ub));
+      if (OP == 7) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(d[c]) : "v"(a[c]));
+      if (OP == 8) asm volatile("v_mov_b32 %0, %1" : "=v"(u[c]) : "v"(u[(c + 1) % kIssueChains]));
+      if (OP == 9) asm volatile("v_add_f64 %0, %1, %0" : "+v"(d[c]) : "v"(db));
+      if (OP == 10) asm volatile("v_mul_f64 %0, %1, %0" : "+v"(d[c]) : "v"(db));
+      if (OP == 11) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(q[c]));
+      if (OP == 12) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(q[c]) : "v"(ub), "v"(ub) : "s0", "s1");
+      if (OP == 13) asm volatile("v_add_f32 %0, %1, %0" : "+v"(a[c]) : "v"(fb));
+    }
+  }
+  float acc = 0.0f;
+  for (int c = 0; c < kIssueChains; c++) acc += a[c] + (float)d[c] + (float)u[c] + (float)q[c];
+  if (acc == 1.2345f) big[threadIdx.x] = acc;  // keeps the chains and the LDS request alive
+  if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = acc + big[0] * 0.0f;
+}
+int main3() {
+  int dev = 0, cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  float* d; hipMalloc(&d, 64);
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  const char* names[] = {"v_fma_f32", "v_add_u32", "v_cndmask_b32", "v_fma_f64", "v_rcp_f64", "v_exp_f32",
+                         "v_mul_lo_u32", "v_cvt_f64_f32", "v_mov_b32", "v_add_f64", "v_mul_f64",
+                         "v_lshlrev_b64", "v_mad_u64_u32", "v_add_f32"};
+  const size_t lds = 96 * 1024;  // > half of a CU's 160 KB: one workgroup per CU
+  printf("{\"cus\": %d, \"clock_ghz_nominal\": 2.4, \"chains\": %d, \"results\": [\n", cus, kIssueChains);
+  bool first = true;
+  for (int op = 0; op < 14; op++) {
+    for (int w : {1, 2, 4}) {
+      const int n = 4096;
+      auto launch = [&]() {
+        switch (op) {
+#define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(cus), dim3(256 * w), lds, 0, d, n, 1.0f); break;
+          K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13)
+#undef K
+        }
+      };
+      hipFuncSetAttribute((const void*)k_issue<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      launch(); hipDeviceSynchronize();
+      float best = 1e30f;
+      for (int r = 0; r < 5; r++) {
+        hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms = 0.0f; hipEventElapsedTime(&ms, e0, e1);
+        best = ms < best ? ms : best;
+      }
+      const double per_simd = (double)n * kIssueChains * w;  // wave-instructions per SIMD
+      const double cyc = best * 1e-3 * 2.4e9 / per_simd;
+      printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"simd_cycles_per_wave_instr\": %.3f}",
+             first ? " " : ",\n ", names[op], w, best, cyc);
+      first = false;
+    }
+  }
+  printf("\n]}\n");
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'i') return main3();
+  if (argc > 1) return main2();
+  return main1();
+}

@@ -642,7 +642,11 @@ int ensure_workspace(DevCtx& c, int dim, size_t npts) {
 }
 
 // walk tasks per batch: 2^24 tasks = 0.8 GB (2D) / 1.0 GB (3D) of workspace
-constexpr int64_t kMaxBatchTasks = (int64_t)1 << 24;
+#ifndef WOS_BATCH_LOG2
+#define WOS_BATCH_LOG2 24
+#endif
+static_assert(WOS_BATCH_LOG2 <= 30, "task indices carry a flag in bit 31 (wos_walk_kernel hand-out)");
+constexpr int64_t kMaxBatchTasks = (int64_t)1 << WOS_BATCH_LOG2;
 
 int ensure_tasks_in(float*& d_tasks, int64_t& task_cap, int32_t*& d_pstate, int64_t& pstate_cap, int dim,
                     int64_t tasks, int64_t points) {

@@ -463,3 +463,40 @@ def test_fast_bessel_error_within_certified_band(gpu, oracle, which, ref_which):
     ref = np.array([oracle.lib().oracle_bessel(ref_which, float(v), 0) for v in x])
     rel = np.abs(got - ref) / np.abs(ref)
     assert rel.max() < 2e-6, rel.max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [2, 3])
+def test_empty_single_and_outside_batches(gpu, oracle, dim):
+    """Degenerate batches the time-stepper can hand over: no points (empty outputs, zero
+    counters), one point, and points that all lie outside the domain (p = grad p = 0, no
+    walks) -- host and device inputs alike; the single point equals the oracle bit for bit."""
+    import torch
+    if dim == 2:
+        cfg = workloads.karman_config(n_walks=32)
+        v, ix = objparse.load(cfg["obj"], 2)
+        outside = np.array([[-100.0, -100.0], [100.0, 50.0]], np.float32)
+    else:
+        cfg = workloads.cube_config(res=8, n_walks=16)
+        v, ix = objparse.load(cfg["obj"], 3)
+        outside = np.array([[2.0, 0.0, 0.0], [0.0, -3.0, 0.5]], np.float32)
+    prm = solver_params(cfg["solver"], cfg["output"])
+    sc = WosScene(v, ix, cfg["source"], 350.0, watertight=True)
+    try:
+        p, g, st = sc.solve(np.zeros((0, dim), np.float32), prm)
+        assert p.shape == (0,) and g.shape == (0, dim) and st["walk_steps"] == 0 and st["walks_recorded"] == 0
+        pd, gd, _ = sc.solve(torch.zeros((0, dim), device="cuda"), prm)
+        assert pd.shape == (0,) and gd.shape == (0, dim)
+        one = np.ascontiguousarray(cfg["points"][3:4])
+        p1, g1, st1 = sc.solve(one, prm)
+        po, go, _, _, _ = oracle.solve(oracle.OracleScene(v, ix, cfg["source"], 350.0),
+                                       oracle.make_params(cfg["solver"], cfg["output"]), one, index_base=3)
+        assert st1["walks_recorded"] > 0
+        p1b, g1b, _ = sc.solve(one, prm, index_base=3)
+        assert_bits_equal(p1b, po)
+        assert_bits_equal(g1b, go)
+        p0, g0, st0 = sc.solve(outside, prm)
+        assert np.array_equal(p0, np.zeros(2, np.float32)) and np.array_equal(g0, np.zeros((2, dim), np.float32))
+        assert st0["walk_steps"] == 0 and st0["points_estimated"] == 0
+    finally:
+        sc.close()

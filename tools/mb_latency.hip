@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <vector>
+#include <algorithm>
 __global__ void k_lds_chain(unsigned long long* out, int n, int seed) {
   __shared__ int buf[1024];
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) buf[i] = (i * 7 + 1) & 1023;
@@ -183,7 +185,8 @@ int main2() {
 // the same nominal clock the counter passes divide by.
 constexpr int kIssueChains = 16;
 template <int OP>
-__global__ void k_issue(float* out, int n, float seed) {
+__global__ void k_issue(float* out, int n, float seed, unsigned long long* clk) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ float big[];
   float a[kIssueChains];
   double d[kIssueChains];
@@ -198,12 +201,13 @@ __global__ void k_issue(float* out, int n, float seed) {
   const float fb = seed * 0.5f, fc = seed * 0.25f;
   const double db = (double)fb, dc = (double)fc;
   const unsigned ub = (unsigned)threadIdx.x + 3u;
+  const unsigned long long em = __builtin_amdgcn_read_exec();  // a lane mask in an SGPR pair (no VCC hazard)
   for (int i = 0; i < n; i++) {
 #pragma unroll
     for (int c = 0; c < kIssueChains; c++) {
       if (OP == 0) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[c]) : "v"(fb), "v"(fc));
       if (OP == 1) asm volatile("v_add_u32 %0, %1, %0" : "+v"(u[c]) : "v"(ub));
-      if (OP == 2) asm volatile("v_cndmask_b32 %0, %1, %0, vcc" : "+v"(u[c]) : "v"(ub) : "vcc");  // any mask
+      if (OP == 2) asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(u[c]) : "v"(ub), "s"(em));  // SGPR mask
       if (OP == 3) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d[c]) : "v"(db), "v"(dc));
       if (OP == 4) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[c]));
       if (OP == 5) asm volatile("v_exp_f32 %0, %0" : "+v"(a[c]));
@@ -221,16 +225,24 @@ __global__ void k_issue(float* out, int n, float seed) {
   for (int c = 0; c < kIssueChains; c++) acc += a[c] + (float)d[c] + (float)u[c] + (float)q[c];
   if (acc == 1.2345f) big[threadIdx.x] = acc;  // keeps the chains and the LDS request alive
   if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = acc + big[0] * 0.0f;
+  // in-kernel clock of this workgroup: shader cycles (s_memtime) over 100 MHz ticks (s_memrealtime)
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t1 - t0; clk[2 * blockIdx.x + 1] = r1 - r0; }
 }
 int main3() {
   int dev = 0, cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   float* d; hipMalloc(&d, 64);
+  unsigned long long* dclk; hipMalloc(&dclk, 2 * sizeof(unsigned long long) * cus);
+  std::vector<unsigned long long> hclk(2 * cus);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const char* names[] = {"v_fma_f32", "v_add_u32", "v_cndmask_b32", "v_fma_f64", "v_rcp_f64", "v_exp_f32",
                          "v_mul_lo_u32", "v_cvt_f64_f32", "v_mov_b32", "v_add_f64", "v_mul_f64",
                          "v_lshlrev_b64", "v_mad_u64_u32", "v_add_f32"};
   const size_t lds = 96 * 1024;  // > half of a CU's 160 KB: one workgroup per CU
+#define A(o) hipFuncSetAttribute((const void*)k_issue<o>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7) A(8) A(9) A(10) A(11) A(12) A(13)
+#undef A
   printf("{\"cus\": %d, \"clock_ghz_nominal\": 2.4, \"chains\": %d, \"results\": [\n", cus, kIssueChains);
   bool first = true;
   for (int op = 0; op < 14; op++) {
@@ -238,23 +250,32 @@ int main3() {
       const int n = 4096;
       auto launch = [&]() {
         switch (op) {
-#define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(cus), dim3(256 * w), lds, 0, d, n, 1.0f); break;
+#define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(cus), dim3(256 * w), lds, 0, d, n, 1.0f, dclk); break;
           K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13)
 #undef K
         }
       };
-      hipFuncSetAttribute((const void*)k_issue<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      launch(); hipDeviceSynchronize();
+      // ~0.3 s of back-to-back launches first, so the chip holds its loaded clock (DVFS)
+      hipEventRecord(e0);
+      for (int r = 0; r < 400; r++) launch();
+      hipEventRecord(e1); hipEventSynchronize(e1);
       float best = 1e30f;
       for (int r = 0; r < 5; r++) {
         hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
         float ms = 0.0f; hipEventElapsedTime(&ms, e0, e1);
         best = ms < best ? ms : best;
       }
+      hipMemcpy(hclk.data(), dclk, hclk.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+      std::vector<double> ghz;
+      for (int b = 0; b < cus; b++)
+        if (hclk[2 * b + 1]) ghz.push_back((double)hclk[2 * b] / (double)hclk[2 * b + 1] * 0.1);
+      std::sort(ghz.begin(), ghz.end());
+      const double clk_ghz = ghz.empty() ? 0.0 : ghz[ghz.size() / 2];
       const double per_simd = (double)n * kIssueChains * w;  // wave-instructions per SIMD
       const double cyc = best * 1e-3 * 2.4e9 / per_simd;
-      printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"simd_cycles_per_wave_instr\": %.3f}",
-             first ? " " : ",\n ", names[op], w, best, cyc);
+      printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"simd_cycles_per_wave_instr\": %.3f, "
+             "\"clock_ghz_in_kernel\": %.3f, \"cycles_at_kernel_clock\": %.3f}",
+             first ? " " : ",\n ", names[op], w, best, cyc, clk_ghz, cyc * clk_ghz / 2.4);
       first = false;
     }
   }

@@ -543,6 +543,7 @@ def main():
             cal = "valu_issue_frac" in sq and "issue_cycles" in sq
             line["valu_issue"] = {"kernel": sq["kernel"],
                                   "frac": sq["valu_issue_frac"] if cal else None,
+                                  "frac_hi": sq.get("valu_issue_frac_hi") if cal else None,
                                   "frac_4cyc": sq.get("valu_issue_frac_4cyc", sq.get("valu_issue_frac")),
                                   "calibrated": cal,
                                   "parts": sq.get("valu_issue_parts"),

@@ -641,9 +641,13 @@ int ensure_workspace(DevCtx& c, int dim, size_t npts) {
   return WOS_OK;
 }
 
-// walk tasks per batch: 2^24 tasks = 0.8 GB (2D) / 1.0 GB (3D) of workspace
+// walk tasks per batch: 2^28 tasks = 16 GB of workspace at most (60 B per task, sized for 3D), 5.6 % of a
+// MI355X's 288 GB -- config E (2^31 walks) runs in 8 batches, D (2^27) and each rank's share of an 8-GPU
+// E in one.  Fewer batches, fewer ramp-downs of the persistent kernels: against 2^24 (round 5) C 12.8 ->
+// 11.6 ms, D 26.0 -> 24.0 ms, E 420 -> 376 ms, first balls of E 127 -> 102 ms, bit-exact
+// (profiles/r6c_ab_batch.log; 2^26 / 2^27 in between).  A smaller solve allocates only what it uses.
 #ifndef WOS_BATCH_LOG2
-#define WOS_BATCH_LOG2 24
+#define WOS_BATCH_LOG2 28
 #endif
 static_assert(WOS_BATCH_LOG2 <= 30, "task indices carry a flag in bit 31 (wos_walk_kernel hand-out)");
 constexpr int64_t kMaxBatchTasks = (int64_t)1 << WOS_BATCH_LOG2;

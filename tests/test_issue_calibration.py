@@ -19,6 +19,7 @@ def _mb(cyc):
 def test_weighted_issue_sums_types_at_their_cost():
     import collect_sq as cs
     cyc = {op: 2.0 for op in set(cs.TYPE_OPS.values()) | set(cs.OTHER_OPS)}
+    cyc["v_cndmask_b32"] = 5.0
     cyc.update({"v_fma_f64": 4.0, "v_mul_f64": 4.0, "v_add_f64": 4.0, "v_rcp_f64": 8.0, "v_exp_f32": 4.0})
     got = cs.issue_cycles(_mb(cyc))
     assert got == cyc  # the 4-waves-per-SIMD column
@@ -34,3 +35,5 @@ def test_weighted_issue_sums_types_at_their_cost():
     assert sum(parts.values()) == pytest.approx(frac)
     # the CDNA3 rule of thumb would have charged every instruction 4 cycles
     assert frac < 1000 * 4 / simd_cycles
+    hi, _, _ = cs.weighted_issue(issue, mix, mix2, cyc, other_op="v_cndmask_b32")
+    assert hi == pytest.approx((busy + 390 * 3.0) / simd_cycles)

@@ -112,7 +112,8 @@ TYPE_OPS = {
     "SQ_INSTS_VALU_INT32": "v_add_u32", "SQ_INSTS_VALU_INT64": "v_lshlrev_b64",
     "SQ_INSTS_VALU_CVT": "v_cvt_f64_f32",
 }
-OTHER_OPS = ("v_cndmask_b32", "v_mov_b32")  # untyped VALU: moves, selects, compares, lane ops
+OTHER_OPS = ("v_mov_b32", "v_cndmask_b32")  # untyped VALU (moves, selects, compares, lane ops): at the
+# move's cost (the calibrated figure) and at the SGPR-mask select's (the upper bound, `_hi`)
 
 
 def issue_cycles(mb, waves=4):
@@ -120,7 +121,7 @@ def issue_cycles(mb, waves=4):
     return {r["op"]: r["simd_cycles_per_wave_instr"] for r in mb["results"] if r["waves_per_simd"] == waves}
 
 
-def weighted_issue(issue, mix, mix2, cyc):
+def weighted_issue(issue, mix, mix2, cyc, other_op="v_mov_b32"):
     """Calibrated VALU issue fraction of one kernel: sum over types of count x cycles / SIMD-cycles."""
     n = dict(mix["counters"], **mix2["counters"])
     parts, typed = {}, 0.0
@@ -128,7 +129,7 @@ def weighted_issue(issue, mix, mix2, cyc):
         parts[ctr] = n.get(ctr, 0.0) * cyc[op]
         typed += n.get(ctr, 0.0)
     other = max(0.0, issue["counters"]["SQ_INSTS_VALU"] - typed)
-    c_other = max(cyc[o] for o in OTHER_OPS)
+    c_other = cyc[other_op]
     parts["untyped"] = other * c_other
     busy = sum(parts.values())
     denom = issue["kernel_s"] * CLOCK_HZ * SIMDS
@@ -145,12 +146,14 @@ def combine(tag, config, mb_path):
     mix = json.load(open(os.path.join(out, f"{pfx}_mix_walk_sq.json")))
     mix2 = json.load(open(os.path.join(out, f"{pfx}_mix2_walk_sq.json")))
     frac, parts, other = weighted_issue(issue, mix, mix2, cyc)
+    frac_hi, _, _ = weighted_issue(issue, mix, mix2, cyc, other_op="v_cndmask_b32")
     issue.update({
-        "valu_issue_frac": frac, "valu_issue_parts": parts, "valu_untyped_instr": other,
+        "valu_issue_frac": frac, "valu_issue_frac_hi": frac_hi, "valu_issue_parts": parts,
+        "valu_untyped_instr": other,
         "issue_cycles": {op: cyc[op] for op in sorted(set(TYPE_OPS.values()) | set(OTHER_OPS))},
         "issue_calibration": f"{os.path.basename(mb_path)}: tools/mb_latency.hip issue, SIMD-cycles per wave64 "
                              "instruction at 4 waves/SIMD; counts from the mix / mix2 passes of the same launches "
-                             "(untyped VALU at the move / select cost)",
+                             "(untyped VALU at the move's cost; valu_issue_frac_hi: at the SGPR-mask select's)",
     })
     issue["source"] = issue["source"].replace(
         "VALU issue = INSTS_VALU x 4 cycles / (kernel time x 2.4 GHz x 1024 SIMDs)",
@@ -158,7 +161,8 @@ def combine(tag, config, mb_path):
         "SIMDs); valu_issue_frac_4cyc = INSTS_VALU x 4 cycles / the same")
     path = os.path.join(out, f"{pfx}_walk_sq.json")
     json.dump(issue, open(path, "w"), indent=1)
-    print(json.dumps({"config": config, "valu_issue_frac": frac, "valu_issue_frac_4cyc": issue["valu_issue_frac_4cyc"],
+    print(json.dumps({"config": config, "valu_issue_frac": frac, "valu_issue_frac_hi": frac_hi,
+                      "valu_issue_frac_4cyc": issue["valu_issue_frac_4cyc"],
                       "parts": parts}))
 
 

@@ -180,7 +180,7 @@ int main2() {
 }
 // ---- VALU issue cost per wave64 instruction type (the calibration of tools/collect_sq.py)
 // One workgroup per CU (the LDS request admits one), W waves per SIMD (4 W waves per workgroup,
-// dealt one per SIMD in turn), every wave issuing 16 independent chains of one instruction type
+// dealt one per SIMD in turn; W = 8: two 16-wave workgroups per CU), every wave issuing 16 independent chains of one instruction type
 // for `n` rounds: SIMD-cycles per wave-instruction = elapsed x 2.4 GHz / (instructions per SIMD),
 // the same nominal clock the counter passes divide by.
 constexpr int kIssueChains = 16;
@@ -233,24 +233,26 @@ int main3() {
   int dev = 0, cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   float* d; hipMalloc(&d, 64);
-  unsigned long long* dclk; hipMalloc(&dclk, 2 * sizeof(unsigned long long) * cus);
-  std::vector<unsigned long long> hclk(2 * cus);
+  unsigned long long* dclk; hipMalloc(&dclk, 4 * sizeof(unsigned long long) * cus);
+  std::vector<unsigned long long> hclk(4 * cus);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const char* names[] = {"v_fma_f32", "v_add_u32", "v_cndmask_b32", "v_fma_f64", "v_rcp_f64", "v_exp_f32",
                          "v_mul_lo_u32", "v_cvt_f64_f32", "v_mov_b32", "v_add_f64", "v_mul_f64",
                          "v_lshlrev_b64", "v_mad_u64_u32", "v_add_f32"};
   const size_t lds = 96 * 1024;  // > half of a CU's 160 KB: one workgroup per CU
+  const size_t lds8 = 72 * 1024;  // 8 waves/SIMD: two 1024-thread workgroups per CU
 #define A(o) hipFuncSetAttribute((const void*)k_issue<o>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7) A(8) A(9) A(10) A(11) A(12) A(13)
 #undef A
   printf("{\"cus\": %d, \"clock_ghz_nominal\": 2.4, \"chains\": %d, \"results\": [\n", cus, kIssueChains);
   bool first = true;
   for (int op = 0; op < 14; op++) {
-    for (int w : {1, 2, 4}) {
+    for (int w : {1, 2, 4, 8}) {
       const int n = 4096;
       auto launch = [&]() {
         switch (op) {
-#define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(cus), dim3(256 * w), lds, 0, d, n, 1.0f, dclk); break;
+#define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(w > 4 ? 2 * cus : cus), dim3(w > 4 ? 1024 : 256 * w), \
+                                        w > 4 ? lds8 : lds, 0, d, n, 1.0f, dclk); break;
           K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13)
 #undef K
         }
@@ -267,7 +269,7 @@ int main3() {
       }
       hipMemcpy(hclk.data(), dclk, hclk.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
       std::vector<double> ghz;
-      for (int b = 0; b < cus; b++)
+      for (int b = 0; b < (w > 4 ? 2 * cus : cus); b++)
         if (hclk[2 * b + 1]) ghz.push_back((double)hclk[2 * b] / (double)hclk[2 * b + 1] * 0.1);
       std::sort(ghz.begin(), ghz.end());
       const double clk_ghz = ghz.empty() ? 0.0 : ghz[ghz.size() / 2];

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define WOS_ABI_VERSION 9
+#define WOS_ABI_VERSION 10
 
 enum {
     WOS_OK = 0,
@@ -112,6 +112,13 @@ int wos_scene_set_source(wos_scene *scene, const float *source, const int32_t *d
  * workspace allocation nor a re-preparation.  This releases both for `device`
  * (-1: every device); live scenes stay valid and the next solve reallocates. */
 int wos_release_caches(int32_t device);
+
+/* Walk tasks per batch (ABI 10).  A solve runs its points in batches of at most this many walk
+ * tasks (the per-device workspace holds one batch: 60 B per task); default 2^28 = 16 GB at most,
+ * sized for a 288 GB MI355X (fewer batches, fewer ramp-downs of the persistent kernels).  A
+ * caller that shares the GPU with other work can cap it.  max_tasks <= 0: the default; else
+ * clamped to [2^16, 2^30].  Returns the previous value.  Results do not depend on it. */
+int64_t wos_set_max_batch_tasks(int64_t max_tasks);
 
 typedef struct wos_scene_info {
     int32_t dim, n_prims, n_silhouettes, n_dprims, device;

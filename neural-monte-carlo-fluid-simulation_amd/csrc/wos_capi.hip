@@ -22,6 +22,7 @@
 #include <cstring>
 #include <memory>
 #include <condition_variable>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -339,6 +340,18 @@ int dir_grid(Geom& g, bool* ok) {
   return WOS_OK;
 }
 
+// walk tasks per batch: 2^28 tasks = 16 GB of workspace at most (60 B per task, sized for 3D), 5.6 % of a
+// MI355X's 288 GB -- config E (2^31 walks) runs in 8 batches, D (2^27) and each rank's share of an 8-GPU
+// E in one.  Fewer batches, fewer ramp-downs of the persistent kernels: against 2^24 (round 5) C 12.8 ->
+// 11.6 ms, D 26.0 -> 24.0 ms, E 420 -> 376 ms, first balls of E 127 -> 102 ms, bit-exact
+// (profiles/r6c_ab_batch.log; 2^26 / 2^27 in between).  A smaller solve allocates only what it uses.
+#ifndef WOS_BATCH_LOG2
+#define WOS_BATCH_LOG2 28
+#endif
+static_assert(WOS_BATCH_LOG2 <= 30, "task indices carry a flag in bit 31 (wos_walk_kernel hand-out)");
+constexpr int64_t kDefaultBatchTasks = (int64_t)1 << WOS_BATCH_LOG2;
+std::atomic<int64_t> g_max_batch_tasks{kDefaultBatchTasks};  // wos_set_max_batch_tasks
+
 }  // namespace
 
 struct wos_scene {
@@ -585,6 +598,12 @@ int wos_scene_destroy(wos_scene* s) {
   return WOS_OK;
 }
 
+int64_t wos_set_max_batch_tasks(int64_t max_tasks) {
+  const int64_t v = max_tasks <= 0 ? kDefaultBatchTasks
+                                   : std::min<int64_t>(std::max<int64_t>(max_tasks, (int64_t)1 << 16), (int64_t)1 << 30);
+  return g_max_batch_tasks.exchange(v);
+}
+
 int wos_release_caches(int32_t device) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
@@ -641,16 +660,6 @@ int ensure_workspace(DevCtx& c, int dim, size_t npts) {
   return WOS_OK;
 }
 
-// walk tasks per batch: 2^28 tasks = 16 GB of workspace at most (60 B per task, sized for 3D), 5.6 % of a
-// MI355X's 288 GB -- config E (2^31 walks) runs in 8 batches, D (2^27) and each rank's share of an 8-GPU
-// E in one.  Fewer batches, fewer ramp-downs of the persistent kernels: against 2^24 (round 5) C 12.8 ->
-// 11.6 ms, D 26.0 -> 24.0 ms, E 420 -> 376 ms, first balls of E 127 -> 102 ms, bit-exact
-// (profiles/r6c_ab_batch.log; 2^26 / 2^27 in between).  A smaller solve allocates only what it uses.
-#ifndef WOS_BATCH_LOG2
-#define WOS_BATCH_LOG2 28
-#endif
-static_assert(WOS_BATCH_LOG2 <= 30, "task indices carry a flag in bit 31 (wos_walk_kernel hand-out)");
-constexpr int64_t kMaxBatchTasks = (int64_t)1 << WOS_BATCH_LOG2;
 
 int ensure_tasks_in(float*& d_tasks, int64_t& task_cap, int32_t*& d_pstate, int64_t& pstate_cap, int dim,
                     int64_t tasks, int64_t points) {
@@ -1029,7 +1038,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
 #ifdef WOS_ACCT_NOSPREAD
   dp.tail_spread = 0;  // HBM-accounting build: the walk kernel without tail spreading (no scratch)
 #endif
-  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, kMaxBatchTasks / wpp));
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n, g_max_batch_tasks.load() / wpp));
   const int64_t n_chunks = n > 0 ? (n + chunk - 1) / chunk : 0;
   int grid_fb = 0, grid_walk = 0, bpc_fb = 0, bpc_walk = 0;
   if (n > 0) {
@@ -1400,21 +1409,22 @@ int wos_bvc(wos_scene* s, const wos_solver_params* prm, const wos_bvc_params* bp
     if (rc != WOS_OK) return rc;
   }
   int64_t side_tasks[kSideWs] = {0, 0}, side_points[kSideWs] = {0, 0};
+  const int64_t max_batch = g_max_batch_tasks.load();
   for (const Run& r : runs) {
     const int64_t m = r.b1 - r.b0;
     if (!r.dir || bp->use_finite_differences) {
       const int64_t w = r.dir ? bp->n_walks_gradient : bp->n_walks_solution;
-      if (m * w > kMaxBatchTasks) return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
+      if (m * w > max_batch) return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
       side_tasks[0] = std::max(side_tasks[0], m * w);
       side_points[0] = std::max(side_points[0], m);
     } else if (dir_solve) {
       const int64_t wpp = gp.disable_gradient_antithetic_variates ? gp.n_walks : 2 * std::max(1, gp.n_walks / 2);
-      const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(m, kMaxBatchTasks / wpp));
+      const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(m, max_batch / wpp));
       int rc = ensure_tasks(c, 2, chunk * wpp, chunk);
       if (rc != WOS_OK) return rc;
     }
   }
-  if (nn * bp->n_walks_solution > kMaxBatchTasks)
+  if (nn * bp->n_walks_solution > max_batch)
     return fail(WOS_E_CAPACITY, "wos_bvc: samples x nWalks exceed one task batch");
   side_tasks[1] = nn * bp->n_walks_solution;
   side_points[1] = nn;

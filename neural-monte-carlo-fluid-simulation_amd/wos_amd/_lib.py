@@ -9,7 +9,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("WOS_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libwos_hip.so")
 
-ABI_VERSION = 9  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
+ABI_VERSION = 10  # include/wos.h WOS_ABI_VERSION this binding's structs mirror
 WOS_OK = 0
 WOS_E_CAPACITY = -4
 WOS_PTRS_DEVICE = 0x1
@@ -99,7 +99,7 @@ EXPORTS = (
     "wos_load_obj", "wos_mesh_free", "wos_scene_create", "wos_scene_destroy",
     "wos_scene_get_info", "wos_scene_set_source", "wos_release_caches", "wos_default_params", "wos_solve",
     "wos_solve_stats", "wos_default_bvc_params", "wos_bvc",
-    "wos_selftest_math", "wos_last_error", "wos_abi_version", "wos_device_count",
+    "wos_selftest_math", "wos_last_error", "wos_abi_version", "wos_device_count", "wos_set_max_batch_tasks",
 )
 
 _lib = None
@@ -127,6 +127,8 @@ def load():
     L.wos_scene_set_source.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.c_void_p]
     L.wos_release_caches.restype = C.c_int
     L.wos_release_caches.argtypes = [C.c_int32]
+    L.wos_set_max_batch_tasks.restype = C.c_int64
+    L.wos_set_max_batch_tasks.argtypes = [C.c_int64]
     L.wos_default_params.restype = None
     L.wos_default_params.argtypes = [C.POINTER(SolverParams)]
     L.wos_solve.restype = C.c_int

@@ -364,6 +364,12 @@ def release_caches(device=-1):
     check(_lib.load().wos_release_caches(int(device)), "wos_release_caches")
 
 
+def set_max_batch_tasks(n):
+    """Walk tasks per batch (wos_set_max_batch_tasks; n <= 0: the default 2^28).  Returns the
+    previous value.  Results do not depend on it; it bounds the per-device workspace."""
+    return int(_lib.load().wos_set_max_batch_tasks(int(n)))
+
+
 def selftest_math(which, x, device=0):
     x = np.ascontiguousarray(x, dtype=np.float64)
     out = np.empty_like(x)

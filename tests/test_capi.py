@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert wos_amd.load_library().wos_abi_version() == wos_amd._lib.ABI_VERSION == 9
+    assert wos_amd.load_library().wos_abi_version() == wos_amd._lib.ABI_VERSION == 10
 
 
 @pytest.mark.parametrize("path,dim", [(workloads.KARMAN_OBJ, 2), (workloads.SQUARE_OBJ, 2), (workloads.CUBE_OBJ, 3)])
@@ -101,3 +101,14 @@ def test_schedule_bits_match_header():
     for name, v in bits.items():
         assert getattr(_lib, name) == v, name
     assert len(set(bits.values())) == len(bits) and all(v & (v - 1) == 0 for v in bits.values())
+
+
+def test_max_batch_tasks_setting():
+    """wos_set_max_batch_tasks (ABI 10): returns the previous value, clamps to [2^16, 2^30],
+    <= 0 restores the default 2^28 -- a host-side setting, no GPU needed."""
+    L = wos_amd.load_library()
+    first = L.wos_set_max_batch_tasks(0)
+    assert L.wos_set_max_batch_tasks(1000) == 1 << 28
+    assert L.wos_set_max_batch_tasks(1 << 40) == 1 << 16
+    assert L.wos_set_max_batch_tasks(-1) == 1 << 30
+    assert wos_amd.set_max_batch_tasks(first) == 1 << 28

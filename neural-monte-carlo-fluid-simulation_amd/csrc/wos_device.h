@@ -3986,6 +3986,9 @@ __device__ __forceinline__ void flush_walk_counters(unsigned long long* counters
 #define WOS_TASK_GRAB 64
 #endif
 constexpr unsigned int kTaskGrab = WOS_TASK_GRAB;  // tasks a wave takes from the global queue at once
+#ifndef WOS_TASK_GRAB3
+#define WOS_TASK_GRAB3 128u  // the same in 3D (wos_walk_kernel kGrabD)
+#endif
 // The walk queue is dealt round-robin over kTaskQueues counters in windows of kTaskGrab
 // tasks (queue x serves windows x, x + Q, x + 2Q, ... of the cost order): a wave draws
 // from the counter of its block's home queue and, once that one is exhausted, from the
@@ -4142,7 +4145,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   // <= 64 points per window
   // 3D: windows of 128 tasks (walk kernel -2 % on D and E, bit-exact: profiles/r5zo_ab_grab3.log; in 2D they
   // slowed the karman stride-8 shard, r5zl_ab_star_help2_queue.log)
-  constexpr uint32_t kGrabD = DIM == 3 ? 128u : kTaskGrab;
+  constexpr uint32_t kGrabD = DIM == 3 ? WOS_TASK_GRAB3 : kTaskGrab;
   const uint32_t G_win = kGrabD < 63u * wpp ? kGrabD : 63u * wpp;
   // the head of the cost order (the hardest points) is dealt in smaller windows, so the
   // long walks of one point spread over more waves: kTaskHead windows of kTaskGrabHead

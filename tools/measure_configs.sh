@@ -14,7 +14,7 @@ for c in $CFGS; do
   t=${TAG}_$c; [ $c = B ] && t=$TAG
   timeout -k 10 600 python3 tools/collect_traffic.py $t $c > gpurun_out/${t}_traffic.log 2>&1 || exit 1
   timeout -k 10 300 python3 tools/collect_sq.py $t $c > gpurun_out/${t}_sq.log 2>&1 || exit 1
-  timeout -k 10 300 python3 tools/collect_sq.py $TAG $c mix > gpurun_out/${t}_mix.log 2>&1 || exit 1
-  timeout -k 10 300 python3 tools/collect_sq.py $TAG $c mix2 > gpurun_out/${t}_mix2.log 2>&1 || exit 1
+  timeout -k 10 300 python3 tools/collect_sq.py $t $c mix > gpurun_out/${t}_mix.log 2>&1 || exit 1
+  timeout -k 10 300 python3 tools/collect_sq.py $t $c mix2 > gpurun_out/${t}_mix2.log 2>&1 || exit 1
   python3 tools/collect_sq.py combine $TAG $c gpurun_out/${TAG}_mb_issue.json >> gpurun_out/${TAG}_issue.log 2>&1 || exit 1
 done

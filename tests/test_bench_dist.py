@@ -178,3 +178,17 @@ def test_bench_two_ranks_gloo_hip_engine(tmp_path, gpu):
     _, _, st = sc.solve(cfg["points"], solver_params(cfg["solver"], cfg["output"]))
     sc.close()
     assert s["walk_steps_per_projection"] == st["walk_steps"]
+
+
+@pytest.mark.gpu
+def test_bench_more_rccl_ranks_than_gpus_is_refused():
+    """`bench.py --gpus 2` over RCCL on a box with fewer GPUs than ranks exits non-zero with a
+    message and prints no line (RCCL cannot put two ranks on one GPU); it does not hang."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("needs a box with a single GPU")
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--points", "1024", "--no-cpu-baseline",
+                "--no-projection-wall", "--no-strong"], timeout=110)
+    assert r.returncode != 0
+    assert "RCCL ranks need 2 GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -972,6 +972,10 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
   const int lhs_floats = ((2 * dp.n_pairs * (dim - 1)) + 3) & ~3;
   // the first-ball kernel stages no geometry (the point-setup kernel did the queries)
   const size_t shmem_fb = wos::kWavesPerBlockHost * wos::first_ball_wave_lds_bytes(lhs_floats, dp.n_pairs);
+  size_t shmem_fb_run = shmem_fb;  // + the staged jump constants (dp.lhs_jump_n), decided below
+#ifndef WOS_LHS_JUMP_STAGE
+#define WOS_LHS_JUMP_STAGE 1
+#endif
   // scenes beyond the LDS budget (or WOS_SCHED_GEOM_GLOBAL): geometry read from global
   // memory through L2, LDS for the per-wave scratch only
   wos::DevScene dfb = s->dev;
@@ -1045,6 +1049,16 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     int rc = ensure_tasks(c, dim, chunk * wpp, chunk);
     if (rc != WOS_OK) return rc;
     HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, false, shmem_fb, &bpc_fb, dp.robust != 0));
+    // the stratified samples' jump constants in LDS, unless they cost the first-ball kernel a block per CU
+    const int jn = std::min(2 * (2 * dp.n_pairs) * (dim - 1), wos::kLhsJumpMax);
+    const size_t shmem_j = shmem_fb + (size_t)jn * 2 * sizeof(uint64_t);
+    int bpc_j = 0;
+    if (jn > 0 && shmem_j <= kLdsDynamicMax)
+      HIP_TRY(wos::occupancy_blocks_per_cu(0, dim, false, shmem_j, &bpc_j, dp.robust != 0));
+    if (WOS_LHS_JUMP_STAGE && jn > 0 && bpc_j >= bpc_fb) {
+      dp.lhs_jump_n = jn;
+      shmem_fb_run = shmem_j;
+    }
     const int64_t fb_waves = (chunk + wos::first_ball_points_per_wave(dp.n_pairs) - 1) / wos::first_ball_points_per_wave(dp.n_pairs);
     grid_fb = (int)std::min<int64_t>((fb_waves + wos::kWavesPerBlockHost - 1) / wos::kWavesPerBlockHost,
                                      (int64_t)std::max(1, bpc_fb) * std::max(1, c.num_cus));
@@ -1090,7 +1104,7 @@ int solve_locked(wos_scene* s, const wos_solver_params* prm, const float* pts, i
     HIP_TRY(wos::launch_point_setup(dim, dfb, dp, d_pts + b0 * dim, nb, tk, st));
     HIP_TRY(wos::launch_lpt_order(tk, nb, st));
     HIP_TRY(wos::launch_first_balls(dim, dfb, dp, d_pts + b0 * dim, nb, bbase, index_stride, tk, c.d_counters,
-                                    q_points, grid_fb, shmem_fb, lhs_floats, st));
+                                    q_points, grid_fb, shmem_fb_run, lhs_floats, st));
     HIP_TRY(hipEventRecord(ev[1], st));
     HIP_TRY(wos::launch_walks(dim, dsc, dp, tk, bbase, index_stride, c.d_counters, q_tasks, walk_grid,
                               shmem_walk, geom_floats_walk, st));

@@ -2996,8 +2996,8 @@ __device__ __forceinline__ float star_radius_wave(const LGeom& G, const DevScene
 // ---------------------------------------------------------------------------
 //   1. wos_first_ball_kernel  -- one wave per query point (atomic point queue):
 //      closest-point setup + inside test, the per-point stratified samples (all
-//      lanes at once from a PCG32 jump-ahead table; only the Fisher-Yates swaps
-//      are serial), then lane = antithetic pair: source sample + boundary
+//      lanes at once from a PCG32 jump-ahead table staged in LDS; the Fisher-Yates
+//      shuffle resolved wave-parallel, exactly), then lane = antithetic pair: source sample + boundary
 //      direction of the first ball for both members (walk_on_stars.h:494-575).
 //      Each member becomes a walk task in HBM (start state + its record fields).
 //   2. wos_walk_kernel        -- persistent: every lane runs one walk task at a
@@ -3094,9 +3094,11 @@ __device__ __forceinline__ void lhs_permute(float* strat, const int* partner, in
 }
 
 // per-wave first-ball scratch after the stratified samples and partners: the
-// rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute
-__host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats) {
-  const size_t a = sizeof(RejLDS), b = (size_t)28 * lhs_floats + 64;
+// rejection sampler's LDS, or (before it) the shuffle scratch of lhs_permute -- only
+// for 129..256 strata (fewer: lhs_permute_reg, in registers; more: the serial shuffle)
+__host__ __device__ constexpr size_t fb_union_bytes(int lhs_floats, int nstrat) {
+  const size_t a = sizeof(RejLDS),
+               b = (nstrat > 2 * kWave && nstrat <= 4 * kWave) ? (size_t)28 * lhs_floats + 64 : 0;
   return ((a > b ? a : b) + 15) & ~size_t(15);
 }
 
@@ -3115,134 +3117,124 @@ __host__ __device__ constexpr int fb_points_per_wave(int n_pairs) {
              : 1;
 }
 
-// lhs_permute for the M = P * sd independent shuffles of a wave's P point slots (slot s at
-// wbase + 2 s lhs_floats: samples, then partners) in one pass: the same arithmetic per
-// shuffle, one set of wave syncs and LDS round trips for all of them (M * ceil(nstrat / 64)
-// <= 4 elements per lane).  Scratch: 7 words per element (fb_union_bytes(P * lhs_floats)).
-// Out of line: inlined, its element arrays pushed the first-ball kernels into spills.
-template <int SD, int R>
-__device__ __attribute__((noinline)) void lhs_permute_all_r(float* wbase, int lhs_floats, int P, int nstrat, char* scratch,
-                                                  int lane) {
-  constexpr int C = 4;  // elements per lane: shuffle m = c / R, step j = 64 (c % R) + lane
-  const int M = P * SD, N = M * nstrat;
-  int* link = reinterpret_cast<int*>(scratch);
-  int* val = link + N;
-  int* last = val + N;
-  int* perm = last + N;
-  int* tmp = perm + N;
-  unsigned long long* cmask = reinterpret_cast<unsigned long long*>(tmp + N + (N & 1));
-  int jj[C], bb[C];
-  const int* pd[C];
-  bool ok[C];
+// The same permutation P(j) as lhs_permute, computed in registers: no LDS scratch, no
+// atomics, no wave syncs.  Element e = 64 r + lane of a shuffle lives in chunk r (R chunks,
+// nstrat <= 64 R).  For each chunk the wave ballots every bit of the partners; the lanes of
+// chunk r whose partner equals t are then the AND over bits b of (ballot_b or its
+// complement, as bit b of t), so link(k) and pred(j) are the highest such lane below the
+// element (chunks below it entirely).  V resolves by pointer jumping and the final values by
+// one lane permute (ds_bpermute) per chunk.  Up to MM shuffles (m0 .. m0 + M - 1; shuffle m
+// is dimension m % SD of slot m / SD: samples at strat0 + slot * slot_floats, partners at
+// part0 + slot * slot_floats + dim * nstrat) run side by side for instruction-level overlap.
+template <int B0, int B1>
+__device__ __forceinline__ uint64_t partner_bits_match(const uint64_t* bc, uint32_t t) {
+  uint32_t lo = ~0u, hi = ~0u;
+#pragma unroll
+  for (int b = B0; b < B1; b++) {
+    const uint32_t s = (uint32_t)((int32_t)(t << (31 - b)) >> 31);  // all ones when bit b of t is set
+    lo &= ~((uint32_t)bc[b] ^ s);
+    hi &= ~((uint32_t)(bc[b] >> 32) ^ s);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int R>
+__device__ __forceinline__ int chunk_fetch(const int* v, int e) {  // element e of a shuffle's R chunks
+  int r = __shfl(v[0], e & (kWave - 1));
+#pragma unroll
+  for (int c = 1; c < R; c++) {
+    const int t = __shfl(v[c], e & (kWave - 1));
+    r = (e >> 6) == c ? t : r;
+  }
+  return r;
+}
+
+template <int SD, int R, int MM>
+__device__ __forceinline__ void lhs_permute_reg_body(float* strat0, const int* part0, int slot_floats, int m0, int M,
+                                                     int nstrat, int lane) {
+  constexpr int C = MM * R, NB = R == 1 ? 6 : (R == 2 ? 7 : 8);
+  const uint64_t below = (1ull << lane) - 1ull;
+  int q[C], L[C], V[C], a[C];
+  uint64_t bc[C][NB], vc[C];
 #pragma unroll
   for (int c = 0; c < C; c++) {
-    const int m = c / R;
-    jj[c] = (c % R) * kWave + lane;
-    ok[c] = m < M && jj[c] < nstrat;
-    bb[c] = m * nstrat;
-    pd[c] = reinterpret_cast<const int*>(wbase + 2 * (m / SD) * lhs_floats + lhs_floats) + (m % SD) * nstrat;
+    const int m = m0 + c / R, e = (c % R) * kWave + lane;
+    const bool ok = c / R < M && e < nstrat;
+    const float* st = strat0 + (m / SD) * slot_floats;
+    const int* pd = part0 + (m / SD) * slot_floats + (m % SD) * nstrat;
+    q[c] = ok ? pd[e] : e;
+    a[c] = ok ? __float_as_int(st[SD * e + m % SD]) : 0;
+    vc[c] = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < NB; b++) bc[c][b] = __ballot(ok && ((q[c] >> b) & 1));
   }
+  // link(k): the last step m < k with partner[m] = k (k's high bits are its chunk, a constant)
 #pragma unroll
-  for (int c = 0; c < C; c++)
-    if (ok[c]) { link[bb[c] + jj[c]] = -1; last[bb[c] + jj[c]] = -1; cmask[bb[c] + jj[c]] = 0ull; }
-  wave_sync();
+  for (int c = 0; c < C; c++) {
+    const int r = c % R, c0 = c - r;
+    int l = -1;
 #pragma unroll
-  for (int c = 0; c < C; c++)
-    if (ok[c]) {
-      const int q = pd[c][jj[c]];
-      if (q != jj[c]) atomicMax(&link[bb[c] + q], jj[c]);
+    for (int s = 0; s <= r; s++) {
+      uint64_t mk = vc[c0 + s] & partner_bits_match<0, 6>(bc[c0 + s], (uint32_t)lane) &
+                    partner_bits_match<6, NB>(bc[c0 + s], (uint32_t)(r * kWave));
+      if (s == r) mk &= below;
+      if (mk) l = s * kWave + 63 - __builtin_clzll(mk);
     }
-  wave_sync();
-#pragma unroll
-  for (int c = 0; c < C; c++)
-    if (ok[c]) val[bb[c] + jj[c]] = jj[c];
-  wave_sync();
+    L[c] = l;
+    V[c] = r * kWave + lane;
+  }
+  // V(k) = V(link(k)), by pointer jumping
   for (;;) {
     bool pending = false;
     int nl[C], nv[C];
 #pragma unroll
     for (int c = 0; c < C; c++) {
-      nl[c] = -1;
-      nv[c] = 0;
-      if (ok[c]) {
-        const int p = link[bb[c] + jj[c]];
-        nl[c] = p;
-        nv[c] = val[bb[c] + jj[c]];
-        if (p >= 0) {
-          const int pp = link[bb[c] + p];
-          if (pp < 0) { nv[c] = val[bb[c] + p]; nl[c] = -1; } else { nl[c] = pp; pending = true; }
-        }
+      const int c0 = c - c % R, p = L[c] < 0 ? 0 : L[c];
+      const int pl = chunk_fetch<R>(L + c0, p), pv = chunk_fetch<R>(V + c0, p);
+      nl[c] = L[c];
+      nv[c] = V[c];
+      if (L[c] >= 0) {
+        if (pl < 0) { nv[c] = pv; nl[c] = -1; } else { nl[c] = pl; pending = true; }
       }
     }
-    wave_sync();
 #pragma unroll
-    for (int c = 0; c < C; c++)
-      if (ok[c]) { link[bb[c] + jj[c]] = nl[c]; val[bb[c] + jj[c]] = nv[c]; }
-    wave_sync();
+    for (int c = 0; c < C; c++) { L[c] = nl[c]; V[c] = nv[c]; }
     if (!__any(pending)) break;
   }
-  // predecessor among steps with the same target, 64 steps (one round r) at a time
+  // a'[j] = a[P(j)]: V(j) for a fixed point, else V(pred(j)), or q if no earlier step targets q
+  int out[C];
 #pragma unroll
-  for (int r = 0; r < R; r++) {
+  for (int c = 0; c < C; c++) {
+    const int r = c % R, c0 = c - r, j = r * kWave + lane, qj = q[c];
+    int pr = -1;
 #pragma unroll
-    for (int c = r; c < C; c += R)
-      if (ok[c]) {
-        const int q = pd[c][jj[c]];
-        if (q != jj[c]) atomicOr(&cmask[bb[c] + q], 1ull << lane);
-      }
-    wave_sync();
-#pragma unroll
-    for (int c = r; c < C; c += R)
-      if (ok[c]) {
-        const int q = pd[c][jj[c]];
-        int Pv;
-        if (q == jj[c]) {
-          Pv = val[bb[c] + jj[c]];
-        } else {
-          const unsigned long long below = cmask[bb[c] + q] & ((1ull << lane) - 1ull);
-          const int pred = below ? r * kWave + 63 - __builtin_clzll(below) : last[bb[c] + q];
-          Pv = pred >= 0 ? val[bb[c] + pred] : q;
-        }
-        perm[bb[c] + jj[c]] = Pv;
-      }
-    wave_sync();
-#pragma unroll
-    for (int c = r; c < C; c += R)
-      if (ok[c]) {
-        const int q = pd[c][jj[c]];
-        if (q != jj[c]) { atomicMax(&last[bb[c] + q], jj[c]); cmask[bb[c] + q] = 0ull; }
-      }
-    wave_sync();
+    for (int s = 0; s <= r; s++) {
+      uint64_t mk = vc[c0 + s] & partner_bits_match<0, NB>(bc[c0 + s], (uint32_t)qj);
+      if (s == r) mk &= below;
+      if (mk) pr = s * kWave + 63 - __builtin_clzll(mk);
+    }
+    const int vp = chunk_fetch<R>(V + c0, pr < 0 ? 0 : pr);
+    const int Pv = qj == j ? V[c] : (pr >= 0 ? vp : qj);
+    out[c] = chunk_fetch<R>(a + c0, Pv);
   }
 #pragma unroll
-  for (int c = 0; c < C; c++)
-    if (ok[c]) {
-      const int m = c / R;
-      const float* st = wbase + 2 * (m / SD) * lhs_floats;
-      tmp[bb[c] + jj[c]] = __float_as_int(st[SD * perm[bb[c] + jj[c]] + (m % SD)]);
-    }
-  wave_sync();
-#pragma unroll
-  for (int c = 0; c < C; c++)
-    if (ok[c]) {
-      const int m = c / R;
-      float* st = wbase + 2 * (m / SD) * lhs_floats;
-      st[SD * jj[c] + (m % SD)] = __int_as_float(tmp[bb[c] + jj[c]]);
-    }
+  for (int c = 0; c < C; c++) {
+    const int m = m0 + c / R, e = (c % R) * kWave + lane;
+    if (c / R < M && e < nstrat) strat0[(m / SD) * slot_floats + SD * e + m % SD] = __int_as_float(out[c]);
+  }
   wave_sync();
 }
 
-template <int DIM>
-__device__ __forceinline__ void lhs_permute_all(float* wbase, int lhs_floats, int P, int nstrat, char* scratch,
-                                                int lane) {
-  const int R = (nstrat + kWave - 1) / kWave;  // lhs_all_fits: P (DIM - 1) R <= 4
-  if (R == 1) lhs_permute_all_r<DIM - 1, 1>(wbase, lhs_floats, P, nstrat, scratch, lane);
-  else if (R == 2) lhs_permute_all_r<DIM - 1, 2>(wbase, lhs_floats, P, nstrat, scratch, lane);
-  else lhs_permute_all_r<DIM - 1, 4>(wbase, lhs_floats, P, nstrat, scratch, lane);
+// Out of line: inlined, the element arrays cost the first-ball kernels registers across the
+// whole point loop (measured: within noise of inline for 2D, slower for 3D).
+template <int SD, int R, int MM>
+__device__ __attribute__((noinline)) void lhs_permute_reg(float* strat0, const int* part0, int slot_floats, int m0,
+                                                          int M, int nstrat, int lane) {
+  lhs_permute_reg_body<SD, R, MM>(strat0, part0, slot_floats, m0, M, nstrat, lane);
 }
 
 // A wave's stratified samples (every point slot, every dimension) are shuffled in one
-// lhs_permute_all pass when they fit its registers, instead of one lhs_permute per slot and dimension
+// lhs_permute_reg pass when they fit its registers, instead of one pass per slot and dimension
 __host__ __device__ constexpr bool lhs_all_fits(int n_pairs, int dim, int P) {
   // 3D only: a 2D wave with one point has one shuffle, and the out-of-line pass costs the 2D
   // first-ball kernel spills
@@ -3250,9 +3242,20 @@ __host__ __device__ constexpr bool lhs_all_fits(int n_pairs, int dim, int P) {
          P * (dim - 1) * ((2 * n_pairs + kWave - 1) / kWave == 3 ? 4 : (2 * n_pairs + kWave - 1) / kWave) <= 4;
 }
 
+// The jump constants of the stratified samples' first prm.lhs_jump_n draws, staged by the
+// first-ball kernel in its dynamic LDS after the per-wave regions (the host sizes the table:
+// at most kLhsJumpMax entries, none when it would cost the kernel a block per CU).  The draws
+// then wait on no global load -- a global one also waited, in order, for the next point's
+// coordinates and state the kernel prefetches just before (vmcnt counts loads in issue order).
+__device__ __forceinline__ uint64_t lhs_jump_state(const DevParams& prm, const unsigned long long* ljump, uint64_t s0,
+                                                   int k) {
+  if (k < prm.lhs_jump_n) return ljump[2 * k] * s0 + ljump[2 * k + 1];
+  return jump_state(prm, s0, k);
+}
+
 template <int DIM>
-__device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, float* strat, int* partner,
-                                          char* scratch, int lane, bool permute = true) {
+__device__ __forceinline__ void build_lhs(const DevParams& prm, const unsigned long long* ljump, int64_t gidx, float* strat,
+                                          int* partner, char* scratch, int lane, bool permute = true) {
   constexpr int sd = DIM - 1;
   const int nstrat = 2 * prm.n_pairs;
   const int nd = nstrat * sd;
@@ -3263,7 +3266,7 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   const float inv = 1.0f / (float)nstrat;
   for (int idx = lane; idx < nd; idx += kWave) {
     const int i = sd == 1 ? idx : idx / sd;
-    const uint32_t r = pcg_output(jump_state(prm, s0, idx));
+    const uint32_t r = pcg_output(lhs_jump_state(prm, ljump, s0, idx));
     const float u = bits_to_float((r >> 9) | 0x3f800000u) - 1.0f;
     strat[idx] = smin(((float)i + u) * inv, ome);
   }
@@ -3271,7 +3274,7 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
   for (int idx = lane; idx < nd; idx += kWave) {
     const int j = sd == 1 ? idx : idx % nstrat;
     const uint32_t bound = (uint32_t)(nstrat - j);
-    const uint32_t r = pcg_output(jump_state(prm, s0, nd + idx));
+    const uint32_t r = pcg_output(lhs_jump_state(prm, ljump, s0, nd + idx));
     // PCG's rejection threshold th = 2^32 mod bound < bound: only r < bound can fall below it
     if (r < bound) rej |= r < (~bound + 1u) % bound;
     partner[idx] = j + (int)(r % bound);
@@ -3287,7 +3290,14 @@ __device__ __forceinline__ void build_lhs(const DevParams& prm, int64_t gidx, fl
     }
     wave_sync();
   }
-  if (!permute) return;  // the caller shuffles (lhs_permute_all)
+  if (!permute) return;  // the caller shuffles (lhs_permute_reg over every slot)
+  if (nstrat <= 2 * kWave) {
+    for (int i = 0; i < sd; ++i) {
+      if (nstrat <= kWave) lhs_permute_reg<sd, 1, 1>(strat, partner, 0, i, 1, nstrat, lane);
+      else lhs_permute_reg<sd, 2, 1>(strat, partner, 0, i, 1, nstrat, lane);
+    }
+    return;
+  }
   if (nstrat <= 4 * kWave) {
     for (int i = 0; i < sd; ++i) lhs_permute(strat, partner, nstrat, sd, i, scratch, lane);
     return;
@@ -3709,17 +3719,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
+  const int npairs = prm.n_pairs;
+  // P points per wave (fb_points_per_wave): slot s holds its stratified samples and
+  // shuffle partners at wbase + 2 s lhs_floats; the rejection sampler's / shuffle's
+  // scratch follows the P slots; the block's staged jump constants follow the waves
+  const int P = fb_points_per_wave(npairs);
+  const int wave_floats = 2 * P * lhs_floats + (int)(fb_union_bytes(P * lhs_floats, 2 * npairs) / sizeof(float));
+  float* wbase = smem + wave * wave_floats;
+  unsigned long long* ljump = reinterpret_cast<unsigned long long*>(smem + (int)(blockDim.x / kWave) * wave_floats);
   stage_rej_jump(prm);
+  for (int i = threadIdx.x; i < 2 * prm.lhs_jump_n; i += blockDim.x) ljump[i] = prm.jump[i];
 #if WOS_DIAG
   if (threadIdx.x < D_NUM) s_diag[threadIdx.x] = 0u;
 #endif
   __syncthreads();
-  const int npairs = prm.n_pairs;
-  // P points per wave (fb_points_per_wave): slot s holds its stratified samples and
-  // shuffle partners at wbase + 2 s lhs_floats; the rejection sampler's / shuffle's
-  // scratch follows the P slots
-  const int P = fb_points_per_wave(npairs);
-  float* wbase = smem + wave * (2 * P * lhs_floats + (int)(fb_union_bytes(P * lhs_floats) / sizeof(float)));
   RejLDS* rejL = reinterpret_cast<RejLDS*>(wbase + 2 * P * lhs_floats);
   // this lane's point slot and pair (P == 1: all lanes serve the one point, pairs w0 + lane);
   // span = lanes per slot, so lane s * span is slot s's first lane (wave-uniform)
@@ -3799,11 +3812,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DIM == 2
     for (int s = 0; s < P; s++) {
       if (!all && !((em >> (s * span)) & 1ull)) continue;
       float* strat_s = wbase + 2 * s * lhs_floats;
-      build_lhs<DIM>(prm, base + (int64_t)(idx + (unsigned int)s) * stride, strat_s,
+      build_lhs<DIM>(prm, ljump, base + (int64_t)(idx + (unsigned int)s) * stride, strat_s,
                      reinterpret_cast<int*>(strat_s + lhs_floats), reinterpret_cast<char*>(rejL), lane, !all);
     }
     if constexpr (DIM == 3)
-      if (all) lhs_permute_all<DIM>(wbase, lhs_floats, P, 2 * npairs, reinterpret_cast<char*>(rejL), lane);
+      if (all) {
+        const int ns = 2 * npairs;
+        const int* part0 = reinterpret_cast<const int*>(wbase + lhs_floats);
+        if (ns <= kWave) lhs_permute_reg<DIM - 1, 1, 4>(wbase, part0, 2 * lhs_floats, 0, P * (DIM - 1), ns, lane);
+        else lhs_permute_reg<DIM - 1, 2, 2>(wbase, part0, 2 * lhs_floats, 0, P * (DIM - 1), ns, lane);
+      }
     DIAG_ADD(D_FB_LHS, t_fb1);
     DIAG_T0(t_fb2);
     // lanes without a point of their own (an unestimated slot, or beyond P slots) run the

@@ -219,7 +219,7 @@ hipError_t launch_fold(int dim, const DevParams& prm, const DevTasks& tk, int64_
 // P points' stratified samples and partners (fb_points_per_wave), then the sampler / shuffle scratch
 size_t first_ball_wave_lds_bytes(int lhs_floats, int n_pairs) {
   const int P = fb_points_per_wave(n_pairs);
-  return (size_t)2 * P * lhs_floats * sizeof(float) + fb_union_bytes(P * lhs_floats);
+  return (size_t)2 * P * lhs_floats * sizeof(float) + fb_union_bytes(P * lhs_floats, 2 * n_pairs);
 }
 
 int first_ball_points_per_wave(int n_pairs) { return fb_points_per_wave(n_pairs); }

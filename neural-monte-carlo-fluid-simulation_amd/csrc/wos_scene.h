@@ -137,6 +137,8 @@ struct DevParams {
   // per-point stratified samples in parallel.  n_jump entries.
   const uint64_t* jump;
   int32_t n_jump;
+  // entries of jump staged in the first-ball kernel's LDS (its stratified-sample draws; 0: none)
+  int32_t lhs_jump_n;
   // certain-reject bounds of the Yukawa rejection threshold by bin of s = mu R
   // (wos_host_scene.h rejection_bound_table), kRejTabBins floats; nullptr: none
   const float* rej_tab;
@@ -148,6 +150,8 @@ struct DevParams {
 constexpr int kMaxTaskQueues = 32;
 constexpr unsigned int kTaskQueueStride = 16;
 constexpr int kRejTabBins = 96;
+// most jump constants the first-ball kernel stages in LDS (16 B each)
+constexpr int kLhsJumpMax = 512;
 constexpr float kRejTabScale = 8.0f;
 
 // Walk-task workspace of one batch of points, SoA over T = n_points * wpp tasks

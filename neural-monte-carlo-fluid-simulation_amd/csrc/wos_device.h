@@ -1815,11 +1815,13 @@ __device__ __forceinline__ int rej_fast_decide3(float u, float r, float sqrtL, f
 // Round 2 measured the screen alone (every iteration still paid for the fast test whenever a
 // lane of its wave needed it); the own generation now screens its whole block first and runs
 // the fast test on the survivors only (tests/test_rejection_bounds.py checks the bound).
-__device__ __forceinline__ bool rej_xreject3(float u, float r, float sqrtL, float invNB, float xabs) {
-  const float z = r * sqrtL;
-  if (!(r > 0.0f) || !(z < 80.0f)) return false;
-  const float e = __builtin_amdgcn_exp2f(z * -1.44269502f);
-  return u > (r * e * invNB) * 1.001f + xabs;
+// The ball's constants come folded: kz = -sqrtL log2(e), kb = 1.001 invNB, so t = r kz and
+// 2^t = e^{-mu r} up to the rounding of the folded product (a few ulp of t: <= 3e-5 relative
+// in e below mu r = 80, far inside the margin).  t > -115 keeps mu r < 79.7.
+__device__ __forceinline__ bool rej_xreject3(float u, float r, float kz, float kb, float xabs) {
+  const float t = r * kz;
+  if (!(r > 0.0f) || !(t > -115.0f)) return false;
+  return u > __builtin_fmaf(r * kb, __builtin_amdgcn_exp2f(t), xabs);
 }
 
 // exact 3D Yukawa test of one iteration with an owner's ball constants: the same
@@ -1956,14 +1958,17 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         // order through the fast and the exact test, the first accept wins.  The wave pays
         // phase B's tests once per survivor round, not once per iteration.
         const float rho0 = g.A0 / g.A1, xabs = 1e-6f * g.R * invNB0;
+        const float kz = g.sqrtLambda * -1.44269502f, kb = invNB0 * 1.001f;
         uint32_t surv = 0u;
+        // the block's states in stream order, two draws per step (no jump-table reads)
+        uint64_t st = s0;
 #pragma unroll 4
         for (int b = 0; b < kRejOwnD<DIM, FB>; b++) {
-          const uint64_t st = rej_state(prm, s0, b);
           const float u = draw_float(st);
           DIAG_LANE(D_RITEMS);
-          if (!(u > qb0) && !rej_xreject3(u, draw_float(st * kPcgMult + kPcgInc) * g.R, g.sqrtLambda, invNB0, xabs))
+          if (!(u > qb0) && !rej_xreject3(u, draw_float(st * kPcgMult + kPcgInc) * g.R, kz, kb, xabs))
             surv |= 1u << b;
+          st = st * kPcgMult2 + kPcgInc2;
         }
         for (uint32_t m = surv; m != 0u; m &= m - 1u) {
           const int b = __builtin_ctz(m);
@@ -1975,9 +1980,9 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
           if (dcs == 1) { jacc = b; done = true; break; }
         }
       } else {
+      uint64_t st = s0;  // the block's states in stream order (no jump-table reads)
 #pragma unroll 4
       for (int b = 0; b < kRejOwnD<DIM, FB>; b++) {
-        const uint64_t st = rej_state(prm, s0, b);
         const float u = draw_float(st);
         int dcs = 0;
         DIAG_LANE(D_RITEMS);
@@ -1993,6 +1998,7 @@ __device__ __forceinline__ void sample_volume_wave(const DevParams& prm, bool ac
         }
         if (dcs == 1) acc |= 1u << b;
         else if (dcs < 0) und |= 1u << b;
+        st = st * kPcgMult2 + kPcgInc2;
       }
       for (uint32_t m = acc | und; m != 0u; m &= m - 1u) {
         const int b = __builtin_ctz(m);

@@ -163,20 +163,24 @@ def test_tabulated_bound_dominates_exact_threshold(rej_table, dim, lam):
 
 
 def _xbound3(R, lam, xs, inv_nb):
-    """rej_xreject3's bound r e^{-mu r} invNB * 1.001 + 1e-6 R invNB (exp in double here; the
-    kernel's hardware exp2 is within a few ulp of it, far inside the 0.1 % margin)"""
+    """rej_xreject3's bound fma(r kb, 2^(r kz), xabs) with kz = -sqrtL log2(e), kb = 1.001 invNB,
+    xabs = 1e-6 R invNB, in the kernel's float order (2^t in double here; the kernel's hardware
+    exp2 is within a few ulp of it, far inside the 0.1 % margin).  Returns the bound and t."""
     sl = f32(np.sqrt(f32(lam)))
+    kz = f32(sl * f32(-1.44269502))
+    kb = f32(f32(inv_nb) * f32(1.001))
+    xabs = f32(f32(f32(1e-6) * f32(R)) * f32(inv_nb))
     r = (xs * R).astype(np.float32)
-    z = (r * sl).astype(np.float32)
-    e = np.exp(-z.astype(np.float64))
-    return (r * e * float(inv_nb)) * 1.001 + 1e-6 * float(R) * float(inv_nb)
+    t = (r * kz).astype(np.float32)
+    e = np.exp2(t.astype(np.float64))
+    return (r * kb).astype(np.float64) * e + float(xabs), t
 
 
 @pytest.mark.parametrize("lam", [1e-2, 50.0, 350.0, 2000.0, 1e4])
 def test_radius_bound_3d_dominates_exact_threshold(lam):
     """the radius-dependent certain reject of the 3D own generation (rej_xreject3) is above the
     exact threshold at every radius draw, and rejects most of what the exact test rejects.
-    The kernel applies it to every 3D Yukawa ball with mu R < 80: the sweep covers small and
+    The kernel applies it to every 3D Yukawa ball with mu r < 79.7: the sweep covers small and
     large lambda, balls up to mu R = 79.9, and radius draws r -> R, where the exact path's
     float subtraction e^{-mu r} - A0 sinh(mu r) / A1 cancels"""
     rng = np.random.default_rng(23)
@@ -192,9 +196,8 @@ def test_radius_bound_3d_dominates_exact_threshold(lam):
         T, q, (muR, inv_nb) = _thresholds_3d(f32(R), f32(lam), xs)
         if not (inv_nb > 0 and np.isfinite(inv_nb)):
             continue
-        z = (xs * R).astype(np.float32) * f32(np.sqrt(f32(lam)))
-        B = _xbound3(f32(R), lam, xs, inv_nb)
-        ok = np.isfinite(T) & (z < 80)
+        B, t = _xbound3(f32(R), lam, xs, inv_nb)
+        ok = np.isfinite(T) & (t > -115.0)
         assert (T[ok] <= B[ok]).all(), (lam, float(R), float((T - B)[ok].max()))
         # share of the reject interval (T, min(q, 1)) of u that the screen resolves
         top = min(float(q), 1.0)

@@ -219,6 +219,10 @@ __global__ void k_issue(float* out, int n, float seed, unsigned long long* clk) 
       if (OP == 11) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(q[c]));
       if (OP == 12) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(q[c]) : "v"(ub), "v"(ub) : "s0", "s1");
       if (OP == 13) asm volatile("v_add_f32 %0, %1, %0" : "+v"(a[c]) : "v"(fb));
+      // packed f32 (two lanes' worth per lane): a register pair per operand
+      if (OP == 14) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(d[c]) : "v"(db), "v"(dc));
+      if (OP == 15) asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(d[c]) : "v"(db));
+      if (OP == 16) asm volatile("v_pk_add_f32 %0, %1, %0" : "+v"(d[c]) : "v"(db));
     }
   }
   float acc = 0.0f;
@@ -238,22 +242,23 @@ int main3() {
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const char* names[] = {"v_fma_f32", "v_add_u32", "v_cndmask_b32", "v_fma_f64", "v_rcp_f64", "v_exp_f32",
                          "v_mul_lo_u32", "v_cvt_f64_f32", "v_mov_b32", "v_add_f64", "v_mul_f64",
-                         "v_lshlrev_b64", "v_mad_u64_u32", "v_add_f32"};
+                         "v_lshlrev_b64", "v_mad_u64_u32", "v_add_f32", "v_pk_fma_f32", "v_pk_mul_f32",
+                         "v_pk_add_f32"};
   const size_t lds = 96 * 1024;  // > half of a CU's 160 KB: one workgroup per CU
   const size_t lds8 = 72 * 1024;  // 8 waves/SIMD: two 1024-thread workgroups per CU
 #define A(o) hipFuncSetAttribute((const void*)k_issue<o>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7) A(8) A(9) A(10) A(11) A(12) A(13)
+  A(0) A(1) A(2) A(3) A(4) A(5) A(6) A(7) A(8) A(9) A(10) A(11) A(12) A(13) A(14) A(15) A(16)
 #undef A
   printf("{\"cus\": %d, \"clock_ghz_nominal\": 2.4, \"chains\": %d, \"results\": [\n", cus, kIssueChains);
   bool first = true;
-  for (int op = 0; op < 14; op++) {
+  for (int op = 0; op < 17; op++) {
     for (int w : {1, 2, 4, 8}) {
       const int n = 4096;
       auto launch = [&]() {
         switch (op) {
 #define K(o) case o: hipLaunchKernelGGL(k_issue<o>, dim3(w > 4 ? 2 * cus : cus), dim3(w > 4 ? 1024 : 256 * w), \
                                         w > 4 ? lds8 : lds, 0, d, n, 1.0f, dclk); break;
-          K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13)
+          K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15) K(16)
 #undef K
         }
       };
